@@ -1,0 +1,117 @@
+"""ctypes binding of liblamellar_gpu_ops.so (include/lamellar_gpu_ops.h).
+
+This is the same binding a Rust maintainer would write with ``extern "C"``
+(see INTEGRATION.md); Python uses it for the host-side mirror of the
+reference's op-builder API, the tests and the benchmark.
+
+There is no fallback: if the HIP library is missing or fails to load, importing
+the package's device path raises :class:`LamellarLibraryError`.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from ctypes import (POINTER, Structure, c_char_p, c_int, c_uint8, c_uint32,
+                    c_uint64, c_void_p)
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("LAMELLAR_GPU_OPS_LIB",
+                          os.path.join(_HERE, "liblamellar_gpu_ops.so"))
+
+
+class LamellarLibraryError(RuntimeError):
+    pass
+
+
+class lmr_layout_t(Structure):
+    """UnsafeArrayInner index-math fields (src/array/unsafe.rs:107-116)."""
+    _fields_ = [
+        ("distribution", c_uint32),
+        ("num_pes", c_uint32),
+        ("my_pe", c_uint32),
+        ("sub", c_uint32),
+        ("orig_elem_per_pe", c_uint64),
+        ("orig_remaining_elems", c_uint64),
+        ("offset", c_uint64),
+        ("size", c_uint64),
+    ]
+
+    def as_tuple(self):
+        return tuple(getattr(self, f) for f, _ in self._fields_)
+
+
+class lmr_apply_desc_t(Structure):
+    _fields_ = [
+        ("shard", c_void_p),
+        ("shard_len", c_uint64),
+        ("kind", c_uint32),
+        ("dtype", c_uint32),
+        ("op", c_uint32),
+        ("strategy", c_uint32),
+        ("cmp_bits", c_uint64),
+        ("eps_bits", c_uint64),
+    ]
+
+
+# name -> (restype, argtypes). Every symbol of include/lamellar_gpu_ops.h.
+SIGNATURES = {
+    "lmr_abi_version": (c_uint32, []),
+    "lmr_status_string": (c_char_p, [c_int]),
+    "lmr_ctx_create": (c_int, [c_int, POINTER(c_void_p)]),
+    "lmr_ctx_destroy": (c_int, [c_void_p]),
+    "lmr_ctx_reserve": (c_int, [c_void_p, c_uint64]),
+    "lmr_ctx_error": (c_int, [c_void_p, c_void_p, POINTER(c_uint32), c_int]),
+    "lmr_ctx_profile": (c_int, [c_void_p, c_int]),
+    "lmr_ctx_profile_read": (c_int, [c_void_p, c_void_p, POINTER(ctypes.c_double), POINTER(c_uint64), c_int]),
+    "lmr_layout_new": (c_int, [POINTER(lmr_layout_t), c_uint64, c_uint32, c_uint32, c_uint32]),
+    "lmr_layout_sub": (c_int, [POINTER(lmr_layout_t), c_uint64, c_uint64, POINTER(lmr_layout_t)]),
+    "lmr_pe_and_offset": (c_int, [POINTER(lmr_layout_t), c_uint64, POINTER(c_uint64), POINTER(c_uint64)]),
+    "lmr_num_elems_pe": (c_uint64, [POINTER(lmr_layout_t), c_uint32]),
+    "lmr_local_slice_start": (c_uint64, [POINTER(lmr_layout_t), c_uint32]),
+    "lmr_index_size": (c_uint32, [POINTER(lmr_layout_t)]),
+    "lmr_record_bytes": (c_uint32, [c_uint32, c_uint32]),
+    "lmr_record_val_offset": (c_uint32, [c_uint32, c_uint32]),
+    "lmr_op_ret_kind": (c_uint32, [c_uint32]),
+    "lmr_op_supported": (c_int, [c_uint32, c_uint32, c_uint32]),
+    "lmr_pack": (c_int, [c_void_p, POINTER(lmr_layout_t), c_void_p, c_uint64, c_void_p, c_uint32,
+                         c_uint32, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
+    "lmr_apply_mvmi": (c_int, [c_void_p, POINTER(lmr_apply_desc_t), c_void_p, c_uint64, c_uint32,
+                               c_void_p, c_void_p, c_void_p]),
+    "lmr_apply_svmi": (c_int, [c_void_p, POINTER(lmr_apply_desc_t), c_void_p, c_void_p, c_uint64,
+                               c_uint32, c_void_p, c_void_p, c_void_p]),
+    "lmr_apply_mvsi": (c_int, [c_void_p, POINTER(lmr_apply_desc_t), c_void_p, c_uint64, c_uint64,
+                               c_void_p, c_void_p, c_void_p]),
+    "lmr_apply_soa": (c_int, [c_void_p, POINTER(lmr_apply_desc_t), c_void_p, c_uint32, c_void_p,
+                              c_void_p, c_uint64, c_void_p, c_void_p, c_void_p]),
+    "lmr_scatter_results": (c_int, [c_void_p, c_void_p, c_uint64, c_uint32, c_void_p, c_void_p,
+                                    c_void_p, c_void_p]),
+}
+
+STAGES = ["direct", "mvsi", "bin_count", "scan", "bin_scatter", "tile_apply", "pack",
+          "scatter_results"]
+
+_lib = None
+
+
+def lib():
+    """Load (once) and return the HIP library; raise loudly if unavailable."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise LamellarLibraryError(
+                f"liblamellar_gpu_ops.so not found at {LIB_PATH}; build it with "
+                f"`python __graft_entry__.py build` (hipcc --offload-arch=gfx950)")
+        try:
+            l = ctypes.CDLL(LIB_PATH)
+        except OSError as e:  # pragma: no cover - environment specific
+            raise LamellarLibraryError(f"failed to load {LIB_PATH}: {e}") from e
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(l, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = l
+    return _lib
+
+
+def status_string(st: int) -> str:
+    return lib().lmr_status_string(st).decode()

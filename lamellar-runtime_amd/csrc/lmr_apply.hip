@@ -1,0 +1,415 @@
+// lmr_apply.hip — gfx950 apply kernels for batched element ops.
+//
+// Replaces the element loops of the reference's generated AM exec bodies
+// (impl/src/array_ops.rs:203-250 loop shapes, :863-1408 bodies):
+//   * k_apply_direct : one device-scope atomic RMW per record (any op/type);
+//                      the path for small op buffers (one AM of ~6250 records).
+//   * k_apply_mvsi   : many values at one index, applied in buffer order as
+//                      one atomic block (array_ops.rs:235-250: lock once, loop).
+//   * tiled path     : k_bin_count -> scan -> k_bin_scatter -> k_tile_apply.
+//                      Records are counting-sorted into 64 KiB shard tiles; one
+//                      workgroup owns a tile, stages it in LDS, applies every
+//                      record with LDS atomics (ds_add_u64, ds_cmpst_b64, ...)
+//                      and writes the tile back once: random 8-B HBM RMWs become
+//                      streaming reads of the binned records plus one coalesced
+//                      read+write of the shard.
+#include "lmr_internal.hpp"
+#include "lmr_device.hpp"
+
+namespace lmr {
+
+template <typename T>
+__device__ __forceinline__ T load_val(const ApplyArgs& a, uint64_t k) {
+    if (a.val) return *reinterpret_cast<const T*>(a.val + k * a.val_stride);
+    return from_bits<T>(typename bits_of<T>::U(a.val_bits));
+}
+
+template <int IW>
+__device__ __forceinline__ uint64_t load_idx(const uint8_t* base, uint64_t stride, uint64_t k) {
+    using I = typename idx_t<IW>::I;
+    return uint64_t(*reinterpret_cast<const I*>(base + k * stride));
+}
+
+// ------------------------------------------------------------------ direct
+template <typename T, int IW>
+__global__ __launch_bounds__(256) void k_apply_direct(ApplyArgs a) {
+    using U = typename bits_of<T>::U;
+    T* shard = reinterpret_cast<T*>(a.shard);
+    const T cmp = from_bits<T>(U(a.cmp_bits)), eps = from_bits<T>(U(a.eps_bits));
+    const uint64_t stride = uint64_t(gridDim.x) * blockDim.x;
+    for (uint64_t k = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x; k < a.n; k += stride) {
+        uint64_t idx = load_idx<IW>(a.idx, a.idx_stride, k);
+        T v = load_val<T>(a, k);
+        if (idx >= a.shard_len) {
+            raise_err(a.err, LMR_ERRBIT_OOB);
+            continue;
+        }
+        uint8_t ok = 0;
+        T r = rmw_global<T>(shard + idx, a.op, a.kind, v, cmp, eps, ok, a.err);
+        if (a.ret != LMR_RET_NONE) reinterpret_cast<T*>(a.results)[k] = r;
+        if (a.ret == LMR_RET_RESULT) a.ok[k] = ok;
+    }
+}
+
+// ------------------------------------------------------------------ MVSI
+// One thread walks the values in order on a register copy of the element and
+// publishes the final value with one CAS (retrying the whole block if another
+// kernel raced on the element): the block of values is applied atomically, as
+// under the reference's per-AM lock.
+template <typename T>
+__global__ __launch_bounds__(64) void k_apply_mvsi(ApplyArgs a, uint64_t index) {
+    using U = typename bits_of<T>::U;
+    if (threadIdx.x != 0 || a.n == 0) return;
+    if (index >= a.shard_len) { raise_err(a.err, LMR_ERRBIT_OOB); return; }
+    const T cmp = from_bits<T>(U(a.cmp_bits)), eps = from_bits<T>(U(a.eps_bits));
+    T* p = reinterpret_cast<T*>(a.shard) + index;
+    const bool ret = a.ret != LMR_RET_NONE;
+    if constexpr (sizeof(T) >= 4) {
+        U cur = __hip_atomic_load(reinterpret_cast<U*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        while (true) {
+            T s = from_bits<T>(cur);
+            uint32_t errs = 0;
+            for (uint64_t k = 0; k < a.n; k++) {
+                T v = load_val<T>(a, k), nw, r;
+                uint8_t ok = 0;
+                uint32_t eb = 0;
+                if (op_math<T>(a.op, a.kind, s, v, cmp, eps, nw, r, ok, eb)) s = nw;
+                else errs |= eb;
+                if (ret) reinterpret_cast<T*>(a.results)[k] = r;
+                if (a.ret == LMR_RET_RESULT) a.ok[k] = ok;
+            }
+            U expected = cur;
+            if (to_bits(s) == cur ||
+                __hip_atomic_compare_exchange_strong(reinterpret_cast<U*>(p), &expected, to_bits(s),
+                                                     __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                     __HIP_MEMORY_SCOPE_AGENT)) {
+                if (errs) raise_err(a.err, errs);
+                return;
+            }
+            cur = expected;
+        }
+    } else {
+        uintptr_t ad = reinterpret_cast<uintptr_t>(p);
+        uint32_t* wp = reinterpret_cast<uint32_t*>(ad & ~uintptr_t(3));
+        const unsigned sh = unsigned(ad & 3) * 8;
+        const uint32_t mask = uint32_t((1u << (8 * sizeof(T))) - 1u) << sh;
+        uint32_t cur = __hip_atomic_load(wp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        while (true) {
+            T s = T(U((cur & mask) >> sh));
+            uint32_t errs = 0;
+            for (uint64_t k = 0; k < a.n; k++) {
+                T v = load_val<T>(a, k), nw, r;
+                uint8_t ok = 0;
+                uint32_t eb = 0;
+                if (op_math<T>(a.op, a.kind, s, v, cmp, eps, nw, r, ok, eb)) s = nw;
+                else errs |= eb;
+                if (ret) reinterpret_cast<T*>(a.results)[k] = r;
+                if (a.ret == LMR_RET_RESULT) a.ok[k] = ok;
+            }
+            uint32_t nb = (cur & ~mask) | (uint32_t(U(s)) << sh);
+            uint32_t expected = cur;
+            if (nb == cur ||
+                __hip_atomic_compare_exchange_strong(wp, &expected, nb, __ATOMIC_RELAXED,
+                                                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+                if (errs) raise_err(a.err, errs);
+                return;
+            }
+            cur = expected;
+        }
+    }
+}
+
+// ------------------------------------------------------------------ tiled
+struct BinArgs {
+    const uint8_t* idx;
+    uint64_t idx_stride;
+    const uint8_t* val;
+    uint64_t val_stride;
+    uint64_t n;
+    uint64_t shard_len;
+    uint64_t chunk;        // records per block
+    int tile_shift;
+    uint32_t num_tiles;
+    uint32_t G;
+    uint32_t* counts;      // [num_tiles * G], tile-major
+    uint16_t* bin_lidx;
+    uint8_t* bin_val;
+    uint32_t* bin_pos;     // null when nothing is returned
+    uint32_t* err;
+};
+
+template <int IW>
+__global__ __launch_bounds__(kBinBlock) void k_bin_count(BinArgs b) {
+    extern __shared__ uint32_t hist[];
+    for (uint32_t t = threadIdx.x; t < b.num_tiles; t += blockDim.x) hist[t] = 0;
+    __syncthreads();
+    const uint64_t lo = uint64_t(blockIdx.x) * b.chunk;
+    const uint64_t hi = min(lo + b.chunk, b.n);
+    bool oob = false;
+    for (uint64_t k = lo + threadIdx.x; k < hi; k += blockDim.x) {
+        uint64_t idx = load_idx<IW>(b.idx, b.idx_stride, k);
+        if (idx >= b.shard_len) { oob = true; continue; }
+        atomicAdd(&hist[uint32_t(idx >> b.tile_shift)], 1u);
+    }
+    if (oob) raise_err(b.err, LMR_ERRBIT_OOB);
+    __syncthreads();
+    for (uint32_t t = threadIdx.x; t < b.num_tiles; t += blockDim.x)
+        b.counts[uint64_t(t) * b.G + blockIdx.x] = hist[t];
+}
+
+template <int IW, int VB>
+__global__ __launch_bounds__(kBinBlock) void k_bin_scatter(BinArgs b) {
+    using V = typename idx_t<VB>::I;   // raw value bits of VB bytes
+    extern __shared__ uint32_t cursor[];
+    for (uint32_t t = threadIdx.x; t < b.num_tiles; t += blockDim.x)
+        cursor[t] = b.counts[uint64_t(t) * b.G + blockIdx.x];
+    __syncthreads();
+    const uint64_t lo = uint64_t(blockIdx.x) * b.chunk;
+    const uint64_t hi = min(lo + b.chunk, b.n);
+    const uint32_t lmask = (1u << b.tile_shift) - 1u;
+    for (uint64_t k = lo + threadIdx.x; k < hi; k += blockDim.x) {
+        uint64_t idx = load_idx<IW>(b.idx, b.idx_stride, k);
+        if (idx >= b.shard_len) continue;
+        uint32_t pos = atomicAdd(&cursor[uint32_t(idx >> b.tile_shift)], 1u);
+        b.bin_lidx[pos] = uint16_t(uint32_t(idx) & lmask);
+        if (b.val) reinterpret_cast<V*>(b.bin_val)[pos] = *reinterpret_cast<const V*>(b.val + k * b.val_stride);
+        if (b.bin_pos) b.bin_pos[pos] = uint32_t(k);
+    }
+}
+
+__global__ void k_tile_starts(const uint32_t* counts, uint32_t num_tiles, uint32_t G,
+                              const uint32_t* total, uint32_t* tile_start) {
+    uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t < num_tiles) tile_start[t] = counts[uint64_t(t) * G];
+    if (t == num_tiles) tile_start[t] = *total;
+}
+
+struct TileArgs {
+    void* shard;
+    uint64_t shard_len;
+    int tile_shift;
+    int kind;
+    int op;
+    int ret;
+    uint64_t cmp_bits;
+    uint64_t eps_bits;
+    uint64_t val_bits;       // scalar value (SVMI)
+    bool scalar;
+    const uint32_t* tile_start;
+    const uint16_t* bin_lidx;
+    const uint8_t* bin_val;
+    const uint32_t* bin_pos;
+    void* results;
+    uint8_t* ok;
+    uint32_t* err;
+};
+
+// OPT >= 0 fixes the op at compile time (hot paths); -1 reads it from the args.
+template <typename T, int OPT>
+__global__ __launch_bounds__(1024) void k_tile_apply(TileArgs a) {
+    using U = typename bits_of<T>::U;
+    using W = typename word_of<T>::W;
+    extern __shared__ __align__(16) uint8_t lds_raw[];
+    W* tile = reinterpret_cast<W*>(lds_raw);
+    const int op = OPT >= 0 ? OPT : a.op;
+    const uint32_t t = blockIdx.x;
+    const uint64_t base = uint64_t(t) << a.tile_shift;
+    const uint32_t len = uint32_t(min(uint64_t(1) << a.tile_shift, a.shard_len - base));
+    T* shard = reinterpret_cast<T*>(a.shard) + base;
+    const uint32_t r0 = a.tile_start[t], r1 = a.tile_start[t + 1];
+    if (r0 == r1) return;   // untouched tile: nothing to read or write
+    for (uint32_t e = threadIdx.x; e < len; e += blockDim.x) tile[e] = W(to_bits(shard[e]));
+    __syncthreads();
+    const T cmp = from_bits<T>(U(a.cmp_bits)), eps = from_bits<T>(U(a.eps_bits));
+    const T sv = from_bits<T>(U(a.val_bits));
+    const int ret = a.ret;
+    for (uint32_t r = r0 + threadIdx.x; r < r1; r += blockDim.x) {
+        uint32_t l = a.bin_lidx[r];
+        T v = a.scalar ? sv : reinterpret_cast<const T*>(a.bin_val)[r];
+        uint8_t ok = 0;
+        T old = rmw_lds<T>(tile + l, op, a.kind, v, cmp, eps, ok, a.err);
+        if (ret != LMR_RET_NONE) {
+            uint32_t p = a.bin_pos[r];
+            reinterpret_cast<T*>(a.results)[p] = old;
+            if (ret == LMR_RET_RESULT) a.ok[p] = ok;
+        }
+    }
+    __syncthreads();
+    if (op_is_read(op)) return;
+    for (uint32_t e = threadIdx.x; e < len; e += blockDim.x) {
+        if constexpr (sizeof(T) >= 4) shard[e] = from_bits<T>(U(tile[e]));
+        else shard[e] = T(U(tile[e]));
+    }
+}
+
+// ------------------------------------------------------------------ dispatch
+template <typename F>
+static hipError_t dispatch_dtype(int dtype, F&& f) {
+    switch (dtype) {
+    case LMR_U8: return f(uint8_t{});
+    case LMR_U16: return f(uint16_t{});
+    case LMR_U32: return f(uint32_t{});
+    case LMR_U64: return f(uint64_t{});
+    case LMR_I8: return f(int8_t{});
+    case LMR_I16: return f(int16_t{});
+    case LMR_I32: return f(int32_t{});
+    case LMR_I64: return f(int64_t{});
+    case LMR_F32: return f(float{});
+    case LMR_F64: return f(double{});
+    default: return hipErrorInvalidValue;
+    }
+}
+
+template <typename F>
+static hipError_t dispatch_iw(int iw, F&& f) {
+    switch (iw) {
+    case 1: return f(std::integral_constant<int, 1>{});
+    case 2: return f(std::integral_constant<int, 2>{});
+    case 4: return f(std::integral_constant<int, 4>{});
+    case 8: return f(std::integral_constant<int, 8>{});
+    default: return hipErrorInvalidValue;
+    }
+}
+
+static unsigned grid_for(uint64_t n, unsigned block, unsigned cap) {
+    uint64_t g = (n + block - 1) / block;
+    if (g > cap) g = cap;
+    return unsigned(g ? g : 1);
+}
+
+hipError_t launch_apply_direct(int dtype, int index_size, const ApplyArgs& a, hipStream_t s) {
+    if (a.n == 0) return hipSuccess;
+    ProfScope ps(a.prof, LMR_STAGE_DIRECT, s);
+    return dispatch_dtype(dtype, [&](auto tag) {
+        using T = decltype(tag);
+        return dispatch_iw(index_size, [&](auto iw) {
+            hipLaunchKernelGGL((k_apply_direct<T, decltype(iw)::value>),
+                               dim3(grid_for(a.n, 256, 256 * 32)), dim3(256), 0, s, a);
+            return hipGetLastError();
+        });
+    });
+}
+
+hipError_t launch_apply_mvsi(int dtype, const ApplyArgs& a, uint64_t index, hipStream_t s) {
+    if (a.n == 0) return hipSuccess;
+    ProfScope ps(a.prof, LMR_STAGE_MVSI, s);
+    return dispatch_dtype(dtype, [&](auto tag) {
+        using T = decltype(tag);
+        hipLaunchKernelGGL((k_apply_mvsi<T>), dim3(1), dim3(64), 0, s, a, index);
+        return hipGetLastError();
+    });
+}
+
+static int tile_shift_for(int dtype) {
+    int wb = dtype_bytes(dtype) < 4 ? 4 : dtype_bytes(dtype);
+    int len = kTileBytes / wb;
+    int sh = 0;
+    while ((1 << (sh + 1)) <= len) sh++;
+    return sh;
+}
+
+bool tiled_supported(int dtype, uint64_t shard_len) {
+    uint64_t tiles = (shard_len + (uint64_t(1) << tile_shift_for(dtype)) - 1) >> tile_shift_for(dtype);
+    return tiles >= 1 && tiles <= uint64_t(kMaxTiles);
+}
+
+size_t tiled_ws_bytes(uint64_t cap) {
+    size_t b = 0;
+    auto al = [](size_t x) { return (x + 255) & ~size_t(255); };
+    b += al(size_t(kMaxTiles) * kMaxBinBlocks * 4);                         // counts
+    b += al((size_t(kMaxTiles) * kMaxBinBlocks + kScanItems - 1) / kScanItems * 4);  // partials
+    b += al((size_t(kMaxTiles) + 1) * 4);                                   // tile_start
+    b += al(cap * 2) + al(cap * 8) + al(cap * 4) + al(4);
+    return b;
+}
+
+TiledWs carve_tiled_ws(uint8_t* base, uint64_t cap) {
+    auto al = [](size_t x) { return (x + 255) & ~size_t(255); };
+    TiledWs w;
+    uint8_t* p = base;
+    w.counts = reinterpret_cast<uint32_t*>(p); p += al(size_t(kMaxTiles) * kMaxBinBlocks * 4);
+    w.partials = reinterpret_cast<uint32_t*>(p);
+    p += al((size_t(kMaxTiles) * kMaxBinBlocks + kScanItems - 1) / kScanItems * 4);
+    w.tile_start = reinterpret_cast<uint32_t*>(p); p += al((size_t(kMaxTiles) + 1) * 4);
+    w.bin_lidx = reinterpret_cast<uint16_t*>(p); p += al(cap * 2);
+    w.bin_val = p; p += al(cap * 8);
+    w.bin_pos = reinterpret_cast<uint32_t*>(p); p += al(cap * 4);
+    w.total = reinterpret_cast<uint32_t*>(p);
+    return w;
+}
+
+// One tiled piece: a.n <= workspace capacity, a.n < 2^32.
+hipError_t launch_apply_tiled(int dtype, int index_size, const ApplyArgs& a, const TiledWs& w,
+                              hipStream_t s) {
+    if (a.n == 0) return hipSuccess;
+    const int shift = tile_shift_for(dtype);
+    const uint64_t num_tiles = (a.shard_len + (uint64_t(1) << shift) - 1) >> shift;
+    if (num_tiles == 0 || num_tiles > uint64_t(kMaxTiles)) return hipErrorNotSupported;
+    const int vb = dtype_bytes(dtype);
+    // G blocks: >= 64K records each, at most kMaxBinBlocks
+    uint64_t G = (a.n + 65535) / 65536;
+    if (G > uint64_t(kMaxBinBlocks)) G = kMaxBinBlocks;
+    if (G < 1) G = 1;
+    BinArgs b;
+    b.idx = a.idx; b.idx_stride = a.idx_stride;
+    b.val = a.val; b.val_stride = a.val_stride;
+    b.n = a.n; b.shard_len = a.shard_len;
+    b.chunk = (a.n + G - 1) / G;
+    b.tile_shift = shift; b.num_tiles = uint32_t(num_tiles); b.G = uint32_t(G);
+    b.counts = w.counts; b.bin_lidx = w.bin_lidx; b.bin_val = w.bin_val;
+    b.bin_pos = (a.ret != LMR_RET_NONE) ? w.bin_pos : nullptr;
+    b.err = a.err;
+    const size_t hist_lds = size_t(num_tiles) * 4;
+    hipError_t e;
+    {
+    ProfScope ps(a.prof, LMR_STAGE_BIN_COUNT, s);
+    e = dispatch_iw(index_size, [&](auto iw) {
+        hipLaunchKernelGGL((k_bin_count<decltype(iw)::value>), dim3(unsigned(G)), dim3(kBinBlock),
+                           hist_lds, s, b);
+        return hipGetLastError();
+    });
+    }
+    if (e != hipSuccess) return e;
+    {
+    ProfScope ps(a.prof, LMR_STAGE_SCAN, s);
+    e = scan_exclusive_u32(w.counts, num_tiles * G, w.partials, w.total, s);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_tile_starts, dim3(unsigned((num_tiles + 1 + 255) / 256)), dim3(256), 0, s,
+                       w.counts, uint32_t(num_tiles), uint32_t(G), w.total, w.tile_start);
+    }
+    {
+    ProfScope ps(a.prof, LMR_STAGE_BIN_SCATTER, s);
+    e = dispatch_iw(index_size, [&](auto iw) {
+        constexpr int IW = decltype(iw)::value;
+        switch (vb) {
+        case 1: hipLaunchKernelGGL((k_bin_scatter<IW, 1>), dim3(unsigned(G)), dim3(kBinBlock), hist_lds, s, b); break;
+        case 2: hipLaunchKernelGGL((k_bin_scatter<IW, 2>), dim3(unsigned(G)), dim3(kBinBlock), hist_lds, s, b); break;
+        case 4: hipLaunchKernelGGL((k_bin_scatter<IW, 4>), dim3(unsigned(G)), dim3(kBinBlock), hist_lds, s, b); break;
+        default: hipLaunchKernelGGL((k_bin_scatter<IW, 8>), dim3(unsigned(G)), dim3(kBinBlock), hist_lds, s, b); break;
+        }
+        return hipGetLastError();
+    });
+    }
+    if (e != hipSuccess) return e;
+    TileArgs t;
+    t.shard = a.shard; t.shard_len = a.shard_len; t.tile_shift = shift;
+    t.kind = a.kind; t.op = a.op; t.ret = a.ret;
+    t.cmp_bits = a.cmp_bits; t.eps_bits = a.eps_bits; t.val_bits = a.val_bits;
+    t.scalar = (a.val == nullptr);
+    t.tile_start = w.tile_start; t.bin_lidx = w.bin_lidx; t.bin_val = w.bin_val;
+    t.bin_pos = w.bin_pos; t.results = a.results; t.ok = a.ok; t.err = a.err;
+    const size_t tile_lds = size_t(kTileBytes);
+    ProfScope ps(a.prof, LMR_STAGE_TILE_APPLY, s);
+    return dispatch_dtype(dtype, [&](auto tag) {
+        using T = decltype(tag);
+        if (a.op == LMR_OP_ADD)
+            hipLaunchKernelGGL((k_tile_apply<T, LMR_OP_ADD>), dim3(unsigned(num_tiles)), dim3(1024), tile_lds, s, t);
+        else if (a.op == LMR_OP_FETCH_ADD)
+            hipLaunchKernelGGL((k_tile_apply<T, LMR_OP_FETCH_ADD>), dim3(unsigned(num_tiles)), dim3(1024), tile_lds, s, t);
+        else
+            hipLaunchKernelGGL((k_tile_apply<T, -1>), dim3(unsigned(num_tiles)), dim3(1024), tile_lds, s, t);
+        return hipGetLastError();
+    });
+}
+
+}  // namespace lmr

@@ -1,0 +1,372 @@
+// lmr_device.hpp — device-side building blocks for the gfx950 batched
+// element-op path: element-type traits, (sub)array index math, and the
+// per-element read-modify-write that every apply kernel uses.
+//
+// The RMW restates the per-kind op semantics of the reference's generated
+// apply bodies (impl/src/array_ops.rs:327-545, src/array/native_atomic.rs:29-113)
+// as single device atomics where CDNA4 has one and as compare-and-swap loops
+// where it does not. Every record is applied atomically per element, which is
+// a valid linearisation of all reference array kinds (NativeAtomic: SeqCst
+// RMW; Generic: per-element mutex; LocalLock/GlobalLock: whole-shard lock;
+// Unsafe: racy, so any atomic order is allowed).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include "../../include/lamellar_types.h"
+
+namespace lmr {
+
+// ---------------------------------------------------------------- traits
+template <typename T> struct bits_of;
+template <> struct bits_of<uint8_t>  { using U = uint8_t;  };
+template <> struct bits_of<int8_t>   { using U = uint8_t;  };
+template <> struct bits_of<uint16_t> { using U = uint16_t; };
+template <> struct bits_of<int16_t>  { using U = uint16_t; };
+template <> struct bits_of<uint32_t> { using U = uint32_t; };
+template <> struct bits_of<int32_t>  { using U = uint32_t; };
+template <> struct bits_of<uint64_t> { using U = uint64_t; };
+template <> struct bits_of<int64_t>  { using U = uint64_t; };
+template <> struct bits_of<float>    { using U = uint32_t; };
+template <> struct bits_of<double>   { using U = uint64_t; };
+
+template <typename T> struct is_flt { static constexpr bool v = false; };
+template <> struct is_flt<float>  { static constexpr bool v = true; };
+template <> struct is_flt<double> { static constexpr bool v = true; };
+
+template <typename T> struct is_sgn { static constexpr bool v = T(-1) < T(0); };
+
+template <typename T> __host__ __device__ inline constexpr T min_of() {
+    return is_sgn<T>::v ? T(T(1) << (sizeof(T) * 8 - 1)) : T(0);
+}
+
+// LDS word type: 8/16-bit elements are widened to 32 bits in LDS tiles so the
+// ds_* atomics apply (low bits hold the element; high bits are ignored).
+template <typename T> struct word_of { using W = T; };
+template <> struct word_of<uint8_t>  { using W = uint32_t; };
+template <> struct word_of<int8_t>   { using W = uint32_t; };
+template <> struct word_of<uint16_t> { using W = uint32_t; };
+template <> struct word_of<int16_t>  { using W = uint32_t; };
+
+template <typename T>
+__device__ __forceinline__ T from_bits(typename bits_of<T>::U u) { return __builtin_bit_cast(T, u); }
+template <typename T>
+__device__ __forceinline__ typename bits_of<T>::U to_bits(T v) {
+    return __builtin_bit_cast(typename bits_of<T>::U, v);
+}
+
+// ---------------------------------------------------------------- layout
+// Restates UnsafeArray::pe_and_offset_for_global_index (src/array/unsafe.rs:1207-1223)
+// and the helpers it calls (:1610-1647 full arrays, :1651-1673 and :1708-1736 sub-arrays).
+__host__ __device__ inline bool pe_for_dist_index(const lmr_layout_t& L, uint64_t index,
+                                                  uint64_t& pe) {
+    if (!(L.size > index)) return false;
+    uint64_t g = index + L.offset;
+    if (L.distribution == LMR_DIST_BLOCK) {
+        uint64_t rem_index = L.orig_remaining_elems * (L.orig_elem_per_pe + 1);
+        pe = (g < rem_index) ? g / (L.orig_elem_per_pe + 1)
+                             : L.orig_remaining_elems + (g - rem_index) / L.orig_elem_per_pe;
+    } else {
+        pe = g % L.num_pes;
+    }
+    return true;
+}
+
+__host__ __device__ inline bool pe_and_offset(const lmr_layout_t& L, uint64_t index,
+                                              uint64_t& pe, uint64_t& off) {
+    if (!(L.size > index)) return false;
+    if (!L.sub) {
+        if (L.distribution == LMR_DIST_BLOCK) {
+            uint64_t rem_index = L.orig_remaining_elems * (L.orig_elem_per_pe + 1);
+            if (index < rem_index) {
+                pe = index / (L.orig_elem_per_pe + 1);
+                off = index - pe * (L.orig_elem_per_pe + 1);
+            } else {
+                uint64_t t = index - rem_index;
+                uint64_t tp = t / L.orig_elem_per_pe;
+                pe = L.orig_remaining_elems + tp;
+                off = t - tp * L.orig_elem_per_pe;
+            }
+        } else {
+            pe = index % L.num_pes;
+            off = index / L.num_pes;
+        }
+        return true;
+    }
+    pe_for_dist_index(L, index, pe);
+    uint64_t start_pe;
+    pe_for_dist_index(L, 0, start_pe);
+    if (L.distribution == LMR_DIST_BLOCK) {
+        if (start_pe == pe) { off = index; return true; }
+        uint64_t g = L.offset + index;
+        uint64_t rem_index = L.orig_remaining_elems * (L.orig_elem_per_pe + 1);
+        if (g < rem_index) {
+            off = g - pe * (L.orig_elem_per_pe + 1);
+        } else {
+            uint64_t t = g - rem_index;
+            uint64_t tp = t / L.orig_elem_per_pe;
+            off = t - tp * L.orig_elem_per_pe;
+        }
+        return true;
+    }
+    off = index / L.num_pes;  // (index + offset) % npes == pe holds by construction
+    return true;
+}
+
+// ---------------------------------------------------------------- errors
+__device__ __forceinline__ void raise_err(uint32_t* err, uint32_t bit) {
+    if (err) __hip_atomic_fetch_or(err, bit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// ---------------------------------------------------------------- op math
+// new value for `old op v` (pure function, no memory). Returns false when the
+// op must not be applied (Rust would panic): errbit is set accordingly.
+// `ok` is written for the two Result ops; `ret` is the value the record returns.
+template <typename T>
+__device__ __forceinline__ bool op_math(int op, int kind, T old, T v, T cmp, T eps,
+                                        T& nw, T& ret, uint8_t& ok, uint32_t& errbit) {
+    using U = typename bits_of<T>::U;
+    ret = old;
+    nw = old;
+    switch (op) {
+    case LMR_OP_ADD: case LMR_OP_FETCH_ADD:
+        if constexpr (is_flt<T>::v) nw = old + v; else nw = T(U(U(old) + U(v)));
+        return true;
+    case LMR_OP_SUB: case LMR_OP_FETCH_SUB:
+        if constexpr (is_flt<T>::v) nw = old - v; else nw = T(U(U(old) - U(v)));
+        return true;
+    case LMR_OP_MUL: case LMR_OP_FETCH_MUL:
+        if constexpr (is_flt<T>::v) nw = old * v;
+        else if constexpr (sizeof(T) < 4) nw = T(U(uint32_t(U(old)) * uint32_t(U(v))));
+        else nw = T(U(U(old) * U(v)));
+        return true;
+    case LMR_OP_DIV: case LMR_OP_FETCH_DIV:
+        if constexpr (is_flt<T>::v) { nw = old / v; return true; }
+        else {
+            if (v == T(0)) { errbit = LMR_ERRBIT_DIVZERO; return false; }
+            if constexpr (is_sgn<T>::v)
+                if (old == min_of<T>() && v == T(-1)) { errbit = LMR_ERRBIT_OVERFLOW; return false; }
+            nw = T(old / v);
+            return true;
+        }
+    case LMR_OP_REM: case LMR_OP_FETCH_REM:
+        if constexpr (is_flt<T>::v) { nw = fmod(old, v); return true; }
+        else {
+            if (v == T(0)) { errbit = LMR_ERRBIT_DIVZERO; return false; }
+            if constexpr (is_sgn<T>::v)
+                if (old == min_of<T>() && v == T(-1)) { errbit = LMR_ERRBIT_OVERFLOW; return false; }
+            nw = T(old % v);
+            return true;
+        }
+    case LMR_OP_STORE: case LMR_OP_PUT: case LMR_OP_SWAP:
+        nw = v;
+        return true;
+    case LMR_OP_LOAD: case LMR_OP_GET:
+        return true;
+    case LMR_OP_COMPARE_EXCHANGE_EPS: {
+        if constexpr (is_flt<T>::v) {
+            bool same = (cmp > old) ? ((cmp - old) < eps) : ((old - cmp) < eps);
+            if (same) { nw = v; ok = 1; ret = cmp; } else { ok = 0; }
+            return true;
+        } else {
+            if (kind == LMR_KIND_NATIVE_ATOMIC) {
+                // impl/src/array_ops.rs:391-419
+                if (old == cmp) { nw = v; ok = 1; ret = v; return true; }
+                U d = (old > cmp) ? U(U(old) - U(cmp)) : U(U(cmp) - U(old));
+                if (T(d) < eps) { nw = v; ok = 1; ret = old; } else { ok = 0; }
+                return true;
+            }
+            // impl/src/array_ops.rs:521-535
+            bool same = (cmp > old) ? (T(U(U(cmp) - U(old))) < eps) : (T(U(U(old) - U(cmp))) < eps);
+            if (same) { nw = v; ok = 1; ret = cmp; } else { ok = 0; }
+            return true;
+        }
+    }
+    default: break;
+    }
+    if constexpr (!is_flt<T>::v) {
+        constexpr unsigned BITS = sizeof(T) * 8;
+        switch (op) {
+        case LMR_OP_AND: case LMR_OP_FETCH_AND: nw = T(old & v); return true;
+        case LMR_OP_OR:  case LMR_OP_FETCH_OR:  nw = T(old | v); return true;
+        case LMR_OP_XOR: case LMR_OP_FETCH_XOR: nw = T(old ^ v); return true;
+        case LMR_OP_COMPARE_EXCHANGE:
+            if (old == cmp) { nw = v; ok = 1; ret = cmp; } else { ok = 0; }
+            return true;
+        case LMR_OP_SHL: case LMR_OP_FETCH_SHL: {
+            unsigned s = unsigned(U(v)) & (BITS - 1);
+            if constexpr (sizeof(T) < 4) nw = T(U(uint32_t(U(old)) << s));
+            else nw = T(U(U(old) << s));
+            return true;
+        }
+        case LMR_OP_SHR: case LMR_OP_FETCH_SHR: {
+            unsigned s = unsigned(U(v)) & (BITS - 1);
+            nw = T(old >> s);
+            return true;
+        }
+        default: break;
+        }
+    }
+    errbit = LMR_ERRBIT_UNSUPPORTED;
+    return false;
+}
+
+// true when `op` never changes the element (no write needed)
+__device__ __forceinline__ bool op_is_read(int op) { return op == LMR_OP_LOAD || op == LMR_OP_GET; }
+
+// ---------------------------------------------------------------- RMW on a
+// naturally aligned 32/64-bit word (global or LDS; the address space is
+// inferred after inlining). T has sizeof 4 or 8.
+template <typename T>
+__device__ __forceinline__ T rmw_word(T* p, int op, int kind, T v, T cmp, T eps,
+                                      uint8_t& ok, uint32_t* err) {
+    static_assert(sizeof(T) == 4 || sizeof(T) == 8, "word RMW");
+    using U = typename bits_of<T>::U;
+    U* up = reinterpret_cast<U*>(p);
+    // single-instruction forms
+    if constexpr (!is_flt<T>::v) {
+        switch (op) {
+        case LMR_OP_ADD: case LMR_OP_FETCH_ADD:
+            return T(__hip_atomic_fetch_add(up, U(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+        case LMR_OP_SUB: case LMR_OP_FETCH_SUB:
+            return T(__hip_atomic_fetch_add(up, U(U(0) - U(v)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+        case LMR_OP_AND: case LMR_OP_FETCH_AND:
+            return T(__hip_atomic_fetch_and(up, U(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+        case LMR_OP_OR: case LMR_OP_FETCH_OR:
+            return T(__hip_atomic_fetch_or(up, U(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+        case LMR_OP_XOR: case LMR_OP_FETCH_XOR:
+            return T(__hip_atomic_fetch_xor(up, U(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+        case LMR_OP_COMPARE_EXCHANGE: {
+            U expected = U(cmp);
+            __hip_atomic_compare_exchange_strong(up, &expected, U(v), __ATOMIC_RELAXED,
+                                                 __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            // expected now holds the value that was there
+            ok = (expected == U(cmp)) ? 1 : 0;
+            return ok ? cmp : T(expected);
+        }
+        default: break;
+        }
+    } else {
+        if (op == LMR_OP_ADD || op == LMR_OP_FETCH_ADD)
+            return unsafeAtomicAdd(p, v);
+        if (op == LMR_OP_SUB || op == LMR_OP_FETCH_SUB)
+            return unsafeAtomicAdd(p, -v);   // x - y == x + (-y) in IEEE-754
+    }
+    if (op == LMR_OP_STORE || op == LMR_OP_PUT || op == LMR_OP_SWAP)
+        return from_bits<T>(__hip_atomic_exchange(up, to_bits(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    if (op_is_read(op))
+        return from_bits<T>(__hip_atomic_load(up, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    // compare-and-swap loop for mul/div/rem/shl/shr/compare_exchange_epsilon
+    U cur = __hip_atomic_load(up, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    while (true) {
+        T old = from_bits<T>(cur), nw, ret;
+        uint32_t eb = 0;
+        if (!op_math<T>(op, kind, old, v, cmp, eps, nw, ret, ok, eb)) {
+            raise_err(err, eb);
+            return old;
+        }
+        U nb = to_bits(nw);
+        if (nb == cur) return ret;   // nothing to write (e.g. failed compare)
+        U expected = cur;
+        if (__hip_atomic_compare_exchange_strong(up, &expected, nb, __ATOMIC_RELAXED,
+                                                 __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+            return ret;
+        cur = expected;
+    }
+}
+
+// RMW of an 8/16-bit element held in the low bits of a 32-bit LDS word.
+template <typename T>
+__device__ __forceinline__ T rmw_widened(uint32_t* p, int op, int kind, T v, T cmp, T eps,
+                                         uint8_t& ok, uint32_t* err) {
+    using U = typename bits_of<T>::U;
+    // wrapping add/sub/and/or/xor on the low bits are exact in 32 bits
+    switch (op) {
+    case LMR_OP_ADD: case LMR_OP_FETCH_ADD:
+        return T(U(__hip_atomic_fetch_add(p, uint32_t(U(v)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)));
+    case LMR_OP_SUB: case LMR_OP_FETCH_SUB:
+        return T(U(__hip_atomic_fetch_add(p, uint32_t(0) - uint32_t(U(v)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)));
+    case LMR_OP_AND: case LMR_OP_FETCH_AND:
+        return T(U(__hip_atomic_fetch_and(p, uint32_t(U(v)) | 0xFFFFFFFFu << (8 * sizeof(T)),
+                                          __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)));
+    case LMR_OP_OR: case LMR_OP_FETCH_OR:
+        return T(U(__hip_atomic_fetch_or(p, uint32_t(U(v)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)));
+    case LMR_OP_XOR: case LMR_OP_FETCH_XOR:
+        return T(U(__hip_atomic_fetch_xor(p, uint32_t(U(v)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)));
+    case LMR_OP_STORE: case LMR_OP_PUT: case LMR_OP_SWAP:
+        return T(U(__hip_atomic_exchange(p, uint32_t(U(v)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)));
+    case LMR_OP_LOAD: case LMR_OP_GET:
+        return T(U(__hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)));
+    default: break;
+    }
+    uint32_t cur = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    while (true) {
+        T old = T(U(cur)), nw, ret;
+        uint32_t eb = 0;
+        if (!op_math<T>(op, kind, old, v, cmp, eps, nw, ret, ok, eb)) {
+            raise_err(err, eb);
+            return old;
+        }
+        uint32_t nb = uint32_t(U(nw));
+        if (nb == (cur & ((1u << (8 * sizeof(T))) - 1u))) return ret;
+        uint32_t expected = cur;
+        if (__hip_atomic_compare_exchange_strong(p, &expected, nb, __ATOMIC_RELAXED,
+                                                 __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP))
+            return ret;
+        cur = expected;
+    }
+}
+
+// RMW of an 8/16-bit element in global memory: CAS on the naturally aligned
+// 32-bit word that contains it. Requires the shard allocation to be readable
+// up to the next 4-byte boundary (hipMalloc/torch allocations are 256-B granular).
+template <typename T>
+__device__ __forceinline__ T rmw_subword_global(T* p, int op, int kind, T v, T cmp, T eps,
+                                                uint8_t& ok, uint32_t* err) {
+    using U = typename bits_of<T>::U;
+    uintptr_t a = reinterpret_cast<uintptr_t>(p);
+    uint32_t* wp = reinterpret_cast<uint32_t*>(a & ~uintptr_t(3));
+    const unsigned sh = unsigned(a & 3) * 8;
+    const uint32_t mask = uint32_t((1u << (8 * sizeof(T))) - 1u) << sh;
+    uint32_t cur = __hip_atomic_load(wp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    while (true) {
+        T old = T(U((cur & mask) >> sh)), nw, ret;
+        uint32_t eb = 0;
+        if (!op_math<T>(op, kind, old, v, cmp, eps, nw, ret, ok, eb)) {
+            raise_err(err, eb);
+            return old;
+        }
+        if (op_is_read(op)) return ret;
+        uint32_t nb = (cur & ~mask) | (uint32_t(U(nw)) << sh);
+        if (nb == cur) return ret;
+        uint32_t expected = cur;
+        if (__hip_atomic_compare_exchange_strong(wp, &expected, nb, __ATOMIC_RELAXED,
+                                                 __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+            return ret;
+        cur = expected;
+    }
+}
+
+// Global-memory RMW of one element of any supported type.
+template <typename T>
+__device__ __forceinline__ T rmw_global(T* p, int op, int kind, T v, T cmp, T eps,
+                                        uint8_t& ok, uint32_t* err) {
+    if constexpr (sizeof(T) >= 4) return rmw_word<T>(p, op, kind, v, cmp, eps, ok, err);
+    else return rmw_subword_global<T>(p, op, kind, v, cmp, eps, ok, err);
+}
+
+// LDS-tile RMW (tile words of type word_of<T>::W).
+template <typename T>
+__device__ __forceinline__ T rmw_lds(typename word_of<T>::W* p, int op, int kind, T v, T cmp,
+                                     T eps, uint8_t& ok, uint32_t* err) {
+    if constexpr (sizeof(T) >= 4) return rmw_word<T>(p, op, kind, v, cmp, eps, ok, err);
+    else return rmw_widened<T>(p, op, kind, v, cmp, eps, ok, err);
+}
+
+// ---------------------------------------------------------------- index load
+template <int IW> struct idx_t;
+template <> struct idx_t<1> { using I = uint8_t; };
+template <> struct idx_t<2> { using I = uint16_t; };
+template <> struct idx_t<4> { using I = uint32_t; };
+template <> struct idx_t<8> { using I = uint64_t; };
+
+}  // namespace lmr

@@ -1,0 +1,122 @@
+// lmr_internal.hpp — host-side internals shared by the .hip translation units
+// of liblamellar_gpu_ops.so (not part of the C ABI).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stddef.h>
+#include "../../include/lamellar_gpu_ops.h"
+
+namespace lmr { struct Prof; }
+
+struct lmr_ctx {
+    int device = 0;
+    uint32_t* d_err = nullptr;     // device error word (LMR_ERRBIT_*)
+    // tiled-apply / pack workspace (allocated by lmr_ctx_reserve, never on the hot path)
+    uint8_t* ws = nullptr;
+    size_t ws_bytes = 0;
+    uint64_t rec_cap = 0;          // records one tiled piece may hold
+    int num_cus = 256;
+    lmr::Prof* prof = nullptr;     // stage timing (lmr_ctx_profile), null when off
+};
+
+namespace lmr {
+
+// ---- tiling constants (gfx950: 160 KiB LDS per CU; two 64 KiB tiles per CU) ----
+constexpr int kTileBytes = 64 * 1024;
+constexpr int kMaxTiles = 16384;          // LDS histogram of 64 KiB u32 counters
+constexpr int kBinBlock = 1024;           // threads per bin/scatter block
+constexpr int kMaxBinBlocks = 1024;       // G: blocks of the bin passes
+constexpr int kScanItems = 4096;          // elements per scan block (1024 threads x 4)
+constexpr int kMaxPackPes = 512;
+
+// ---- stage timing: HIP events around kernel stages (see lmr_ctx_profile) ----
+void prof_begin(Prof* p, int stage, hipStream_t s);
+void prof_end(Prof* p, int stage, hipStream_t s);
+struct ProfScope {
+    Prof* p; int st; hipStream_t s;
+    ProfScope(Prof* p_, int st_, hipStream_t s_) : p(p_), st(st_), s(s_) { if (p) prof_begin(p, st, s); }
+    ~ProfScope() { if (p) prof_end(p, st, s); }
+};
+
+// Workspace carve-up of one tiled piece.
+struct TiledWs {
+    uint32_t* counts;      // [num_tiles * G]
+    uint32_t* partials;    // scan block partials
+    uint32_t* tile_start;  // [num_tiles + 1]
+    uint16_t* bin_lidx;    // [cap]
+    uint8_t* bin_val;      // [cap * 8]
+    uint32_t* bin_pos;     // [cap]
+    uint32_t* total;       // [1]
+};
+size_t tiled_ws_bytes(uint64_t cap);
+TiledWs carve_tiled_ws(uint8_t* base, uint64_t cap);
+
+// exclusive scan of d[0..m) in place; *d_total = sum (may be null). partials
+// must hold ceil(m / kScanItems) entries.
+hipError_t scan_exclusive_u32(uint32_t* d, uint64_t m, uint32_t* partials, uint32_t* d_total,
+                              hipStream_t s);
+
+struct ApplyArgs {
+    void* shard;
+    uint64_t shard_len;
+    int kind;
+    int op;
+    int ret;
+    uint64_t cmp_bits;
+    uint64_t eps_bits;
+    uint32_t* err;
+    // records: index k at idx + k*idx_stride (bytes); value at val + k*val_stride,
+    // or the scalar `val_bits` when val == nullptr (single value, many indices)
+    const uint8_t* idx;
+    uint64_t idx_stride;
+    const uint8_t* val;
+    uint64_t val_stride;
+    uint64_t val_bits;
+    uint64_t n;
+    void* results;   // T per record (ret != NONE)
+    uint8_t* ok;     // per record (ret == RESULT)
+    Prof* prof;
+};
+
+// launchers (dtype-dispatching), defined in lmr_apply.hip
+hipError_t launch_apply_direct(int dtype, int index_size, const ApplyArgs& a, hipStream_t s);
+hipError_t launch_apply_mvsi(int dtype, const ApplyArgs& a, uint64_t index, hipStream_t s);
+// tiled apply of SoA/AoS records; returns hipErrorNotSupported when the shard
+// is too large for the single-level tile histogram.
+hipError_t launch_apply_tiled(int dtype, int index_size, const ApplyArgs& a, const TiledWs& w,
+                              hipStream_t s);
+bool tiled_supported(int dtype, uint64_t shard_len);
+
+// pack (lmr_pack.hip)
+struct PackArgs {
+    lmr_layout_t layout;
+    const uint64_t* gidx;
+    const uint8_t* vals;     // may be null (SVMI)
+    uint32_t val_bytes;
+    uint64_t n;
+    uint32_t index_size;
+    uint8_t* out_idx;
+    uint8_t* out_vals;
+    uint32_t* out_pos;
+    uint64_t* dest_counts;   // [npes]
+    uint64_t* dest_offsets;  // [npes + 1]
+    uint32_t* err;
+    Prof* prof;
+};
+hipError_t launch_pack(const PackArgs& a, uint32_t* counts, uint32_t* partials, uint32_t* total,
+                       hipStream_t s);
+hipError_t launch_scatter_results(const uint8_t* in, const uint32_t* pos, uint64_t n,
+                                  uint32_t elem_bytes, uint8_t* out, const uint8_t* ok_in,
+                                  uint8_t* ok_out, Prof* prof, hipStream_t s);
+
+inline int dtype_bytes(int d) {
+    switch (d) {
+    case LMR_U8: case LMR_I8: return 1;
+    case LMR_U16: case LMR_I16: return 2;
+    case LMR_U32: case LMR_I32: case LMR_F32: return 4;
+    case LMR_U64: case LMR_I64: case LMR_F64: return 8;
+    default: return 0;
+    }
+}
+
+}  // namespace lmr

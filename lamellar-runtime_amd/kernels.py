@@ -1,0 +1,181 @@
+"""Device kernels of the batched element-op path, called through the C ABI.
+
+`DeviceKernels` is the only product implementation: every method enqueues
+gfx950 kernels of liblamellar_gpu_ops.so on torch's current HIP stream. There
+is no CPU fallback; without a GPU the constructor raises.
+"""
+from __future__ import annotations
+
+import ctypes
+from ctypes import byref, c_uint32, c_uint64, c_void_p
+
+import torch
+
+from . import _capi
+from .types import (ERRBIT_DIVZERO, ERRBIT_OOB, ERRBIT_OVERFLOW, ERRBIT_UNSUPPORTED,
+                    LmrStatus, Strategy)
+
+
+class LamellarError(RuntimeError):
+    """Raised where the reference panics (OOB index, integer div by zero, ...)."""
+
+    def __init__(self, status, msg=""):
+        self.status = LmrStatus(status)
+        super().__init__(f"{self.status.name}: {msg}")
+
+
+def check(st: int, what: str = ""):
+    if st != 0:
+        raise LamellarError(st, f"{what}: {_capi.status_string(st)}")
+
+
+def errbits_to_status(bits: int) -> int:
+    if bits & ERRBIT_OOB:
+        return LmrStatus.OOB
+    if bits & ERRBIT_DIVZERO:
+        return LmrStatus.DIVZERO
+    if bits & ERRBIT_OVERFLOW:
+        return LmrStatus.OVERFLOW
+    if bits & ERRBIT_UNSUPPORTED:
+        return LmrStatus.UNSUPPORTED
+    return LmrStatus.OK
+
+
+def _p(t):
+    return None if t is None else ctypes.c_void_p(t.data_ptr())
+
+
+class DeviceKernels:
+    """Per-device context + the C-ABI calls, on torch's current stream."""
+
+    is_device = True
+
+    def __init__(self, device: torch.device, strategy: int = Strategy.Auto,
+                 max_ws_records: int = 1 << 28):
+        if device.type != "cuda" or not torch.cuda.is_available():
+            raise LamellarError(LmrStatus.INVALID,
+                                "the batched op path runs on a HIP device; no GPU is visible")
+        self.device = device
+        self.lib = _capi.lib()
+        self.ctx = c_void_p()
+        check(self.lib.lmr_ctx_create(device.index or 0, byref(self.ctx)), "lmr_ctx_create")
+        self.strategy = int(strategy)
+        self.max_ws_records = int(max_ws_records)
+        self.reserved = 0
+
+    # ---------------------------------------------------------------- infra
+    def stream(self):
+        return ctypes.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
+
+    def reserve(self, n: int):
+        """Grow the tiled-apply workspace (allocation: call outside timed regions)."""
+        n = min(int(n), self.max_ws_records)
+        if n > self.reserved:
+            torch.cuda.current_stream(self.device).synchronize()
+            check(self.lib.lmr_ctx_reserve(self.ctx, n), "lmr_ctx_reserve")
+            self.reserved = n
+
+    def _maybe_reserve(self, n):
+        if self.strategy != Strategy.Direct and n >= 65536 and self.reserved < min(n, self.max_ws_records):
+            self.reserve(max(n, 1 << 20))
+
+    def errors(self, clear=True) -> int:
+        bits = c_uint32(0)
+        self.lib.lmr_ctx_error(self.ctx, self.stream(), byref(bits), 1 if clear else 0)
+        return bits.value
+
+    def check_errors(self):
+        bits = self.errors(clear=True)
+        if bits:
+            st = errbits_to_status(bits)
+            raise LamellarError(st, f"device error bits 0x{bits:x}")
+
+    def profile(self, enable=True):
+        """Record HIP events around every kernel stage (lmr_ctx_profile)."""
+        check(self.lib.lmr_ctx_profile(self.ctx, 1 if enable else 0), "lmr_ctx_profile")
+
+    def profile_read(self, reset=True):
+        """{stage: (total_ms, launches)} accumulated since the last reset."""
+        n = len(_capi.STAGES)
+        ms = (ctypes.c_double * n)()
+        cnt = (c_uint64 * n)()
+        check(self.lib.lmr_ctx_profile_read(self.ctx, self.stream(), ms, cnt, 1 if reset else 0),
+              "lmr_ctx_profile_read")
+        return {name: (ms[i], cnt[i]) for i, name in enumerate(_capi.STAGES)}
+
+    def synchronize(self):
+        torch.cuda.current_stream(self.device).synchronize()
+
+    def empty(self, n, torch_dtype):
+        return torch.empty(max(int(n), 0), dtype=torch_dtype, device=self.device)
+
+    def to_device(self, t):
+        return t.to(self.device, non_blocking=False)
+
+    # ---------------------------------------------------------------- ops
+    def _desc(self, shard, shard_len, kind, dt, op, cmp_bits=0, eps_bits=0):
+        d = _capi.lmr_apply_desc_t()
+        d.shard = shard.data_ptr()
+        d.shard_len = int(shard_len)
+        d.kind = int(kind)
+        d.dtype = int(dt.code)
+        d.op = int(op)
+        d.strategy = self.strategy
+        d.cmp_bits = int(cmp_bits)
+        d.eps_bits = int(eps_bits)
+        return d
+
+    def apply_soa(self, shard, shard_len, kind, dt, op, idx, iw, vals, scalar_bits, n,
+                  results=None, ok=None, cmp_bits=0, eps_bits=0):
+        """Apply n records (idx: iw-byte local offsets; vals tensor or scalar bits)."""
+        self._maybe_reserve(n)
+        d = self._desc(shard, shard_len, kind, dt, op, cmp_bits, eps_bits)
+        sv = c_uint64(int(scalar_bits) & 0xFFFFFFFFFFFFFFFF)
+        st = self.lib.lmr_apply_soa(self.ctx, byref(d), _p(idx), int(iw), _p(vals),
+                                    None if vals is not None else ctypes.cast(byref(sv), c_void_p),
+                                    int(n), _p(results), _p(ok), self.stream())
+        check(st, "lmr_apply_soa")
+
+    def apply_mvmi(self, shard, shard_len, kind, dt, op, idx_vals_bytes, nbytes, iw,
+                   results=None, ok=None, cmp_bits=0, eps_bits=0):
+        """Apply a reference wire-format op buffer (packed IdxVal<I,T> records)."""
+        self._maybe_reserve(nbytes // max(1, self.lib.lmr_record_bytes(iw, dt.code)))
+        d = self._desc(shard, shard_len, kind, dt, op, cmp_bits, eps_bits)
+        st = self.lib.lmr_apply_mvmi(self.ctx, byref(d), _p(idx_vals_bytes), int(nbytes), int(iw),
+                                     _p(results), _p(ok), self.stream())
+        check(st, "lmr_apply_mvmi")
+
+    def apply_svmi(self, shard, shard_len, kind, dt, op, scalar_bits, indices, n, iw,
+                   results=None, ok=None, cmp_bits=0, eps_bits=0):
+        self._maybe_reserve(n)
+        d = self._desc(shard, shard_len, kind, dt, op, cmp_bits, eps_bits)
+        sv = c_uint64(int(scalar_bits) & 0xFFFFFFFFFFFFFFFF)
+        st = self.lib.lmr_apply_svmi(self.ctx, byref(d), ctypes.cast(byref(sv), c_void_p), _p(indices),
+                                     int(n), int(iw), _p(results), _p(ok), self.stream())
+        check(st, "lmr_apply_svmi")
+
+    def apply_mvsi(self, shard, shard_len, kind, dt, op, vals, n, index, results=None, ok=None,
+                   cmp_bits=0, eps_bits=0):
+        d = self._desc(shard, shard_len, kind, dt, op, cmp_bits, eps_bits)
+        st = self.lib.lmr_apply_mvsi(self.ctx, byref(d), _p(vals), int(n), int(index), _p(results),
+                                     _p(ok), self.stream())
+        check(st, "lmr_apply_mvsi")
+
+    def pack(self, layout, gidx, n, vals, dt, iw):
+        """Stable partition by destination PE -> (idx, vals, pos, counts[int64 host list])."""
+        npes = layout.num_pes
+        out_idx = self.empty(n * iw, torch.uint8)
+        out_vals = self.empty(n * dt.bytes, torch.uint8) if vals is not None else None
+        out_pos = self.empty(n, torch.int32)
+        counts = self.empty(npes, torch.int64)
+        offsets = self.empty(npes + 1, torch.int64)
+        st = self.lib.lmr_pack(self.ctx, byref(layout), _p(gidx), int(n), _p(vals), int(dt.code), int(iw),
+                               _p(out_idx), _p(out_vals), _p(out_pos), _p(counts), _p(offsets),
+                               self.stream())
+        check(st, "lmr_pack")
+        return out_idx, out_vals, out_pos, counts
+
+    def scatter_results(self, res_in, pos, n, eb, res_out, ok_in=None, ok_out=None):
+        st = self.lib.lmr_scatter_results(_p(res_in), _p(pos), int(n), int(eb), _p(res_out),
+                                          _p(ok_in), _p(ok_out), self.stream())
+        check(st, "lmr_scatter_results")

@@ -1,0 +1,321 @@
+"""Device parity: liblamellar_gpu_ops.so (through the C ABI) vs the CPU oracle.
+
+Bar: bit-exact for every integer op; for f32/f64 bit-exact where each element
+sees one record (conflict-free streams), and within a stated relative bound
+where records collide (float addition is not associative).
+"""
+import numpy as np
+import pytest
+import torch
+
+from opgen import (ADD, AND, CAS, CAS_EPS, CODE, COMMUTATIVE_INT, DIV, DTYPE_NAMES, FETCH_ADD,
+                   FETCH_SUB, IS_FLOAT, MUL, NP, OR, REM, SUB, XOR, bits_equal, cas_operands,
+                   ops_for, rand_elems, rand_vals, ret_kind, to_aos)
+
+pytestmark = pytest.mark.gpu
+
+KIND_NATIVE, KIND_GENERIC, KIND_LOCAL_LOCK, KIND_UNSAFE = 1, 2, 3, 0
+
+
+def kind_for(dt):
+    return KIND_GENERIC if IS_FLOAT[dt] else KIND_NATIVE
+
+
+def to_dev(a):
+    a = np.ascontiguousarray(a)
+    return torch.from_numpy(a.view(np.uint8).copy()).cuda()
+
+
+def from_dev(t, dt, n):
+    return t[: n * np.dtype(NP[dt]).itemsize].cpu().numpy().view(NP[dt])
+
+
+class Case:
+    """One kernel-level apply: device vs oracle on identical inputs."""
+
+    def __init__(self, k, orc, lam, dt, op, shard0, idx, vals, shape, strategy, kind=None,
+                 cur=None, eps=None):
+        self.dt, self.op = dt, op
+        kind = kind_for(dt) if kind is None else kind
+        t = NP[dt]
+        n = idx.size if shape != "mvsi" else vals.size
+        L = orc.layout_new(shard0.size, 1, 0, 0)
+        iw = orc.index_size(L)
+        # ---- oracle (sequential, input order) ----
+        ref = shard0.copy()
+        if shape == "mvsi":
+            st_o, res_o, ok_o = orc.apply_mvsi(ref, kind, CODE[dt], t, op, vals, int(idx[0]), cur, eps)
+        elif shape == "svmi":
+            st_o, res_o, ok_o = orc.batch_op(L, [ref], kind, CODE[dt], t, op, idx, vals[:1], cur, eps)
+        else:
+            st_o, res_o, ok_o = orc.batch_op(L, [ref], kind, CODE[dt], t, op, idx, vals, cur, eps)
+        # ---- device ----
+        old_strategy = k.strategy
+        k.strategy = strategy
+        try:
+            dt_obj = lam.dtype_of(dt)
+            d_shard = to_dev(shard0)
+            eb = np.dtype(t).itemsize
+            d_res = torch.zeros(max(n, 1) * eb, dtype=torch.uint8, device="cuda")
+            d_ok = torch.zeros(max(n, 1), dtype=torch.uint8, device="cuda")
+            rk = ret_kind(op)
+            res_arg = d_res if rk else None
+            ok_arg = d_ok if rk == 2 else None
+            cb = dt_obj.to_bits(cur) if cur is not None else 0
+            ebits = dt_obj.to_bits(eps) if eps is not None else 0
+            if shape == "soa":
+                k.apply_soa(d_shard, shard0.size, kind, dt_obj, op, to_dev(idx.astype(np.uint64)), 8,
+                            to_dev(vals), 0, n, res_arg, ok_arg, cb, ebits)
+            elif shape == "svmi":
+                ii = idx.astype({1: np.uint8, 2: np.uint16, 4: np.uint32, 8: np.uint64}[iw])
+                k.apply_svmi(d_shard, shard0.size, kind, dt_obj, op, dt_obj.to_bits(vals[0]),
+                             to_dev(ii), n, iw, res_arg, ok_arg, cb, ebits)
+            elif shape == "aos":
+                rb, vo = orc.record_bytes(iw, CODE[dt]), orc.record_val_offset(iw, CODE[dt])
+                buf = to_aos(idx, vals, iw, dt, rb, vo)
+                k.apply_mvmi(d_shard, shard0.size, kind, dt_obj, op, to_dev(buf), buf.size, iw,
+                             res_arg, ok_arg, cb, ebits)
+            elif shape == "mvsi":
+                k.apply_mvsi(d_shard, shard0.size, kind, dt_obj, op, to_dev(vals), n, int(idx[0]),
+                             res_arg, ok_arg, cb, ebits)
+            k.synchronize()
+            self.err = k.errors(clear=True)
+        finally:
+            k.strategy = old_strategy
+        self.st_o = st_o
+        self.ref, self.res_o, self.ok_o = ref, res_o, ok_o
+        self.got = from_dev(d_shard, dt, shard0.size)
+        self.res_d = from_dev(d_res, dt, n) if rk else None
+        self.ok_d = d_ok[:n].cpu().numpy() if rk == 2 else None
+        self.rk = rk
+
+
+def _perm_inputs(dt, op, rng, shard_len, n):
+    shard0 = rand_elems(dt, shard_len, rng, op)
+    idx = rng.permutation(shard_len)[:n].astype(np.uint64)
+    vals = rand_vals(dt, n, rng, op)
+    cur = eps = None
+    if op in (CAS, CAS_EPS):
+        cur, eps, shard0 = cas_operands(dt, shard0, vals, rng)
+    return shard0, idx, vals, cur, eps
+
+
+@pytest.mark.parametrize("shape", ["soa", "svmi", "aos"])
+@pytest.mark.parametrize("strategy", [1, 2], ids=["direct", "tiled"])
+@pytest.mark.parametrize("dt", DTYPE_NAMES)
+def test_apply_conflict_free_bit_exact(world, orc, lam, dt, strategy, shape):
+    """Every op, every type: one record per element -> bit-exact state and results."""
+    k = world.team().kernels
+    k.reserve(1 << 20)
+    rng = np.random.default_rng(1234 + CODE[dt])
+    for op in ops_for(dt):
+        shard0, idx, vals, cur, eps = _perm_inputs(dt, op, rng, 40000, 30000)
+        if shape == "svmi" and op in (DIV, REM, 7, 9):
+            vals[:] = vals[0]
+        c = Case(k, orc, lam, dt, op, shard0, idx, vals, shape, strategy, cur=cur, eps=eps)
+        assert c.err == 0 and c.st_o == 0, (dt, op, c.err, c.st_o)
+        assert bits_equal(c.got, c.ref), (dt, op, shape, strategy)
+        if c.rk:
+            assert bits_equal(c.res_d, c.res_o), (dt, op, "results")
+        if c.rk == 2:
+            assert np.array_equal(c.ok_d, c.ok_o), (dt, op, "ok")
+
+
+@pytest.mark.parametrize("dt", DTYPE_NAMES)
+def test_apply_cas_eps_generic_kind(world, orc, lam, dt):
+    """compare_exchange_epsilon on non-native kinds (LocalLock): array_ops.rs:521-535."""
+    k = world.team().kernels
+    rng = np.random.default_rng(77)
+    shard0, idx, vals, cur, eps = _perm_inputs(dt, CAS_EPS, rng, 4096, 3000)
+    c = Case(k, orc, lam, dt, CAS_EPS, shard0, idx, vals, "soa", 1, kind=KIND_LOCAL_LOCK, cur=cur, eps=eps)
+    assert bits_equal(c.got, c.ref) and bits_equal(c.res_d, c.res_o) and np.array_equal(c.ok_d, c.ok_o)
+
+
+@pytest.mark.parametrize("dt", DTYPE_NAMES)
+def test_apply_mvsi_in_order(world, orc, lam, dt):
+    """Many values at one index are applied in buffer order: bit-exact even for floats."""
+    k = world.team().kernels
+    rng = np.random.default_rng(5 + CODE[dt])
+    for op in ops_for(dt):
+        shard0 = rand_elems(dt, 64, rng, op)
+        vals = rand_vals(dt, 300, rng, op)
+        cur = eps = None
+        if op in (CAS, CAS_EPS):
+            cur, eps, shard0 = cas_operands(dt, shard0, vals, rng)
+            shard0[17] = cur
+            vals[::3] = cur
+        if op in (MUL, 5) and IS_FLOAT[dt]:
+            vals = np.abs(vals) * 0 + NP[dt](1.0009765625)
+        c = Case(k, orc, lam, dt, op, shard0, np.array([17], dtype=np.uint64), vals, "mvsi", 1,
+                 cur=cur, eps=eps)
+        assert c.err == 0 and c.st_o == 0
+        assert bits_equal(c.got, c.ref), (dt, op)
+        if c.rk:
+            assert bits_equal(c.res_d, c.res_o), (dt, op)
+
+
+@pytest.mark.parametrize("strategy", [1, 2], ids=["direct", "tiled"])
+@pytest.mark.parametrize("dt", ["u8", "u16", "u32", "u64", "i8", "i16", "i32", "i64"])
+def test_apply_collisions_order_independent(world, orc, lam, dt, strategy):
+    """Colliding indices: wrapping integer add/sub/mul/and/or/xor give a bit-exact final state."""
+    k = world.team().kernels
+    k.reserve(1 << 20)
+    rng = np.random.default_rng(99 + CODE[dt])
+    for op in sorted(COMMUTATIVE_INT):
+        shard0 = rand_elems(dt, 5000, rng, op)
+        idx = rng.integers(0, 5000, 200000).astype(np.uint64)
+        vals = rand_vals(dt, idx.size, rng, op)
+        c = Case(k, orc, lam, dt, op, shard0, idx, vals, "soa", strategy)
+        assert c.err == 0
+        assert bits_equal(c.got, c.ref), (dt, op)
+
+
+@pytest.mark.parametrize("strategy", [1, 2], ids=["direct", "tiled"])
+@pytest.mark.parametrize("dt", ["u32", "u64", "i32", "i64", "u16"])
+def test_fetch_add_linearizable(world, orc, lam, dt, strategy):
+    """Colliding fetch_add / fetch_sub: per element the returned olds are exactly the
+    prefix states of some serial order (each old distinct, chain closes at the final value)."""
+    k = world.team().kernels
+    k.reserve(1 << 20)
+    rng = np.random.default_rng(3)
+    t = NP[dt]
+    for op in (FETCH_ADD, FETCH_SUB):
+        shard0 = rand_elems(dt, 1000, rng)
+        idx = rng.integers(0, 1000, 100000).astype(np.uint64)
+        vals = np.ones(idx.size, dtype=t)
+        c = Case(k, orc, lam, dt, op, shard0, idx, vals, "soa", strategy)
+        assert bits_equal(c.got, c.ref)
+        # with v = 1 the olds for element e must be {a0, a0±1, ..., a0±(m-1)} (wrapping)
+        order = np.lexsort((c.res_d.astype(np.uint64), idx))
+        cnt = np.bincount(idx.astype(np.int64), minlength=1000)
+        start = np.concatenate([[0], np.cumsum(cnt)[:-1]])
+        olds = c.res_d[order]
+        step = 1 if op == FETCH_ADD else -1
+        for e in np.nonzero(cnt)[0][:200]:
+            m = cnt[e]
+            got = np.sort(olds[start[e]:start[e] + m].astype(np.uint64))
+            exp = np.sort((np.uint64(shard0[e].astype(np.int64).astype(np.uint64))
+                           + np.arange(m, dtype=np.int64).astype(np.uint64) * np.uint64(step & 0xFFFFFFFFFFFFFFFF))
+                          .astype(t).astype(np.uint64))
+            assert np.array_equal(got, exp), (dt, op, e)
+
+
+@pytest.mark.parametrize("strategy", [1, 2], ids=["direct", "tiled"])
+@pytest.mark.parametrize("dt", ["f32", "f64"])
+def test_float_add_collisions_tolerance(world, orc, lam, dt, strategy):
+    """Colliding float adds: exact with exactly representable values (1.0); random
+    values within |err| <= m * eps_mach * sum|terms| per element (m = updates)."""
+    k = world.team().kernels
+    k.reserve(1 << 20)
+    rng = np.random.default_rng(11)
+    t = NP[dt]
+    shard0 = np.zeros(3000, dtype=t)
+    idx = rng.integers(0, 3000, 120000).astype(np.uint64)
+    c = Case(k, orc, lam, dt, ADD, shard0, idx, np.ones(idx.size, dtype=t), "soa", strategy)
+    assert bits_equal(c.got, c.ref)
+    vals = rng.uniform(-1, 1, idx.size).astype(t)
+    c = Case(k, orc, lam, dt, ADD, shard0, idx, vals, "soa", strategy)
+    m = np.bincount(idx.astype(np.int64), minlength=3000)
+    mag = np.zeros(3000)
+    np.add.at(mag, idx.astype(np.int64), np.abs(vals.astype(np.float64)))
+    tol = m * np.finfo(t).eps * mag + np.finfo(t).tiny
+    assert np.all(np.abs(c.got.astype(np.float64) - c.ref.astype(np.float64)) <= tol)
+
+
+def test_pack_matches_oracle(world, orc, lam):
+    """lmr_pack: per-PE record streams == concatenation of the reference's op buffers."""
+    k = world.team().kernels
+    rng = np.random.default_rng(21)
+    import ctypes
+    from lamellar_runtime_amd import _capi
+    for npes, dist, size, sub in [(2, 0, 1000, None), (3, 1, 997, None), (4, 0, 100003, None),
+                                  (8, 1, 65536 * 3 + 5, None), (4, 0, 5000, (123, 4000)),
+                                  (3, 1, 5000, (7, 4444)), (8, 0, 7, None), (5, 0, 300000, None)]:
+        Lo = orc.layout_new(size, npes, 0, dist)
+        Ld = _capi.lmr_layout_t()
+        _capi.lib().lmr_layout_new(ctypes.byref(Ld), size, npes, 0, dist)
+        if sub:
+            Lo = orc.layout_sub(Lo, *sub)
+            Ld2 = _capi.lmr_layout_t()
+            _capi.lib().lmr_layout_sub(ctypes.byref(Ld), sub[0], sub[1], ctypes.byref(Ld2))
+            Ld = Ld2
+        assert Lo.as_tuple() == Ld.as_tuple()
+        n_len = Lo.size
+        iw = orc.index_size(Lo)
+        gidx = rng.integers(0, n_len, 20000).astype(np.uint64)
+        vals = rng.integers(0, 2**63, 20000).astype(np.uint64)
+        st, ams = orc.pack(Lo, CODE["u64"], np.uint64, gidx, vals, iw)
+        assert st == 0
+        dt_obj = lam.dtype_of("u64")
+        out_idx, out_vals, out_pos, counts = k.pack(Ld, to_dev(gidx).view(torch.int64), gidx.size,
+                                                    to_dev(vals), dt_obj, iw)
+        k.synchronize()
+        counts = counts.cpu().numpy()
+        oi = out_idx.cpu().numpy().view({1: np.uint8, 2: np.uint16, 4: np.uint32, 8: np.uint64}[iw])
+        ov = out_vals.cpu().numpy().view(np.uint64)
+        op_ = out_pos.cpu().numpy().view(np.uint32)
+        off = 0
+        rb, vo = orc.record_bytes(iw, CODE["u64"]), orc.record_val_offset(iw, CODE["u64"])
+        from opgen import record_dtype
+        for p in range(npes):
+            recs = [a for a in ams if a[0] == p]
+            if recs:
+                b = np.concatenate([a[1] for a in recs]).view(record_dtype(iw, "u64", rb, vo))
+                pos = np.concatenate([a[2] for a in recs])
+            else:
+                b = np.zeros(0, dtype=record_dtype(iw, "u64", rb, vo))
+                pos = np.zeros(0, dtype=np.uint64)
+            assert counts[p] == b.size
+            assert np.array_equal(oi[off:off + b.size], b["i"]), (npes, dist, p)
+            assert np.array_equal(ov[off:off + b.size], b["v"])
+            assert np.array_equal(op_[off:off + b.size].astype(np.uint64), pos)
+            off += b.size
+        assert k.errors() == 0
+
+
+def test_scatter_results(world):
+    k = world.team().kernels
+    rng = np.random.default_rng(2)
+    for eb, t in ((1, np.uint8), (2, np.uint16), (4, np.uint32), (8, np.uint64)):
+        n = 5000
+        pos = rng.permutation(n).astype(np.uint32)
+        vals = rng.integers(0, 200, n).astype(t)
+        ok = rng.integers(0, 2, n).astype(np.uint8)
+        out = torch.zeros(n * eb, dtype=torch.uint8, device="cuda")
+        ook = torch.zeros(n, dtype=torch.uint8, device="cuda")
+        k.scatter_results(to_dev(vals), to_dev(pos), n, eb, out, to_dev(ok), ook)
+        k.synchronize()
+        exp = np.zeros(n, dtype=t)
+        exp[pos] = vals
+        eok = np.zeros(n, dtype=np.uint8)
+        eok[pos] = ok
+        assert np.array_equal(out.cpu().numpy().view(t), exp)
+        assert np.array_equal(ook.cpu().numpy(), eok)
+
+
+@pytest.mark.parametrize("strategy", [1, 2], ids=["direct", "tiled"])
+def test_device_errors(world, lam, strategy):
+    """Where Rust panics the device raises the matching error bit and skips the record."""
+    k = world.team().kernels
+    k.reserve(1 << 20)
+    old = k.strategy
+    k.strategy = strategy
+    try:
+        dt = lam.dtype_of("i32")
+        shard = to_dev(np.array([10, -2**31, 5, 6], dtype=np.int32))
+        k.apply_soa(shard, 4, 1, dt, DIV, to_dev(np.array([0, 2], np.uint64)), 8,
+                    to_dev(np.array([0, 1], np.int32)), 0, 2)
+        assert k.errors() == 0x2
+        k.apply_soa(shard, 4, 1, dt, REM, to_dev(np.array([1], np.uint64)), 8,
+                    to_dev(np.array([-1], np.int32)), 0, 1)
+        assert k.errors() == 0x4
+        k.apply_soa(shard, 4, 1, dt, ADD, to_dev(np.array([4, 1 << 40], np.uint64)), 8,
+                    to_dev(np.array([1, 1], np.int32)), 0, 2)
+        assert k.errors() == 0x1
+        got = shard.cpu().numpy().view(np.int32)
+        assert list(got[:4]) == [10, -2**31, 5, 6]   # nothing applied
+        with pytest.raises(lam.LamellarError):
+            k.apply_soa(shard, 4, 2, lam.dtype_of("f32"), XOR, to_dev(np.array([0], np.uint64)), 8,
+                        to_dev(np.array([1], np.float32)), 0, 1)
+    finally:
+        k.strategy = old
