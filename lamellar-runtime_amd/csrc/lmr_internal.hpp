@@ -47,6 +47,10 @@ struct TiledWs {
     uint8_t* bin_val;      // [cap * 8]
     uint32_t* bin_pos;     // [cap]
     uint32_t* total;       // [1]
+    uint32_t* coarse_off;  // [kMaxTiles/128 * G + 1]  (two-level partition)
+    uint32_t* tmp_idx;     // [cap]
+    uint8_t* tmp_val;      // [cap * 8]
+    uint32_t* tmp_pos;     // [cap]
 };
 size_t tiled_ws_bytes(uint64_t cap);
 TiledWs carve_tiled_ws(uint8_t* base, uint64_t cap);

@@ -319,3 +319,42 @@ def test_device_errors(world, lam, strategy):
                         to_dev(np.array([1], np.float32)), 0, 1)
     finally:
         k.strategy = old
+
+
+@pytest.mark.parametrize("dt", ["u64", "u32", "u8", "i16", "i64", "f32", "f64"])
+def test_tiled_two_level_partition_bit_exact(world, orc, lam, dt):
+    """> 128 tiles: coarse + fine LDS-staged partition before the tile apply."""
+    k = world.team().kernels
+    k.reserve(1 << 21)
+    rng = np.random.default_rng(4321 + CODE[dt])
+    shard_len = (1 << 21) + 1234
+    for op in ops_for(dt):
+        shard0, idx, vals, cur, eps = _perm_inputs(dt, op, rng, shard_len, 1 << 20)
+        c = Case(k, orc, lam, dt, op, shard0, idx, vals, "soa", 2, cur=cur, eps=eps)
+        assert c.err == 0 and c.st_o == 0
+        assert bits_equal(c.got, c.ref), (dt, op)
+        if c.rk:
+            assert bits_equal(c.res_d, c.res_o), (dt, op)
+        if c.rk == 2:
+            assert np.array_equal(c.ok_d, c.ok_o)
+
+
+def test_tiled_two_level_collisions(world, orc, lam):
+    """Colliding u64 fetch_add over > 128 tiles: exact final state; each element's olds
+    are exactly init, init+1, ..., init+m-1 (v = 1)."""
+    k = world.team().kernels
+    k.reserve(1 << 22)
+    rng = np.random.default_rng(8)
+    shard_len = (1 << 21) + 5
+    shard0 = rng.integers(0, 2**62, shard_len, dtype=np.uint64)
+    idx = rng.integers(0, shard_len, 1 << 22).astype(np.uint64)
+    vals = np.ones(idx.size, dtype=np.uint64)
+    c = Case(k, orc, lam, "u64", FETCH_ADD, shard0, idx, vals, "soa", 2)
+    assert bits_equal(c.got, c.ref)
+    order = np.lexsort((c.res_d, idx))
+    si, so = idx[order], c.res_d[order]
+    first = np.ones(si.size, dtype=bool)
+    first[1:] = si[1:] != si[:-1]
+    grp_start = np.maximum.accumulate(np.where(first, np.arange(si.size), 0))
+    rank = np.arange(si.size) - grp_start
+    assert np.array_equal(so, shard0[si] + rank.astype(np.uint64))
