@@ -53,7 +53,7 @@ def parse():
     return p.parse_args()
 
 
-def stage_bytes_per_op(stage, iw, vb, eb, n, shard_len, fetch):
+def stage_bytes_per_op(stage, iw, vb, eb, n, shard_len, fetch, two_level=True):
     """Algorithmic HBM bytes per op of each kernel stage."""
     pos = 4 if fetch else 0
     res = eb if fetch else 0
@@ -61,12 +61,14 @@ def stage_bytes_per_op(stage, iw, vb, eb, n, shard_len, fetch):
         return iw + vb + 2 * eb + res
     if stage == "bin_count":
         return iw
-    if stage == "bin_scatter":
-        return iw + vb + 2 + vb + pos
+    if stage == "bin_scatter":      # coarse pass (two-level) or one-level scatter
+        return iw + vb + (4 + vb + pos if two_level else 2 + vb + pos)
     if stage == "tile_apply":
         return 2 + vb + pos + res + 2.0 * eb * shard_len / max(n, 1)
     if stage == "pack":
         return 8 + 8 + vb + iw + vb + 4
+    if stage == "fine_scatter":
+        return 4 + vb + pos + 2 + vb + pos
     if stage == "scatter_results":
         return 4 + 2 * eb
     return 0.0
@@ -184,7 +186,8 @@ def main():
                     roof["traffic"] = tr
             except Exception:
                 pass
-    apply_stages = [s for s in ("direct", "bin_count", "scan", "bin_scatter", "tile_apply") if s in per]
+    apply_stages = [s for s in ("direct", "bin_count", "scan", "bin_scatter", "fine_scatter", "tile_apply")
+                    if s in per]
     apply_ms = sum(per[s][0] * per[s][1] for s in apply_stages)
     survey_bpo = 4 + 8 + 16          # SURVEY.md §8(d) C2 B_op (u32 index, u64 value, element RMW)
 

@@ -15,6 +15,7 @@
 //                      read+write of the shard.
 #include "lmr_internal.hpp"
 #include "lmr_device.hpp"
+#include <stdlib.h>
 
 namespace lmr {
 
@@ -257,6 +258,9 @@ __device__ __forceinline__ void small_excl_scan(const uint32_t* hist, uint32_t* 
     }
 }
 
+// Both passes are software-pipelined: the next round's global loads are issued
+// into registers right after the current round is staged in LDS, so they are
+// in flight while the staged round is written out.
 template <int IW, int VB>
 __global__ __launch_bounds__(1024) void k_coarse_scatter(PartArgs p) {
     using V = typename idx_t<VB>::I;
@@ -270,21 +274,27 @@ __global__ __launch_bounds__(1024) void k_coarse_scatter(PartArgs p) {
     for (uint32_t c = threadIdx.x; c < C; c += blockDim.x) cursor[c] = p.coarse_off[uint64_t(c) * p.G + g];
     const uint64_t lo = uint64_t(g) * p.chunk;
     const uint64_t hi = min(lo + p.chunk, p.n);
-    for (uint64_t r0 = lo; r0 < hi; r0 += kRound) {
-        for (uint32_t c = threadIdx.x; c < C; c += blockDim.x) hist[c] = 0;
-        __syncthreads();
-        uint32_t m_idx[4], m_rank[4], m_c[4];
-        V m_val[4];
-        bool m_ok[4];
+    uint64_t m_raw[4];
+    V m_val[4];
+    auto load_round = [&](uint64_t r0) {
 #pragma unroll
         for (int j = 0; j < 4; j++) {
             const uint64_t k = r0 + uint64_t(j) * 1024 + threadIdx.x;
-            m_ok[j] = k < hi;
-            uint64_t idx = m_ok[j] ? load_idx<IW>(p.idx, p.idx_stride, k) : 0;
-            m_ok[j] = m_ok[j] && idx < p.shard_len;
-            m_idx[j] = uint32_t(idx);
-            m_val[j] = (m_ok[j] && p.val) ? *reinterpret_cast<const V*>(p.val + k * p.val_stride) : V(0);
-            m_c[j] = uint32_t(idx >> cshift);
+            const bool in = k < hi;
+            m_raw[j] = in ? load_idx<IW>(p.idx, p.idx_stride, k) : ~uint64_t(0);
+            m_val[j] = (in && p.val) ? *reinterpret_cast<const V*>(p.val + k * p.val_stride) : V(0);
+        }
+    };
+    load_round(lo);
+    for (uint64_t r0 = lo; r0 < hi; r0 += kRound) {
+        for (uint32_t c = threadIdx.x; c < C; c += blockDim.x) hist[c] = 0;
+        __syncthreads();
+        uint32_t m_rank[4], m_c[4];
+        bool m_ok[4];
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            m_ok[j] = m_raw[j] < p.shard_len;
+            m_c[j] = uint32_t(m_raw[j] >> cshift);
             if (m_ok[j]) m_rank[j] = atomicAdd(&hist[m_c[j]], 1u);
         }
         __syncthreads();
@@ -294,11 +304,12 @@ __global__ __launch_bounds__(1024) void k_coarse_scatter(PartArgs p) {
         for (int j = 0; j < 4; j++) {
             if (!m_ok[j]) continue;
             const uint32_t q = base[m_c[j]] + m_rank[j];
-            s_idx[q] = m_idx[j];
+            s_idx[q] = uint32_t(m_raw[j]);
             s_val[q] = m_val[j];
             s_pos[q] = uint32_t(r0 + uint64_t(j) * 1024 + threadIdx.x);
             s_c[q] = uint8_t(m_c[j]);
         }
+        if (r0 + kRound < hi) load_round(r0 + kRound);     // prefetch the next round
         __syncthreads();
         const uint32_t total = tot;
         for (uint32_t q = threadIdx.x; q < total; q += blockDim.x) {
@@ -313,6 +324,9 @@ __global__ __launch_bounds__(1024) void k_coarse_scatter(PartArgs p) {
     }
 }
 
+// Persistent over (coarse bucket c, producer block g) segments: block b takes
+// segments b, b + gridDim.x, ...; the first round of the next segment is
+// prefetched while the current segment's last round is written out.
 template <int VB>
 __global__ __launch_bounds__(1024) void k_fine_scatter(PartArgs p) {
     using V = typename idx_t<VB>::I;
@@ -321,54 +335,76 @@ __global__ __launch_bounds__(1024) void k_fine_scatter(PartArgs p) {
     __shared__ V s_val[kRound];
     __shared__ uint32_t s_pos[kRound];
     __shared__ uint8_t s_f[kRound];
-    const uint32_t cg = blockIdx.x;
-    const uint32_t c = cg / p.G, g = cg % p.G;
-    const uint32_t t0 = c * kFine;
-    const uint32_t nf = min(uint32_t(kFine), p.num_tiles - t0);
+    const uint32_t nseg = p.C * p.G;
     const uint32_t lmask = (1u << p.tile_shift) - 1u;
-    for (uint32_t f = threadIdx.x; f < nf; f += blockDim.x)
-        cursor[f] = p.fine_off[uint64_t(t0 + f) * p.G + g];
-    const uint32_t lo = p.coarse_off[cg], hi = p.coarse_off[cg + 1];
-    for (uint32_t r0 = lo; r0 < hi; r0 += kRound) {
-        for (uint32_t f = threadIdx.x; f < nf; f += blockDim.x) hist[f] = 0;
-        __syncthreads();
-        uint32_t m_l[4], m_rank[4], m_f[4], m_pos[4];
-        V m_val[4];
-        bool m_ok[4];
+    uint32_t m_idx[4], m_pos[4];
+    V m_val[4];
+    auto load_round = [&](uint32_t r0, uint32_t hi) {
 #pragma unroll
         for (int j = 0; j < 4; j++) {
             const uint32_t k = r0 + uint32_t(j) * 1024 + threadIdx.x;
-            m_ok[j] = k < hi;
-            const uint32_t idx = m_ok[j] ? p.tmp_idx[k] : 0u;
-            m_l[j] = idx & lmask;
-            m_f[j] = (idx >> p.tile_shift) - t0;
-            m_val[j] = (m_ok[j] && p.tmp_val) ? reinterpret_cast<const V*>(p.tmp_val)[k] : V(0);
-            m_pos[j] = (m_ok[j] && p.tmp_pos) ? p.tmp_pos[k] : 0u;
-            if (m_ok[j]) m_rank[j] = atomicAdd(&hist[m_f[j]], 1u);
+            const bool in = k < hi;
+            m_idx[j] = in ? p.tmp_idx[k] : 0xFFFFFFFFu;
+            m_val[j] = (in && p.tmp_val) ? reinterpret_cast<const V*>(p.tmp_val)[k] : V(0);
+            m_pos[j] = (in && p.tmp_pos) ? p.tmp_pos[k] : 0u;
         }
-        __syncthreads();
-        small_excl_scan(hist, base, nf, &tot);
-        __syncthreads();
+    };
+    uint32_t cg = blockIdx.x;
+    if (cg < nseg) load_round(p.coarse_off[cg], p.coarse_off[cg + 1]);
+    for (; cg < nseg; cg += gridDim.x) {
+        const uint32_t c = cg / p.G, g = cg % p.G;
+        const uint32_t t0 = c * kFine;
+        const uint32_t nf = min(uint32_t(kFine), p.num_tiles - t0);
+        const uint32_t lo = p.coarse_off[cg], hi = p.coarse_off[cg + 1];
+        if (lo == hi) {   // empty segment: its (all-invalid) prefetch is replaced by the next one's
+            if (cg + gridDim.x < nseg)
+                load_round(p.coarse_off[cg + gridDim.x], p.coarse_off[cg + gridDim.x + 1]);
+            continue;
+        }
+        for (uint32_t f = threadIdx.x; f < nf; f += blockDim.x)
+            cursor[f] = p.fine_off[uint64_t(t0 + f) * p.G + g];
+        for (uint32_t r0 = lo; r0 < hi; r0 += kRound) {
+            for (uint32_t f = threadIdx.x; f < nf; f += blockDim.x) hist[f] = 0;
+            __syncthreads();
+            uint32_t m_rank[4], m_f[4];
+            bool m_ok[4];
 #pragma unroll
-        for (int j = 0; j < 4; j++) {
-            if (!m_ok[j]) continue;
-            const uint32_t q = base[m_f[j]] + m_rank[j];
-            s_l[q] = uint16_t(m_l[j]);
-            s_val[q] = m_val[j];
-            s_pos[q] = m_pos[j];
-            s_f[q] = uint8_t(m_f[j]);
+            for (int j = 0; j < 4; j++) {
+                m_ok[j] = r0 + uint32_t(j) * 1024 + threadIdx.x < hi;
+                m_f[j] = (m_idx[j] >> p.tile_shift) - t0;
+                if (m_ok[j]) m_rank[j] = atomicAdd(&hist[m_f[j]], 1u);
+            }
+            __syncthreads();
+            small_excl_scan(hist, base, nf, &tot);
+            __syncthreads();
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                if (!m_ok[j]) continue;
+                const uint32_t q = base[m_f[j]] + m_rank[j];
+                s_l[q] = uint16_t(m_idx[j] & lmask);
+                s_val[q] = m_val[j];
+                s_pos[q] = m_pos[j];
+                s_f[q] = uint8_t(m_f[j]);
+            }
+            if (r0 + kRound < hi) {
+                load_round(r0 + kRound, hi);
+            } else if (cg + gridDim.x < nseg) {
+                const uint32_t nx = cg + gridDim.x;
+                load_round(p.coarse_off[nx], p.coarse_off[nx + 1]);
+            }
+            __syncthreads();
+            const uint32_t total = tot;
+            for (uint32_t q = threadIdx.x; q < total; q += blockDim.x) {
+                const uint32_t f = s_f[q];
+                const uint32_t dst = cursor[f] + q - base[f];
+                p.bin_lidx[dst] = s_l[q];
+                if (p.tmp_val) reinterpret_cast<V*>(p.bin_val)[dst] = s_val[q];
+                if (p.bin_pos) p.bin_pos[dst] = s_pos[q];
+            }
+            __syncthreads();
+            for (uint32_t f = threadIdx.x; f < nf; f += blockDim.x) cursor[f] += hist[f];
         }
         __syncthreads();
-        const uint32_t total = tot;
-        for (uint32_t q = threadIdx.x; q < total; q += blockDim.x) {
-            const uint32_t f = s_f[q];
-            const uint32_t dst = cursor[f] + q - base[f];
-            p.bin_lidx[dst] = s_l[q];
-            if (p.tmp_val) reinterpret_cast<V*>(p.bin_val)[dst] = s_val[q];
-            if (p.bin_pos) p.bin_pos[dst] = s_pos[q];
-        }
-        __syncthreads();
-        for (uint32_t f = threadIdx.x; f < nf; f += blockDim.x) cursor[f] += hist[f];
     }
 }
 
@@ -535,6 +571,23 @@ TiledWs carve_tiled_ws(uint8_t* base, uint64_t cap) {
     return w;
 }
 
+// Block counts of the partition passes (tunable for measurements through
+// LMR_BIN_BLOCKS / LMR_FINE_BLOCKS; defaults fill 256 CUs twice).
+static int env_int(const char* name, int dflt, int lo, int hi) {
+    const char* v = getenv(name);
+    if (!v || !*v) return dflt;
+    int x = atoi(v);
+    return x < lo ? lo : (x > hi ? hi : x);
+}
+static int bin_blocks_cap() {
+    static int v = env_int("LMR_BIN_BLOCKS", 512, 1, kMaxBinBlocks);
+    return v;
+}
+static int fine_blocks_cap() {
+    static int v = env_int("LMR_FINE_BLOCKS", 512, 1, 1 << 20);
+    return v;
+}
+
 // One tiled piece: a.n <= workspace capacity, a.n < 2^32.
 hipError_t launch_apply_tiled(int dtype, int index_size, const ApplyArgs& a, const TiledWs& w,
                               hipStream_t s) {
@@ -545,7 +598,7 @@ hipError_t launch_apply_tiled(int dtype, int index_size, const ApplyArgs& a, con
     const int vb = dtype_bytes(dtype);
     // G blocks: >= 64K records each, at most kMaxBinBlocks
     uint64_t G = (a.n + 65535) / 65536;
-    if (G > uint64_t(kMaxBinBlocks)) G = kMaxBinBlocks;
+    if (G > uint64_t(bin_blocks_cap())) G = bin_blocks_cap();
     if (G < 1) G = 1;
     BinArgs b;
     b.idx = a.idx; b.idx_stride = a.idx_stride;
@@ -576,7 +629,7 @@ hipError_t launch_apply_tiled(int dtype, int index_size, const ApplyArgs& a, con
     }
     if (num_tiles > uint64_t(kFine)) {
         // two-level LDS-staged partition: coarse buckets of kFine tiles, then tiles
-        ProfScope ps(a.prof, LMR_STAGE_BIN_SCATTER, s);
+        if (a.prof) prof_begin(a.prof, LMR_STAGE_BIN_SCATTER, s);
         PartArgs q;
         q.idx = a.idx; q.idx_stride = a.idx_stride; q.val = a.val; q.val_stride = a.val_stride;
         q.n = a.n; q.shard_len = a.shard_len; q.chunk = b.chunk; q.tile_shift = shift;
@@ -598,8 +651,11 @@ hipError_t launch_apply_tiled(int dtype, int index_size, const ApplyArgs& a, con
             }
             return hipGetLastError();
         });
+        if (a.prof) prof_end(a.prof, LMR_STAGE_BIN_SCATTER, s);
         if (e != hipSuccess) return e;
-        const unsigned fgrid = unsigned(uint64_t(q.C) * G);
+        ProfScope pf(a.prof, LMR_STAGE_FINE_SCATTER, s);
+        const uint64_t nseg = uint64_t(q.C) * G;
+        const unsigned fgrid = unsigned(nseg < uint64_t(fine_blocks_cap()) ? nseg : fine_blocks_cap());
         switch (vb) {
         case 1: hipLaunchKernelGGL((k_fine_scatter<1>), dim3(fgrid), dim3(1024), 0, s, q); break;
         case 2: hipLaunchKernelGGL((k_fine_scatter<2>), dim3(fgrid), dim3(1024), 0, s, q); break;
