@@ -228,8 +228,8 @@ def main():
         out["cpu_baseline"] = cpu_baseline(args, args.elems_log2)
     if me == 0:
         print(json.dumps(out), flush=True)
-    if npes > 1:
-        import torch.distributed as dist
+    import torch.distributed as dist
+    if dist.is_available() and dist.is_initialized():
         dist.barrier()
         dist.destroy_process_group()
 

@@ -22,12 +22,18 @@ AMs are one-sided.
 from __future__ import annotations
 
 import numbers
+import os
 
 import numpy as np
 import torch
 
 from .kernels import LamellarError
 from .types import RET_KIND, BatchReturnType, DType, LmrStatus, op_supported
+
+
+# Route 1-PE batches through the exchange step too (rehearses the RCCL calls of
+# the multi-GPU path on a one-GPU box); off by default.
+_FORCE_EXCHANGE = os.environ.get("LAMELLAR_FORCE_EXCHANGE", "0") == "1"
 
 
 class BatchResult:
@@ -126,7 +132,7 @@ def run_batch(arr, op, index, val, current=None, eps=None) -> BatchResult:
     results = k.empty(n, dt.torch) if ret != BatchReturnType.None_ else None
     ok = k.empty(n, torch.uint8) if ret == BatchReturnType.Result else None
     mvsi = (i_len == 1 and v_len > 1)
-    if team.num_pes() == 1:
+    if team.num_pes() == 1 and not _FORCE_EXCHANGE:
         _local(arr, k, dt, op, i_scalar, idx, v_scalar, vals, n, mvsi, results, ok, cmp_bits, eps_bits)
     else:
         _distributed(arr, k, dt, op, ret, i_scalar, idx, v_scalar, vals, n, mvsi, results, ok,

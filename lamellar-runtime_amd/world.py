@@ -53,7 +53,7 @@ class LamellarTeam:
     # ---- exchange step (collective) ----
     def alltoall_header(self, send: torch.Tensor) -> torch.Tensor:
         """send: int64 [num_pes, k] (row p goes to PE p) -> recv int64 [num_pes, k]."""
-        if self._num_pes == 1:
+        if not self._collective():
             return send.clone()
         s = send.to(self.comm_device).contiguous()
         r = torch.empty_like(s)
@@ -63,7 +63,7 @@ class LamellarTeam:
     def alltoallv(self, send: torch.Tensor, send_splits, recv_splits) -> torch.Tensor:
         """Byte / element all-to-all-v of a 1-D tensor with per-PE split sizes."""
         total = int(sum(recv_splits))
-        if self._num_pes == 1:
+        if not self._collective():
             return send[:total].clone()
         dev = send.device
         s = send.to(self.comm_device).contiguous()
@@ -71,6 +71,11 @@ class LamellarTeam:
         dist.all_to_all_single(r, s, output_split_sizes=[int(x) for x in recv_splits],
                                input_split_sizes=[int(x) for x in send_splits], group=self.group)
         return r.to(dev)
+
+    def _collective(self):
+        # a 1-PE world still goes through the collective when a process group
+        # exists (LAMELLAR_FORCE_EXCHANGE rehearsal of the RCCL calls)
+        return self._num_pes > 1 or (dist.is_available() and dist.is_initialized())
 
     def all_gather_object(self, obj):
         if self._num_pes == 1:
@@ -145,11 +150,13 @@ class LamellarWorldBuilder:
         if device.type == "cuda":
             torch.cuda.set_device(device)
         group = None
-        if world_size > 1:
+        force = os.environ.get("LAMELLAR_FORCE_EXCHANGE", "0") == "1"
+        if world_size > 1 or force:
             if not dist.is_initialized():
                 os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
                 os.environ.setdefault("MASTER_PORT", "29511")
-                backend = "nccl" if device.type == "cuda" else "gloo"
+                backend = os.environ.get("LAMELLAR_COMM_BACKEND") or \
+                    ("nccl" if device.type == "cuda" else "gloo")
                 kw = {"device_id": device} if backend == "nccl" else {}
                 dist.init_process_group(backend, rank=rank, world_size=world_size, **kw)
             group = dist.group.WORLD
