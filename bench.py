@@ -50,6 +50,8 @@ def parse():
     p.add_argument("--cpu-sample-log2", type=int, default=24)
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-verify", action="store_true")
+    p.add_argument("--e2e", action="store_true",
+                   help="also time the host-buffer path: pinned host records -> H2D copy -> apply")
     return p.parse_args()
 
 
@@ -224,6 +226,32 @@ def main():
         "verified": verified,
         "cpu_baseline": None,
     }
+    if args.e2e:
+        # records originate in host memory (the lamellae's buffers): PCIe-inclusive rate
+        idx_h = idx.cpu().pin_memory()
+        vals_h = vals.cpu().pin_memory()
+        idx_d, vals_d = torch.empty_like(idx), torch.empty_like(vals)
+        fetch = lam.AtomicArray(team, global_len, lam.Distribution.Block, "u64")
+        olds_h = torch.empty(n, dtype=torch.int64).pin_memory()
+        world.barrier()
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            idx_d.copy_(idx_h, non_blocking=True)
+            vals_d.copy_(vals_h, non_blocking=True)
+            arr.batch_add(idx_d, vals_d).spawn()
+        torch.cuda.synchronize(dev)
+        t1 = time.perf_counter()
+        for _ in range(args.steps):
+            idx_d.copy_(idx_h, non_blocking=True)
+            vals_d.copy_(vals_h, non_blocking=True)
+            h = fetch.batch_fetch_add(idx_d, vals_d)
+            olds_h.copy_(h.spawn()._res.vals, non_blocking=True)
+        torch.cuda.synchronize(dev)
+        t2 = time.perf_counter()
+        out["e2e"] = {"batch_add_ops_per_s": npes * n * args.steps / (t1 - t0),
+                      "batch_fetch_add_ops_per_s": npes * n * args.steps / (t2 - t1),
+                      "note": "pinned host idx+vals -> H2D -> device op (-> D2H olds for fetch_add)"}
     if me == 0 and npes == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(args, args.elems_log2)
     if me == 0:
