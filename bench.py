@@ -2,13 +2,18 @@
 """Benchmark of the MI355X batched element-op path (BASELINE.json metric:
 "batched array ops applied/sec (device-resident), 1/2/4/8 MI355X").
 
-A step = one `AtomicArray<u64>::batch_add(indices, vals)` over one batch of
-synthetic device-resident input, every PE (one per GPU) issuing its own batch:
-  N = 1 : C2 — 2^28 u64 add records, uniform-random global indices into a
-          2^26-element array (the local lamellae: no pack, no exchange);
-  N > 1 : C4 — the same batch per PE (weak scaling), indices uniform over the
-          whole N * 2^26-element Block array: device pack by destination PE ->
-          RCCL all-to-all(v) over xGMI -> device apply on every shard.
+A step = one pass of the hot path over one batch of synthetic device-resident
+input, every PE (one per GPU) issuing its own batch (weak scaling):
+  c2 (default, N = 1): AtomicArray<u64>::batch_add(indices, vals), 2^28
+      records, uniform-random global indices into a 2^26-element array; the
+      local lamellae: no pack, no exchange.
+  c4 (default, N > 1): the same batch per PE, indices uniform over the whole
+      N * 2^26-element Block array: device pack by destination PE -> RCCL
+      all-to-all(v) over xGMI -> device apply on every shard.
+  c3: AtomicArray<f64>::batch_fetch_add, 2^26 records, Zipf(0.99) ranks over
+      2^24 elements (ranks randomly permuted), vals = 1.0, olds returned.
+  c5: AtomicArray<u32>, five batches per step (bit_and, bit_or, bit_xor, swap,
+      compare_exchange), 2^30 / 8 records per PE split in equal fifths.
 value = ops applied by all PEs / max-over-PEs wall time of the timed steps.
 
 roofline: the dominant kernel's algorithmic HBM bytes per launch / its average
@@ -17,7 +22,7 @@ the 8.0 TB/s HBM3E peak. cpu_baseline: the reference-structured threaded CPU
 apply (oracle/cpu_baseline.c, a restatement of the Rust path: the reference
 itself cannot be built here) on a bounded sample, rank 0, N = 1.
 
-Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c3|c5]
        python -m torch.distributed.run --nproc-per-node N bench.py --gpus N ...
 """
 import argparse
@@ -43,37 +48,182 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=10)
     p.add_argument("--warmup", type=int, default=3)
-    p.add_argument("--records-log2", type=int, default=28)
-    p.add_argument("--elems-log2", type=int, default=26)
+    p.add_argument("--config", default=None, choices=[None, "c2", "c3", "c4", "c5"])
+    p.add_argument("--records-log2", type=int, default=None)
+    p.add_argument("--elems-log2", type=int, default=None)
     p.add_argument("--strategy", default=os.environ.get("LAMELLAR_OP_STRATEGY", "auto"))
     p.add_argument("--cpu-threads", type=int, default=16)
     p.add_argument("--cpu-sample-log2", type=int, default=24)
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-verify", action="store_true")
     p.add_argument("--e2e", action="store_true",
-                   help="also time the host-buffer path: pinned host records -> H2D copy -> apply")
+                   help="also time the host-buffer path: pinned host records -> H2D copy -> op")
     return p.parse_args()
 
 
-def stage_bytes_per_op(stage, iw, vb, eb, n, shard_len, fetch, two_level=True):
-    """Algorithmic HBM bytes per op of each kernel stage."""
+def stage_bytes_per_op(stage, iw, vb, eb, n, shard_len, fetch):
+    """Algorithmic HBM bytes per op of each kernel stage (Kernels):
+    the bytes a stage must read and write per record, shard traffic amortised."""
     pos = 4 if fetch else 0
     res = eb if fetch else 0
-    if stage == "direct":
-        return iw + vb + 2 * eb + res
-    if stage == "bin_count":
-        return iw
-    if stage == "bin_scatter":      # coarse pass (two-level) or one-level scatter
-        return iw + vb + (4 + vb + pos if two_level else 2 + vb + pos)
-    if stage == "tile_apply":
-        return 2 + vb + pos + res + 2.0 * eb * shard_len / max(n, 1)
-    if stage == "pack":
-        return 8 + 8 + vb + iw + vb + 4
-    if stage == "fine_scatter":
-        return 4 + vb + pos + 2 + vb + pos
-    if stage == "scatter_results":
-        return 4 + 2 * eb
-    return 0.0
+    return {
+        "direct": iw + vb + 2 * eb + res,
+        "bin_count": iw,
+        "bin_scatter": iw + vb + 4 + vb + pos,          # coarse pass: record in, temp record out
+        "fine_scatter": 4 + vb + pos + 2 + vb + pos,    # temp record in, tile-local record out
+        "tile_apply": 2 + vb + pos + res + 2.0 * eb * shard_len / max(n, 1),
+        "pack": 8 + 8 + vb + iw + vb + 4,
+        "scatter_results": 4 + 2 * eb,
+        "mvsi": vb + res,
+    }.get(stage, 0.0)
+
+
+class Workload:
+    """One BASELINE.json configuration: array + inputs + the step."""
+
+    def __init__(self, lam, team, args):
+        self.lam, self.team, self.args = lam, team, args
+        self.k = team.kernels
+        self.dev = self.k.device
+        self.npes, self.me = team.num_pes(), team.my_pe()
+
+    def gen(self):
+        g = torch.Generator(device=self.dev)
+        g.manual_seed(0x1A3E11A2 + self.me)
+        return g
+
+
+class AddUniform(Workload):
+    """C2 (N = 1) / C4 (N > 1): u64 batch_add, uniform indices."""
+    dtype, fetch, eb, vb = "u64", False, 8, 8
+
+    def setup(self):
+        a = self.args
+        self.n = 1 << (a.records_log2 or 28)
+        self.elems = 1 << (a.elems_log2 or 26)
+        glen = self.elems * self.npes
+        self.arr = self.lam.AtomicArray(self.team, glen, self.lam.Distribution.Block, "u64")
+        g = self.gen()
+        self.idx = torch.randint(0, glen, (self.n,), dtype=torch.int64, device=self.dev, generator=g)
+        self.vals = torch.randint(-2**63, 2**63 - 1, (self.n,), dtype=torch.int64, device=self.dev, generator=g)
+        self.ops_per_step = self.n
+
+    def step(self):
+        self.arr.batch_add(self.idx, self.vals).spawn()
+
+    def verify(self, nsteps):
+        # wrapping-sum invariant: sum(array) == steps * sum(vals), over all PEs (mod 2^64)
+        s_arr = self.arr.local_data().sum(dtype=torch.int64)
+        s_val = self.vals.sum(dtype=torch.int64) * nsteps
+        return _allsum(self.npes, s_arr) == _allsum(self.npes, s_val)
+
+    def describe(self):
+        a = self.args
+        if self.npes == 1:
+            return ("C2: 2^%d batched u64 add records, uniform-random indices into a 2^%d-element "
+                    "AtomicArray<u64>" % (a.records_log2 or 28, a.elems_log2 or 26))
+        return ("C4: %d PEs all-to-all batched u64 add, 2^%d records per PE, Block array of %d x 2^%d "
+                "elements, op buffers via RCCL all-to-all(v) over xGMI"
+                % (self.npes, a.records_log2 or 28, self.npes, a.elems_log2 or 26))
+
+    op_name = "batch_add (ArrayOpCmd::Add, MVMI)"
+    survey_bpo = 4 + 8 + 16
+
+
+class FetchAddZipf(Workload):
+    """C3: f64 batch_fetch_add, Zipf(0.99) over 2^24 elements (contention)."""
+    dtype, fetch, eb, vb = "f64", True, 8, 8
+
+    def setup(self):
+        a = self.args
+        self.n = 1 << (a.records_log2 or 26)
+        self.elems = 1 << (a.elems_log2 or 24)
+        glen = self.elems * self.npes
+        self.arr = self.lam.AtomicArray(self.team, glen, self.lam.Distribution.Block, "f64")
+        g = self.gen()
+        ranks = torch.arange(1, glen + 1, dtype=torch.float64, device=self.dev)
+        cdf = torch.cumsum(ranks.pow(-0.99), 0)
+        cdf /= cdf[-1].clone()
+        u = torch.rand(self.n, dtype=torch.float64, device=self.dev, generator=g)
+        r = torch.searchsorted(cdf, u).clamp_(max=glen - 1)
+        g2 = torch.Generator(device=self.dev)
+        g2.manual_seed(0xC3)                                   # same rank->index map on every PE
+        perm = torch.randperm(glen, device=self.dev, generator=g2)
+        self.idx = perm[r].contiguous()
+        self.vals = torch.ones(self.n, dtype=torch.float64, device=self.dev)
+        self.ops_per_step = self.n
+        self.top_share = float((r == 0).float().mean())
+
+    def step(self):
+        self.last = self.arr.batch_fetch_add(self.idx, self.vals).spawn()
+
+    def verify(self, nsteps):
+        # exact with vals = 1.0: element = steps * (records hitting it, all PEs)
+        cnt = torch.bincount(self.idx, minlength=self.elems * self.npes).to(torch.float64) * nsteps
+        if self.npes > 1:
+            import torch.distributed as dist
+            dist.all_reduce(cnt)
+        L = self.arr.local_data()
+        lo = self.me * self.elems
+        return bool(torch.equal(L, cnt[lo:lo + L.numel()]))
+
+    def describe(self):
+        a = self.args
+        return ("C3: f64 fetch_add, 2^%d records per PE, Zipf(0.99) ranks (randomly permuted) over "
+                "2^%d elements per PE, vals = 1.0, olds returned in input order (top element %.1f%% of "
+                "records)" % (a.records_log2 or 26, a.elems_log2 or 24, 100 * self.top_share))
+
+    op_name = "batch_fetch_add (ArrayOpCmd::FetchAdd, MVMI)"
+    survey_bpo = 4 + 8 + 16 + 8
+
+
+class MixedU32(Workload):
+    """C5: u32 and/or/xor/swap/compare_exchange in equal fifths, one batch each."""
+    dtype, fetch, eb, vb = "u32", True, 4, 4
+
+    def setup(self):
+        a = self.args
+        total = 1 << (a.records_log2 or 30)
+        self.n = max(5, total // 8)                               # 2^30 total over 8 PEs
+        self.elems = 1 << (a.elems_log2 or 26)
+        glen = self.elems * self.npes
+        self.arr = self.lam.AtomicArray(self.team, glen, self.lam.Distribution.Block, "u32")
+        g = self.gen()
+        m = self.n // 5
+        self.parts = []
+        for _ in range(5):
+            i = torch.randint(0, glen, (m,), dtype=torch.int64, device=self.dev, generator=g)
+            v = torch.randint(-2**31, 2**31 - 1, (m,), dtype=torch.int32, device=self.dev, generator=g)
+            self.parts.append((i, v))
+        self.ops_per_step = 5 * m
+
+    def step(self):
+        a = self.arr
+        (i0, v0), (i1, v1), (i2, v2), (i3, v3), (i4, v4) = self.parts
+        a.batch_bit_and(i0, v0).spawn()
+        a.batch_bit_or(i1, v1).spawn()
+        a.batch_bit_xor(i2, v2).spawn()
+        a.batch_swap(i3, v3).spawn()
+        a.batch_compare_exchange(i4, 0, v4).spawn()
+
+    def verify(self, nsteps):
+        return None
+
+    def describe(self):
+        a = self.args
+        return ("C5: u32 bit_and/bit_or/bit_xor/swap/compare_exchange(current=0) in five equal batches, "
+                "2^%d records in total over 8 PEs (2^%d per PE), 2^%d-element shard per PE"
+                % (a.records_log2 or 30, (a.records_log2 or 30) - 3, a.elems_log2 or 26))
+
+    op_name = "batch_bit_and/or/xor, batch_swap, batch_compare_exchange"
+    survey_bpo = (16 + 16 + 16 + 20 + 24) / 5
+
+
+def _allsum(npes, t):
+    if npes > 1:
+        import torch.distributed as dist
+        dist.all_reduce(t)
+    return int(t.item())
 
 
 def cpu_baseline(args, elems_log2):
@@ -115,19 +265,14 @@ def main():
     k = team.kernels
     npes, me = world.num_pes(), world.my_pe()
     dev = k.device
-    n = 1 << args.records_log2
-    elems_per_pe = 1 << args.elems_log2
-    global_len = elems_per_pe * npes
-    arr = lam.AtomicArray(team, global_len, lam.Distribution.Block, "u64")
-    g = torch.Generator(device=dev)
-    g.manual_seed(0x1A3E11A2 + me)
-    idx = torch.randint(0, global_len, (n,), dtype=torch.int64, device=dev, generator=g)
-    vals = torch.randint(-2**63, 2**63 - 1, (n,), dtype=torch.int64, device=dev, generator=g)
-    k.reserve(n)
+    cfg = args.config or ("c2" if npes == 1 else "c4")
+    W = {"c2": AddUniform, "c4": AddUniform, "c3": FetchAddZipf, "c5": MixedU32}[cfg](lam, team, args)
+    W.setup()
+    k.reserve(W.n)
     world.barrier()
 
     for _ in range(args.warmup):
-        arr.batch_add(idx, vals).spawn()
+        W.step()
     world.wait_all()
     k.profile(True)
     k.profile_read(reset=True)
@@ -135,7 +280,7 @@ def main():
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        arr.batch_add(idx, vals).spawn()
+        W.step()
     torch.cuda.synchronize(dev)
     world.barrier()
     t1 = time.perf_counter()
@@ -150,22 +295,11 @@ def main():
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
     ms_per_step = elapsed / args.steps * 1e3
-    value = npes * n * args.steps / elapsed
-
-    verified = None
-    if not args.no_verify:
-        # wrapping-sum invariant: sum(array) == (W + K) * sum(vals) over all PEs (mod 2^64)
-        s_arr = arr.local_data().sum(dtype=torch.int64)
-        s_val = vals.sum(dtype=torch.int64) * (args.warmup + args.steps)
-        if npes > 1:
-            import torch.distributed as dist
-            dist.all_reduce(s_arr)
-            dist.all_reduce(s_val)
-        verified = bool(int(s_arr.item()) == int(s_val.item()))
+    value = npes * W.ops_per_step * args.steps / elapsed
+    verified = None if args.no_verify else W.verify(args.warmup + args.steps)
 
     # ---- roofline of the dominant kernel ----
-    iw = 8 if npes == 1 else arr.index_size()
-    recv_n = n  # uniform indices: each PE receives ~n records
+    iw = 8 if npes == 1 else W.arr.index_size()
     per = {}
     for name, (ms, cnt) in stages.items():
         if cnt:
@@ -174,24 +308,20 @@ def main():
     roof = None
     if dom:
         avg_ms, launches_per_step = per[dom]
-        ops_per_launch = recv_n / launches_per_step if dom != "scan" else recv_n
-        bpo = stage_bytes_per_op(dom, iw, 8, 8, ops_per_launch, elems_per_pe, False)
+        ops_per_launch = W.ops_per_step / launches_per_step
+        bpo = stage_bytes_per_op(dom, iw, W.vb, W.eb, ops_per_launch, W.elems, W.fetch)
         achieved = bpo * ops_per_launch / (avg_ms * 1e-3)
         roof = {"bound": "hbm", "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
                 "frac": achieved / HBM_PEAK, "traffic": None, "kernel": dom,
                 "bytes_per_op": bpo, "avg_launch_ms": avg_ms}
-        pmc = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+        pmc = os.path.join(ROOT, "profiles", f"pmc_traffic_{cfg}.json")
         if os.path.exists(pmc):
-            try:
-                tr = json.load(open(pmc)).get(dom)
-                if tr:
-                    roof["traffic"] = tr
-            except Exception:
-                pass
-    apply_stages = [s for s in ("direct", "bin_count", "scan", "bin_scatter", "fine_scatter", "tile_apply")
-                    if s in per]
+            tr = json.load(open(pmc)).get(dom)
+            if tr:
+                roof["traffic"] = tr
+    apply_stages = [s for s in ("direct", "mvsi", "bin_count", "scan", "bin_scatter", "fine_scatter",
+                                "tile_apply") if s in per]
     apply_ms = sum(per[s][0] * per[s][1] for s in apply_stages)
-    survey_bpo = 4 + 8 + 16          # SURVEY.md §8(d) C2 B_op (u32 index, u64 value, element RMW)
 
     out = {
         "metric": METRIC,
@@ -204,62 +334,64 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "u64",
-        "data": "synthetic (seeded uniform-random u64 indices and values, device-resident)",
+        "dtype": W.dtype,
+        "data": "synthetic (seeded random indices and values, device-resident)",
         "config": {
-            "workload": ("C2: 2^%d batched u64 add records, uniform-random indices into a 2^%d-element "
-                         "AtomicArray<u64>" % (args.records_log2, args.elems_log2)) if npes == 1 else
-                        ("C4: %d PEs all-to-all batched u64 add, 2^%d records per PE, Block array of "
-                         "%d x 2^%d elements, op buffers via RCCL all-to-all(v) over xGMI"
-                         % (npes, args.records_log2, npes, args.elems_log2)),
-            "records_per_pe": n,
-            "elems_per_pe": elems_per_pe,
-            "op": "batch_add (ArrayOpCmd::Add, MVMI)",
+            "workload": W.describe(),
+            "records_per_pe": W.ops_per_step,
+            "elems_per_pe": W.elems,
+            "op": W.op_name,
             "strategy": args.strategy,
             "parallelism": f"{npes} PE(s), one per GPU",
         },
         "roofline": roof,
         "apply_pipeline": {"stages_ms_per_step": {s: per[s][0] * per[s][1] for s in per},
                            "apply_ms_per_step": apply_ms,
-                           "survey_bytes_per_op": survey_bpo,
-                           "survey_frac": (survey_bpo * n / (apply_ms * 1e-3) / HBM_PEAK) if apply_ms else None},
+                           "survey_bytes_per_op": W.survey_bpo,
+                           "survey_frac": (W.survey_bpo * W.ops_per_step / (apply_ms * 1e-3) / HBM_PEAK)
+                           if apply_ms else None},
         "verified": verified,
         "cpu_baseline": None,
     }
-    if args.e2e:
-        # records originate in host memory (the lamellae's buffers): PCIe-inclusive rate
-        idx_h = idx.cpu().pin_memory()
-        vals_h = vals.cpu().pin_memory()
-        idx_d, vals_d = torch.empty_like(idx), torch.empty_like(vals)
-        fetch = lam.AtomicArray(team, global_len, lam.Distribution.Block, "u64")
-        olds_h = torch.empty(n, dtype=torch.int64).pin_memory()
-        world.barrier()
-        torch.cuda.synchronize(dev)
-        t0 = time.perf_counter()
-        for _ in range(args.steps):
-            idx_d.copy_(idx_h, non_blocking=True)
-            vals_d.copy_(vals_h, non_blocking=True)
-            arr.batch_add(idx_d, vals_d).spawn()
-        torch.cuda.synchronize(dev)
-        t1 = time.perf_counter()
-        for _ in range(args.steps):
-            idx_d.copy_(idx_h, non_blocking=True)
-            vals_d.copy_(vals_h, non_blocking=True)
-            h = fetch.batch_fetch_add(idx_d, vals_d)
-            olds_h.copy_(h.spawn()._res.vals, non_blocking=True)
-        torch.cuda.synchronize(dev)
-        t2 = time.perf_counter()
-        out["e2e"] = {"batch_add_ops_per_s": npes * n * args.steps / (t1 - t0),
-                      "batch_fetch_add_ops_per_s": npes * n * args.steps / (t2 - t1),
-                      "note": "pinned host idx+vals -> H2D -> device op (-> D2H olds for fetch_add)"}
-    if me == 0 and npes == 1 and not args.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline(args, args.elems_log2)
+    if args.e2e and cfg in ("c2", "c4"):
+        out["e2e"] = e2e(lam, team, W, args)
+    if me == 0 and npes == 1 and not args.no_cpu_baseline and cfg == "c2":
+        out["cpu_baseline"] = cpu_baseline(args, args.elems_log2 or 26)
     if me == 0:
         print(json.dumps(out), flush=True)
     import torch.distributed as dist
     if dist.is_available() and dist.is_initialized():
         dist.barrier()
         dist.destroy_process_group()
+
+
+def e2e(lam, team, W, args):
+    """Records originate in host memory (the lamellae's buffers): PCIe-inclusive rates."""
+    dev = W.dev
+    idx_h = W.idx.cpu().pin_memory()
+    vals_h = W.vals.cpu().pin_memory()
+    idx_d, vals_d = torch.empty_like(W.idx), torch.empty_like(W.vals)
+    fetch = lam.AtomicArray(team, W.elems * W.npes, lam.Distribution.Block, "u64")
+    olds_h = torch.empty(W.n, dtype=torch.int64).pin_memory()
+    team.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        idx_d.copy_(idx_h, non_blocking=True)
+        vals_d.copy_(vals_h, non_blocking=True)
+        W.arr.batch_add(idx_d, vals_d).spawn()
+    torch.cuda.synchronize(dev)
+    t1 = time.perf_counter()
+    for _ in range(args.steps):
+        idx_d.copy_(idx_h, non_blocking=True)
+        vals_d.copy_(vals_h, non_blocking=True)
+        h = fetch.batch_fetch_add(idx_d, vals_d).spawn()
+        olds_h.copy_(h._res.vals, non_blocking=True)
+    torch.cuda.synchronize(dev)
+    t2 = time.perf_counter()
+    return {"batch_add_ops_per_s": W.npes * W.n * args.steps / (t1 - t0),
+            "batch_fetch_add_ops_per_s": W.npes * W.n * args.steps / (t2 - t1),
+            "note": "pinned host idx+vals -> H2D -> device op (-> D2H olds for fetch_add), u64"}
 
 
 if __name__ == "__main__":
