@@ -16,6 +16,7 @@
 #include "lmr_internal.hpp"
 #include "lmr_device.hpp"
 #include <stdlib.h>
+#include <algorithm>
 
 namespace lmr {
 
@@ -408,6 +409,41 @@ __global__ __launch_bounds__(1024) void k_fine_scatter(PartArgs p) {
     }
 }
 
+// ---- tile work plan --------------------------------------------------------
+// Most tiles are one work item in "owner" mode (one workgroup stages the tile
+// in LDS, applies every record, writes the tile back). A tile with far more
+// records than average (skewed streams, e.g. Zipf 0.99: ~5 % of all records on
+// one element) is split into kSplit-record items in "delta" mode when the op
+// combines (add/sub/and/or/xor and their fetch forms): each workgroup combines
+// its records in an LDS delta tile (identity-initialised), then applies one
+// device-scope atomic per touched element; fetch results are the returned base
+// combined with the record's LDS prefix — a valid linearisation with each
+// workgroup's records applied as one block.
+constexpr uint32_t kSplit = 16 * 1024;     // records per delta item (16 per thread)
+
+struct TileItem { uint32_t tile, lo, hi, mode; };
+
+__global__ void k_tile_plan_count(const uint32_t* tile_start, uint32_t num_tiles, uint32_t thresh,
+                                  int combinable, uint32_t* tile_items) {
+    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= num_tiles) return;
+    const uint32_t c = tile_start[t + 1] - tile_start[t];
+    tile_items[t] = (c == 0) ? 0u : ((combinable && c > thresh) ? (c + kSplit - 1) / kSplit : 1u);
+}
+
+__global__ void k_tile_plan_fill(const uint32_t* tile_start, uint32_t num_tiles, const uint32_t* item_base,
+                                 const uint32_t* tile_items, TileItem* items) {
+    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= num_tiles) return;
+    const uint32_t m = tile_items[t], b = item_base[t];
+    const uint32_t lo = tile_start[t], hi = tile_start[t + 1];
+    if (m == 1) { items[b] = TileItem{t, lo, hi, 0u}; return; }
+    for (uint32_t j = 0; j < m; j++) {
+        const uint32_t l = lo + j * kSplit;
+        items[b + j] = TileItem{t, l, min(hi, l + kSplit), 1u};
+    }
+}
+
 struct TileArgs {
     void* shard;
     uint64_t shard_len;
@@ -419,7 +455,8 @@ struct TileArgs {
     uint64_t eps_bits;
     uint64_t val_bits;       // scalar value (SVMI)
     bool scalar;
-    const uint32_t* tile_start;
+    const TileItem* items;
+    const uint32_t* item_count;
     const uint16_t* bin_lidx;
     const uint8_t* bin_val;
     const uint32_t* bin_pos;
@@ -428,7 +465,51 @@ struct TileArgs {
     uint32_t* err;
 };
 
+__host__ __device__ constexpr bool op_combines(int op) {
+    return op == LMR_OP_ADD || op == LMR_OP_FETCH_ADD || op == LMR_OP_SUB || op == LMR_OP_FETCH_SUB ||
+           op == LMR_OP_AND || op == LMR_OP_FETCH_AND || op == LMR_OP_OR || op == LMR_OP_FETCH_OR ||
+           op == LMR_OP_XOR || op == LMR_OP_FETCH_XOR;
+}
+
+// delta mode: how records accumulate in LDS, how the block's delta reaches
+// global memory, and how a record's old value is rebuilt from the base.
+__device__ __forceinline__ int delta_acc_op(int op) {
+    switch (op) {
+    case LMR_OP_ADD: case LMR_OP_FETCH_ADD: case LMR_OP_SUB: case LMR_OP_FETCH_SUB: return LMR_OP_FETCH_ADD;
+    case LMR_OP_AND: case LMR_OP_FETCH_AND: return LMR_OP_FETCH_AND;
+    case LMR_OP_OR: case LMR_OP_FETCH_OR: return LMR_OP_FETCH_OR;
+    default: return LMR_OP_FETCH_XOR;
+    }
+}
+__device__ __forceinline__ int delta_global_op(int op) {
+    switch (op) {
+    case LMR_OP_ADD: case LMR_OP_FETCH_ADD: return LMR_OP_FETCH_ADD;
+    case LMR_OP_SUB: case LMR_OP_FETCH_SUB: return LMR_OP_FETCH_SUB;
+    case LMR_OP_AND: case LMR_OP_FETCH_AND: return LMR_OP_FETCH_AND;
+    case LMR_OP_OR: case LMR_OP_FETCH_OR: return LMR_OP_FETCH_OR;
+    default: return LMR_OP_FETCH_XOR;
+    }
+}
+template <typename T>
+__device__ __forceinline__ T delta_finish(int op, T base, T prefix) {
+    using U = typename bits_of<T>::U;
+    switch (op) {
+    case LMR_OP_ADD: case LMR_OP_FETCH_ADD:
+        if constexpr (is_flt<T>::v) return base + prefix; else return T(U(U(base) + U(prefix)));
+    case LMR_OP_SUB: case LMR_OP_FETCH_SUB:
+        if constexpr (is_flt<T>::v) return base - prefix; else return T(U(U(base) - U(prefix)));
+    default: break;
+    }
+    if constexpr (!is_flt<T>::v) {
+        if (op == LMR_OP_AND || op == LMR_OP_FETCH_AND) return T(base & prefix);
+        if (op == LMR_OP_OR || op == LMR_OP_FETCH_OR) return T(base | prefix);
+        return T(base ^ prefix);
+    }
+    return base;
+}
+
 // OPT >= 0 fixes the op at compile time (hot paths); -1 reads it from the args.
+// Persistent over the work items of the plan (grid-stride).
 template <typename T, int OPT>
 __global__ __launch_bounds__(1024) void k_tile_apply(TileArgs a) {
     using U = typename bits_of<T>::U;
@@ -436,36 +517,92 @@ __global__ __launch_bounds__(1024) void k_tile_apply(TileArgs a) {
     extern __shared__ __align__(16) uint8_t lds_raw[];
     W* tile = reinterpret_cast<W*>(lds_raw);
     const int op = OPT >= 0 ? OPT : a.op;
-    const uint32_t t = blockIdx.x;
-    const uint64_t base = uint64_t(t) << a.tile_shift;
-    const uint32_t len = uint32_t(min(uint64_t(1) << a.tile_shift, a.shard_len - base));
-    T* shard = reinterpret_cast<T*>(a.shard) + base;
-    const uint32_t r0 = a.tile_start[t], r1 = a.tile_start[t + 1];
-    if (r0 == r1) return;   // untouched tile: nothing to read or write
-    for (uint32_t e = threadIdx.x; e < len; e += blockDim.x) {
-        if constexpr (sizeof(T) >= 4) tile[e] = shard[e];          // W == T
-        else tile[e] = W(U(shard[e]));                              // widen the bits
-    }
-    __syncthreads();
     const T cmp = from_bits<T>(U(a.cmp_bits)), eps = from_bits<T>(U(a.eps_bits));
     const T sv = from_bits<T>(U(a.val_bits));
     const int ret = a.ret;
-    for (uint32_t r = r0 + threadIdx.x; r < r1; r += blockDim.x) {
-        uint32_t l = a.bin_lidx[r];
-        T v = a.scalar ? sv : reinterpret_cast<const T*>(a.bin_val)[r];
-        uint8_t ok = 0;
-        T old = rmw_lds<T>(tile + l, op, a.kind, v, cmp, eps, ok, a.err);
-        if (ret != LMR_RET_NONE) {
-            uint32_t p = a.bin_pos[r];
-            reinterpret_cast<T*>(a.results)[p] = old;
-            if (ret == LMR_RET_RESULT) a.ok[p] = ok;
+    const uint32_t nitems = *a.item_count;
+    for (uint32_t it = blockIdx.x; it < nitems; it += gridDim.x) {
+        const TileItem w = a.items[it];
+        const uint64_t base = uint64_t(w.tile) << a.tile_shift;
+        const uint32_t len = uint32_t(min(uint64_t(1) << a.tile_shift, a.shard_len - base));
+        T* shard = reinterpret_cast<T*>(a.shard) + base;
+        if (w.mode == 0) {
+            // ---- owner mode ----
+            for (uint32_t e = threadIdx.x; e < len; e += blockDim.x) {
+                if constexpr (sizeof(T) >= 4) tile[e] = shard[e];          // W == T
+                else tile[e] = W(U(shard[e]));                              // widen the bits
+            }
+            __syncthreads();
+            for (uint32_t r = w.lo + threadIdx.x; r < w.hi; r += blockDim.x) {
+                uint32_t l = a.bin_lidx[r];
+                T v = a.scalar ? sv : reinterpret_cast<const T*>(a.bin_val)[r];
+                uint8_t ok = 0;
+                T old = rmw_lds<T>(tile + l, op, a.kind, v, cmp, eps, ok, a.err);
+                if (ret != LMR_RET_NONE) {
+                    uint32_t p = a.bin_pos[r];
+                    reinterpret_cast<T*>(a.results)[p] = old;
+                    if (ret == LMR_RET_RESULT) a.ok[p] = ok;
+                }
+            }
+            __syncthreads();
+            if (!op_is_read(op)) {
+                for (uint32_t e = threadIdx.x; e < len; e += blockDim.x) {
+                    if constexpr (sizeof(T) >= 4) shard[e] = tile[e];
+                    else shard[e] = T(U(tile[e]));
+                }
+            }
+        } else {
+            // ---- delta mode (combinable ops only; planned by k_tile_plan_count) ----
+            const W ident = (op == LMR_OP_AND || op == LMR_OP_FETCH_AND) ? W(~U(0)) : W(0);
+            const U ident_bits = (op == LMR_OP_AND || op == LMR_OP_FETCH_AND) ? ~U(0) : U(0);
+            for (uint32_t e = threadIdx.x; e < len; e += blockDim.x) tile[e] = ident;
+            __syncthreads();
+            const int acc = delta_acc_op(op);
+            T pre[16];
+            uint32_t rec[16];
+#pragma unroll
+            for (int k = 0; k < 16; k++) {
+                const uint32_t r = w.lo + threadIdx.x + uint32_t(k) * 1024u;
+                rec[k] = r;
+                if (r < w.hi) {
+                    const uint32_t l = a.bin_lidx[r];
+                    const T v = a.scalar ? sv : reinterpret_cast<const T*>(a.bin_val)[r];
+                    uint8_t ok = 0;
+                    pre[k] = rmw_lds<T>(tile + l, acc, a.kind, v, cmp, eps, ok, a.err);
+                }
+            }
+            __syncthreads();
+            const int gop = delta_global_op(op);
+            for (uint32_t e = threadIdx.x; e < len; e += blockDim.x) {
+                T d;
+                if constexpr (sizeof(T) >= 4) d = tile[e];
+                else d = T(U(tile[e]));
+                uint8_t ok = 0;
+                T b;
+                if (U(to_bits(d)) != U(ident_bits)) b = rmw_global<T>(shard + e, gop, a.kind, d, cmp, eps, ok, a.err);
+                else if (ret != LMR_RET_NONE) b = rmw_global<T>(shard + e, LMR_OP_LOAD, a.kind, d, cmp, eps, ok, a.err);
+                else continue;
+                if (ret != LMR_RET_NONE) {
+                    if constexpr (sizeof(T) >= 4) tile[e] = b;
+                    else tile[e] = W(U(b));
+                }
+            }
+            if (ret != LMR_RET_NONE) {
+                __syncthreads();
+#pragma unroll
+                for (int k = 0; k < 16; k++) {
+                    const uint32_t r = rec[k];
+                    if (r < w.hi) {
+                        const uint32_t l = a.bin_lidx[r];
+                        T b;
+                        if constexpr (sizeof(T) >= 4) b = tile[l];
+                        else b = T(U(tile[l]));
+                        reinterpret_cast<T*>(a.results)[a.bin_pos[r]] = delta_finish<T>(op, b, pre[k]);
+                    }
+                }
+            }
         }
-    }
-    __syncthreads();
-    if (op_is_read(op)) return;
-    for (uint32_t e = threadIdx.x; e < len; e += blockDim.x) {
-        if constexpr (sizeof(T) >= 4) shard[e] = tile[e];
-        else shard[e] = T(U(tile[e]));
+        __syncthreads();
     }
 }
 
@@ -549,6 +686,8 @@ size_t tiled_ws_bytes(uint64_t cap) {
     b += al(cap * 2) + al(cap * 8) + al(cap * 4) + al(4);
     b += al((size_t(kMaxCoarse) * kMaxBinBlocks + 1) * 4);
     b += al(cap * 4) + al(cap * 8) + al(cap * 4);
+    b += 2 * al((size_t(kMaxTiles) + 1) * 4) + al(size_t(kMaxTiles) / kScanItems * 4 + 256) + al(4);
+    b += al((size_t(kMaxTiles) + cap / kSplit + 2) * 16);
     return b;
 }
 
@@ -567,7 +706,12 @@ TiledWs carve_tiled_ws(uint8_t* base, uint64_t cap) {
     w.coarse_off = reinterpret_cast<uint32_t*>(p); p += al((size_t(kMaxCoarse) * kMaxBinBlocks + 1) * 4);
     w.tmp_idx = reinterpret_cast<uint32_t*>(p); p += al(cap * 4);
     w.tmp_val = p; p += al(cap * 8);
-    w.tmp_pos = reinterpret_cast<uint32_t*>(p);
+    w.tmp_pos = reinterpret_cast<uint32_t*>(p); p += al(cap * 4);
+    w.tile_items = reinterpret_cast<uint32_t*>(p); p += al((size_t(kMaxTiles) + 1) * 4);
+    w.tile_items2 = reinterpret_cast<uint32_t*>(p); p += al((size_t(kMaxTiles) + 1) * 4);
+    w.plan_partials = reinterpret_cast<uint32_t*>(p); p += al(size_t(kMaxTiles) / kScanItems * 4 + 256);
+    w.item_count = reinterpret_cast<uint32_t*>(p); p += al(4);
+    w.items = p;
     return w;
 }
 
@@ -581,6 +725,10 @@ static int env_int(const char* name, int dflt, int lo, int hi) {
 }
 static int bin_blocks_cap() {
     static int v = env_int("LMR_BIN_BLOCKS", 512, 1, kMaxBinBlocks);
+    return v;
+}
+static int tile_grid_cap() {
+    static int v = env_int("LMR_TILE_BLOCKS", 2048, 1, 1 << 24);
     return v;
 }
 static int fine_blocks_cap() {
@@ -677,23 +825,39 @@ hipError_t launch_apply_tiled(int dtype, int index_size, const ApplyArgs& a, con
     });
     }
     if (e != hipSuccess) return e;
+    ProfScope ps(a.prof, LMR_STAGE_TILE_APPLY, s);
+    // work plan: owner items, and delta items for hot tiles of combinable ops
+    const uint64_t avg = (a.n + num_tiles - 1) / num_tiles;
+    const uint32_t thresh = uint32_t(std::min<uint64_t>(0xFFFFFFFFull, std::max<uint64_t>(4 * avg, 65536)));
+    const unsigned pg = unsigned((num_tiles + 255) / 256);
+    hipLaunchKernelGGL(k_tile_plan_count, dim3(pg), dim3(256), 0, s, w.tile_start, uint32_t(num_tiles), thresh,
+                       op_combines(a.op) ? 1 : 0, w.tile_items);
+    e = scan_exclusive_u32(w.tile_items, num_tiles, w.plan_partials, w.item_count, s);
+    if (e != hipSuccess) return e;
+    // k_tile_plan_fill needs the per-tile item counts next to their scan: recount into tile_items2
+    hipLaunchKernelGGL(k_tile_plan_count, dim3(pg), dim3(256), 0, s, w.tile_start, uint32_t(num_tiles), thresh,
+                       op_combines(a.op) ? 1 : 0, w.tile_items2);
+    hipLaunchKernelGGL(k_tile_plan_fill, dim3(pg), dim3(256), 0, s, w.tile_start, uint32_t(num_tiles),
+                       w.tile_items, w.tile_items2, reinterpret_cast<TileItem*>(w.items));
     TileArgs t;
     t.shard = a.shard; t.shard_len = a.shard_len; t.tile_shift = shift;
     t.kind = a.kind; t.op = a.op; t.ret = a.ret;
     t.cmp_bits = a.cmp_bits; t.eps_bits = a.eps_bits; t.val_bits = a.val_bits;
     t.scalar = (a.val == nullptr);
-    t.tile_start = w.tile_start; t.bin_lidx = w.bin_lidx; t.bin_val = w.bin_val;
+    t.items = reinterpret_cast<const TileItem*>(w.items); t.item_count = w.item_count;
+    t.bin_lidx = w.bin_lidx; t.bin_val = w.bin_val;
     t.bin_pos = w.bin_pos; t.results = a.results; t.ok = a.ok; t.err = a.err;
     const size_t tile_lds = size_t(kTileBytes);
-    ProfScope ps(a.prof, LMR_STAGE_TILE_APPLY, s);
+    const uint64_t max_items = num_tiles + (op_combines(a.op) ? (a.n + kSplit - 1) / kSplit : 0);
+    const unsigned grid = unsigned(std::min<uint64_t>(max_items, uint64_t(tile_grid_cap())));
     return dispatch_dtype(dtype, [&](auto tag) {
         using T = decltype(tag);
         if (a.op == LMR_OP_ADD)
-            hipLaunchKernelGGL((k_tile_apply<T, LMR_OP_ADD>), dim3(unsigned(num_tiles)), dim3(1024), tile_lds, s, t);
+            hipLaunchKernelGGL((k_tile_apply<T, LMR_OP_ADD>), dim3(grid), dim3(1024), tile_lds, s, t);
         else if (a.op == LMR_OP_FETCH_ADD)
-            hipLaunchKernelGGL((k_tile_apply<T, LMR_OP_FETCH_ADD>), dim3(unsigned(num_tiles)), dim3(1024), tile_lds, s, t);
+            hipLaunchKernelGGL((k_tile_apply<T, LMR_OP_FETCH_ADD>), dim3(grid), dim3(1024), tile_lds, s, t);
         else
-            hipLaunchKernelGGL((k_tile_apply<T, -1>), dim3(unsigned(num_tiles)), dim3(1024), tile_lds, s, t);
+            hipLaunchKernelGGL((k_tile_apply<T, -1>), dim3(grid), dim3(1024), tile_lds, s, t);
         return hipGetLastError();
     });
 }

@@ -51,6 +51,11 @@ struct TiledWs {
     uint32_t* tmp_idx;     // [cap]
     uint8_t* tmp_val;      // [cap * 8]
     uint32_t* tmp_pos;     // [cap]
+    uint32_t* tile_items;  // [kMaxTiles + 1] work items per tile, then their exclusive scan
+    uint32_t* tile_items2; // [kMaxTiles + 1] work items per tile
+    uint32_t* plan_partials;
+    uint32_t* item_count;  // [1]
+    uint8_t* items;        // TileItem[kMaxTiles + cap / kSplit + 2]
 };
 size_t tiled_ws_bytes(uint64_t cap);
 TiledWs carve_tiled_ws(uint8_t* base, uint64_t cap);

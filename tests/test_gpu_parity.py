@@ -358,3 +358,39 @@ def test_tiled_two_level_collisions(world, orc, lam):
     grp_start = np.maximum.accumulate(np.where(first, np.arange(si.size), 0))
     rank = np.arange(si.size) - grp_start
     assert np.array_equal(so, shard0[si] + rank.astype(np.uint64))
+
+
+@pytest.mark.parametrize("dt", ["u64", "i32", "u16", "f64", "f32"])
+def test_hot_tile_delta_mode(world, orc, lam, dt):
+    """Skewed stream: one element takes ~40 % of all records, so its tile is split into
+    delta-mode work items (LDS combine + one global atomic per element per item).
+    Integer ops: exact final state, fetch olds a valid chain; floats: exact with 1.0."""
+    k = world.team().kernels
+    k.reserve(1 << 21)
+    rng = np.random.default_rng(17)
+    shard_len = 1 << 18
+    n = 1 << 20
+    idx = rng.integers(0, shard_len, n).astype(np.uint64)
+    idx[rng.random(n) < 0.4] = 12345
+    t = NP[dt]
+    ops = [ADD, FETCH_ADD, SUB, FETCH_SUB] if IS_FLOAT[dt] else \
+        [ADD, FETCH_ADD, SUB, FETCH_SUB, AND, 11, OR, 13, XOR, 15]
+    for op in ops:
+        shard0 = rand_elems(dt, shard_len, rng) if not IS_FLOAT[dt] else np.zeros(shard_len, t)
+        vals = np.ones(n, dtype=t) if (IS_FLOAT[dt] or op in (ADD, FETCH_ADD, SUB, FETCH_SUB)) else \
+            rand_vals(dt, n, rng, op)
+        c = Case(k, orc, lam, dt, op, shard0, idx, vals, "soa", 2)
+        assert c.err == 0
+        assert bits_equal(c.got, c.ref), (dt, op)
+        if op in (FETCH_ADD, FETCH_SUB):
+            hot = idx == 12345
+            olds = np.sort(c.res_d[hot].astype(np.float64 if IS_FLOAT[dt] else np.int64)
+                           if IS_FLOAT[dt] else c.res_d[hot].astype(np.uint64))
+            m = int(hot.sum())
+            step = 1 if op == FETCH_ADD else -1
+            base = shard0[12345]
+            exp = (np.array([base]).astype(t)[0] + (np.arange(m) * step).astype(t)) if IS_FLOAT[dt] else \
+                (np.uint64(base.astype(np.int64).astype(np.uint64)) +
+                 (np.arange(m, dtype=np.int64) * step).astype(np.uint64)).astype(t)
+            exp = np.sort(exp.astype(np.float64) if IS_FLOAT[dt] else exp.astype(np.uint64))
+            assert np.array_equal(olds, exp), (dt, op)
