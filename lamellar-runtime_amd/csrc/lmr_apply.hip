@@ -431,16 +431,26 @@ __global__ void k_tile_plan_count(const uint32_t* tile_start, uint32_t num_tiles
     tile_items[t] = (c == 0) ? 0u : ((combinable && c > thresh) ? (c + kSplit - 1) / kSplit : 1u);
 }
 
-__global__ void k_tile_plan_fill(const uint32_t* tile_start, uint32_t num_tiles, const uint32_t* item_base,
+// Item slot t holds tile t's first piece (mode 2 = empty tile); the remaining
+// delta pieces of split tiles go after num_tiles at extra_base[t] (exclusive
+// scan of items_t - 1), served by a small persistent tail of blocks.
+__global__ void k_tile_plan_extra(const uint32_t* tile_items, uint32_t num_tiles, uint32_t* extra) {
+    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t < num_tiles) extra[t] = tile_items[t] > 1 ? tile_items[t] - 1 : 0u;
+}
+
+__global__ void k_tile_plan_fill(const uint32_t* tile_start, uint32_t num_tiles, const uint32_t* extra_base,
                                  const uint32_t* tile_items, TileItem* items) {
     const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= num_tiles) return;
-    const uint32_t m = tile_items[t], b = item_base[t];
+    const uint32_t m = tile_items[t];
     const uint32_t lo = tile_start[t], hi = tile_start[t + 1];
-    if (m == 1) { items[b] = TileItem{t, lo, hi, 0u}; return; }
-    for (uint32_t j = 0; j < m; j++) {
+    if (m == 0) { items[t] = TileItem{t, lo, hi, 2u}; return; }
+    if (m == 1) { items[t] = TileItem{t, lo, hi, 0u}; return; }
+    items[t] = TileItem{t, lo, min(hi, lo + kSplit), 1u};
+    for (uint32_t j = 1; j < m; j++) {
         const uint32_t l = lo + j * kSplit;
-        items[b + j] = TileItem{t, l, min(hi, l + kSplit), 1u};
+        items[num_tiles + extra_base[t] + j - 1] = TileItem{t, l, min(hi, l + kSplit), 1u};
     }
 }
 
@@ -456,7 +466,8 @@ struct TileArgs {
     uint64_t val_bits;       // scalar value (SVMI)
     bool scalar;
     const TileItem* items;
-    const uint32_t* item_count;
+    const uint32_t* item_count;   // number of extra items (after num_tiles)
+    uint32_t num_tiles;
     const uint16_t* bin_lidx;
     const uint8_t* bin_val;
     const uint32_t* bin_pos;
@@ -520,9 +531,16 @@ __global__ __launch_bounds__(1024) void k_tile_apply(TileArgs a) {
     const T cmp = from_bits<T>(U(a.cmp_bits)), eps = from_bits<T>(U(a.eps_bits));
     const T sv = from_bits<T>(U(a.val_bits));
     const int ret = a.ret;
-    const uint32_t nitems = *a.item_count;
-    for (uint32_t it = blockIdx.x; it < nitems; it += gridDim.x) {
+    // blocks [0, num_tiles): the tile's own first item; the rest: extra delta items, grid-stride
+    const uint32_t nt = a.num_tiles;
+    const uint32_t nextra = *a.item_count;
+    const bool own = blockIdx.x < nt;
+    uint32_t it = own ? blockIdx.x : nt + (blockIdx.x - nt);
+    const uint32_t end = own ? blockIdx.x + 1 : nt + nextra;
+    const uint32_t step = own ? 1u : gridDim.x - nt;
+    for (; it < end; it += step) {
         const TileItem w = a.items[it];
+        if (w.mode == 2) break;
         const uint64_t base = uint64_t(w.tile) << a.tile_shift;
         const uint32_t len = uint32_t(min(uint64_t(1) << a.tile_shift, a.shard_len - base));
         T* shard = reinterpret_cast<T*>(a.shard) + base;
@@ -728,7 +746,7 @@ static int bin_blocks_cap() {
     return v;
 }
 static int tile_grid_cap() {
-    static int v = env_int("LMR_TILE_BLOCKS", 2048, 1, 1 << 24);
+    static int v = env_int("LMR_TILE_EXTRA_BLOCKS", 1024, 1, 1 << 24);
     return v;
 }
 static int fine_blocks_cap() {
@@ -832,24 +850,24 @@ hipError_t launch_apply_tiled(int dtype, int index_size, const ApplyArgs& a, con
     const unsigned pg = unsigned((num_tiles + 255) / 256);
     hipLaunchKernelGGL(k_tile_plan_count, dim3(pg), dim3(256), 0, s, w.tile_start, uint32_t(num_tiles), thresh,
                        op_combines(a.op) ? 1 : 0, w.tile_items);
-    e = scan_exclusive_u32(w.tile_items, num_tiles, w.plan_partials, w.item_count, s);
+    hipLaunchKernelGGL(k_tile_plan_extra, dim3(pg), dim3(256), 0, s, w.tile_items, uint32_t(num_tiles),
+                       w.tile_items2);
+    e = scan_exclusive_u32(w.tile_items2, num_tiles, w.plan_partials, w.item_count, s);
     if (e != hipSuccess) return e;
-    // k_tile_plan_fill needs the per-tile item counts next to their scan: recount into tile_items2
-    hipLaunchKernelGGL(k_tile_plan_count, dim3(pg), dim3(256), 0, s, w.tile_start, uint32_t(num_tiles), thresh,
-                       op_combines(a.op) ? 1 : 0, w.tile_items2);
     hipLaunchKernelGGL(k_tile_plan_fill, dim3(pg), dim3(256), 0, s, w.tile_start, uint32_t(num_tiles),
-                       w.tile_items, w.tile_items2, reinterpret_cast<TileItem*>(w.items));
+                       w.tile_items2, w.tile_items, reinterpret_cast<TileItem*>(w.items));
     TileArgs t;
     t.shard = a.shard; t.shard_len = a.shard_len; t.tile_shift = shift;
     t.kind = a.kind; t.op = a.op; t.ret = a.ret;
     t.cmp_bits = a.cmp_bits; t.eps_bits = a.eps_bits; t.val_bits = a.val_bits;
     t.scalar = (a.val == nullptr);
     t.items = reinterpret_cast<const TileItem*>(w.items); t.item_count = w.item_count;
+    t.num_tiles = uint32_t(num_tiles);
     t.bin_lidx = w.bin_lidx; t.bin_val = w.bin_val;
     t.bin_pos = w.bin_pos; t.results = a.results; t.ok = a.ok; t.err = a.err;
     const size_t tile_lds = size_t(kTileBytes);
-    const uint64_t max_items = num_tiles + (op_combines(a.op) ? (a.n + kSplit - 1) / kSplit : 0);
-    const unsigned grid = unsigned(std::min<uint64_t>(max_items, uint64_t(tile_grid_cap())));
+    const uint64_t max_extra = op_combines(a.op) ? (a.n + kSplit - 1) / kSplit : 0;
+    const unsigned grid = unsigned(num_tiles + std::min<uint64_t>(max_extra, uint64_t(tile_grid_cap())));
     return dispatch_dtype(dtype, [&](auto tag) {
         using T = decltype(tag);
         if (a.op == LMR_OP_ADD)
