@@ -63,15 +63,20 @@ def parse():
 
 def stage_bytes_per_op(stage, iw, vb, eb, n, shard_len, fetch):
     """Algorithmic HBM bytes per op of each kernel stage (Kernels):
-    the bytes a stage must read and write per record, shard traffic amortised."""
+    the bytes a stage must read and write per record, shard traffic amortised.
+    Returned values travel binned -> temp -> input order through stored u32 maps
+    (qpos written by the coarse pass, rpos by the fine pass)."""
     pos = 4 if fetch else 0
     res = eb if fetch else 0
+    tile_elems = 65536 // max(eb, 4)
+    two_level = (shard_len + tile_elems - 1) // tile_elems > 128
     return {
         "direct": iw + vb + 2 * eb + res,
         "bin_count": iw,
-        "bin_scatter": iw + vb + 4 + vb + pos,          # coarse pass: record in, temp record out
-        "fine_scatter": 4 + vb + pos + 2 + vb + pos,    # temp record in, tile-local record out
-        "tile_apply": 2 + vb + pos + res + 2.0 * eb * shard_len / max(n, 1),
+        "bin_scatter": iw + vb + 4 + vb + pos,          # coarse pass: record in, temp record (+ qpos) out
+        "fine_scatter": 4 + vb + 2 + vb + pos,          # temp record in, tile-local record (+ rpos) out
+        "tile_apply": 2 + vb + res + 2.0 * eb * shard_len / max(n, 1),
+        "unpartition": (2 if two_level else 1) * (pos + 2 * res),
         "pack": 8 + 8 + vb + iw + vb + 4,
         "scatter_results": 4 + 2 * eb,
         "mvsi": vb + res,
@@ -320,7 +325,7 @@ def main():
             if tr:
                 roof["traffic"] = tr
     apply_stages = [s for s in ("direct", "mvsi", "bin_count", "scan", "bin_scatter", "fine_scatter",
-                                "tile_apply") if s in per]
+                                "tile_apply", "unpartition") if s in per]
     apply_ms = sum(per[s][0] * per[s][1] for s in apply_stages)
 
     out = {

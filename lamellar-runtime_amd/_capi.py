@@ -88,7 +88,7 @@ SIGNATURES = {
 }
 
 STAGES = ["direct", "mvsi", "bin_count", "scan", "bin_scatter", "tile_apply", "pack",
-          "scatter_results", "fine_scatter"]
+          "scatter_results", "fine_scatter", "unpartition"]
 
 _lib = None
 

@@ -136,7 +136,7 @@ struct BinArgs {
     uint32_t* counts;      // [num_tiles * G], tile-major
     uint16_t* bin_lidx;
     uint8_t* bin_val;
-    uint32_t* bin_pos;     // null when nothing is returned
+    uint32_t* rpos;        // [n] record k -> binned position (~0 = out of bounds); null when nothing is returned
     uint32_t* err;
 };
 
@@ -171,11 +171,14 @@ __global__ __launch_bounds__(kBinBlock) void k_bin_scatter(BinArgs b) {
     const uint32_t lmask = (1u << b.tile_shift) - 1u;
     for (uint64_t k = lo + threadIdx.x; k < hi; k += blockDim.x) {
         uint64_t idx = load_idx<IW>(b.idx, b.idx_stride, k);
-        if (idx >= b.shard_len) continue;
+        if (idx >= b.shard_len) {
+            if (b.rpos) b.rpos[k] = 0xFFFFFFFFu;
+            continue;
+        }
         uint32_t pos = atomicAdd(&cursor[uint32_t(idx >> b.tile_shift)], 1u);
         b.bin_lidx[pos] = uint16_t(uint32_t(idx) & lmask);
         if (b.val) reinterpret_cast<V*>(b.bin_val)[pos] = *reinterpret_cast<const V*>(b.val + k * b.val_stride);
-        if (b.bin_pos) b.bin_pos[pos] = uint32_t(k);
+        if (b.rpos) b.rpos[k] = pos;
     }
 }
 
@@ -218,10 +221,10 @@ struct PartArgs {
     uint32_t* coarse_off;         // [C * G + 1]
     uint32_t* tmp_idx;
     uint8_t* tmp_val;
-    uint32_t* tmp_pos;
+    uint32_t* qpos;               // [n] record k -> temp position (~0 = out of bounds); null: no results
     uint16_t* bin_lidx;
     uint8_t* bin_val;
-    uint32_t* bin_pos;
+    uint32_t* rpos;               // [total] temp position -> binned position; null: no results
 };
 
 // coarse_off[c][g] = start of block g's coarse-c records in the temp buffer
@@ -268,7 +271,6 @@ __global__ __launch_bounds__(1024) void k_coarse_scatter(PartArgs p) {
     __shared__ uint32_t hist[kMaxCoarse], base[kMaxCoarse], cursor[kMaxCoarse], tot;
     __shared__ uint32_t s_idx[kRound];
     __shared__ V s_val[kRound];
-    __shared__ uint32_t s_pos[kRound];
     __shared__ uint8_t s_c[kRound];
     const uint32_t g = blockIdx.x, C = p.C;
     const int cshift = p.tile_shift + kFineShift;
@@ -303,12 +305,16 @@ __global__ __launch_bounds__(1024) void k_coarse_scatter(PartArgs p) {
         __syncthreads();
 #pragma unroll
         for (int j = 0; j < 4; j++) {
-            if (!m_ok[j]) continue;
+            const uint64_t k = r0 + uint64_t(j) * 1024 + threadIdx.x;
+            if (!m_ok[j]) {
+                if (p.qpos && k < hi) p.qpos[k] = 0xFFFFFFFFu;
+                continue;
+            }
             const uint32_t q = base[m_c[j]] + m_rank[j];
             s_idx[q] = uint32_t(m_raw[j]);
             s_val[q] = m_val[j];
-            s_pos[q] = uint32_t(r0 + uint64_t(j) * 1024 + threadIdx.x);
             s_c[q] = uint8_t(m_c[j]);
+            if (p.qpos) p.qpos[k] = cursor[m_c[j]] + m_rank[j];   // coalesced in k
         }
         if (r0 + kRound < hi) load_round(r0 + kRound);     // prefetch the next round
         __syncthreads();
@@ -318,7 +324,6 @@ __global__ __launch_bounds__(1024) void k_coarse_scatter(PartArgs p) {
             const uint32_t dst = cursor[c] + q - base[c];
             p.tmp_idx[dst] = s_idx[q];
             if (p.val) reinterpret_cast<V*>(p.tmp_val)[dst] = s_val[q];
-            if (p.tmp_pos) p.tmp_pos[dst] = s_pos[q];
         }
         __syncthreads();
         for (uint32_t c = threadIdx.x; c < C; c += blockDim.x) cursor[c] += hist[c];
@@ -334,11 +339,10 @@ __global__ __launch_bounds__(1024) void k_fine_scatter(PartArgs p) {
     __shared__ uint32_t hist[kFine], base[kFine], cursor[kFine], tot;
     __shared__ uint16_t s_l[kRound];
     __shared__ V s_val[kRound];
-    __shared__ uint32_t s_pos[kRound];
     __shared__ uint8_t s_f[kRound];
     const uint32_t nseg = p.C * p.G;
     const uint32_t lmask = (1u << p.tile_shift) - 1u;
-    uint32_t m_idx[4], m_pos[4];
+    uint32_t m_idx[4];
     V m_val[4];
     auto load_round = [&](uint32_t r0, uint32_t hi) {
 #pragma unroll
@@ -347,7 +351,6 @@ __global__ __launch_bounds__(1024) void k_fine_scatter(PartArgs p) {
             const bool in = k < hi;
             m_idx[j] = in ? p.tmp_idx[k] : 0xFFFFFFFFu;
             m_val[j] = (in && p.tmp_val) ? reinterpret_cast<const V*>(p.tmp_val)[k] : V(0);
-            m_pos[j] = (in && p.tmp_pos) ? p.tmp_pos[k] : 0u;
         }
     };
     uint32_t cg = blockIdx.x;
@@ -384,8 +387,8 @@ __global__ __launch_bounds__(1024) void k_fine_scatter(PartArgs p) {
                 const uint32_t q = base[m_f[j]] + m_rank[j];
                 s_l[q] = uint16_t(m_idx[j] & lmask);
                 s_val[q] = m_val[j];
-                s_pos[q] = m_pos[j];
                 s_f[q] = uint8_t(m_f[j]);
+                if (p.rpos) p.rpos[r0 + uint32_t(j) * 1024 + threadIdx.x] = cursor[m_f[j]] + m_rank[j];
             }
             if (r0 + kRound < hi) {
                 load_round(r0 + kRound, hi);
@@ -400,7 +403,6 @@ __global__ __launch_bounds__(1024) void k_fine_scatter(PartArgs p) {
                 const uint32_t dst = cursor[f] + q - base[f];
                 p.bin_lidx[dst] = s_l[q];
                 if (p.tmp_val) reinterpret_cast<V*>(p.bin_val)[dst] = s_val[q];
-                if (p.bin_pos) p.bin_pos[dst] = s_pos[q];
             }
             __syncthreads();
             for (uint32_t f = threadIdx.x; f < nf; f += blockDim.x) cursor[f] += hist[f];
@@ -431,26 +433,26 @@ __global__ void k_tile_plan_count(const uint32_t* tile_start, uint32_t num_tiles
     tile_items[t] = (c == 0) ? 0u : ((combinable && c > thresh) ? (c + kSplit - 1) / kSplit : 1u);
 }
 
-// Item slot t holds tile t's first piece (mode 2 = empty tile); the remaining
-// delta pieces of split tiles go after num_tiles at extra_base[t] (exclusive
-// scan of items_t - 1), served by a small persistent tail of blocks.
+// Item slot t holds tile t's owner item (mode 0) or a skip marker (mode 2:
+// empty or split tile). Every delta piece of a split tile goes to the delta
+// list at delta_base[t] (exclusive scan of the per-tile piece counts), served
+// by its own persistent kernel so the owner kernel stays lean on registers.
 __global__ void k_tile_plan_extra(const uint32_t* tile_items, uint32_t num_tiles, uint32_t* extra) {
     const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
-    if (t < num_tiles) extra[t] = tile_items[t] > 1 ? tile_items[t] - 1 : 0u;
+    if (t < num_tiles) extra[t] = tile_items[t] > 1 ? tile_items[t] : 0u;
 }
 
-__global__ void k_tile_plan_fill(const uint32_t* tile_start, uint32_t num_tiles, const uint32_t* extra_base,
-                                 const uint32_t* tile_items, TileItem* items) {
+__global__ void k_tile_plan_fill(const uint32_t* tile_start, uint32_t num_tiles, const uint32_t* delta_base,
+                                 const uint32_t* tile_items, TileItem* items, TileItem* delta) {
     const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= num_tiles) return;
     const uint32_t m = tile_items[t];
     const uint32_t lo = tile_start[t], hi = tile_start[t + 1];
-    if (m == 0) { items[t] = TileItem{t, lo, hi, 2u}; return; }
-    if (m == 1) { items[t] = TileItem{t, lo, hi, 0u}; return; }
-    items[t] = TileItem{t, lo, min(hi, lo + kSplit), 1u};
-    for (uint32_t j = 1; j < m; j++) {
+    items[t] = TileItem{t, lo, hi, m == 1 ? 0u : 2u};
+    if (m <= 1) return;
+    for (uint32_t j = 0; j < m; j++) {
         const uint32_t l = lo + j * kSplit;
-        items[num_tiles + extra_base[t] + j - 1] = TileItem{t, l, min(hi, l + kSplit), 1u};
+        delta[delta_base[t] + j] = TileItem{t, l, min(hi, l + kSplit), 1u};
     }
 }
 
@@ -465,14 +467,14 @@ struct TileArgs {
     uint64_t eps_bits;
     uint64_t val_bits;       // scalar value (SVMI)
     bool scalar;
-    const TileItem* items;
-    const uint32_t* item_count;   // number of extra items (after num_tiles)
+    const TileItem* items;        // one per tile (owner kernel)
+    const TileItem* delta;        // delta pieces (delta kernel)
+    const uint32_t* delta_count;  // number of delta pieces (device)
     uint32_t num_tiles;
     const uint16_t* bin_lidx;
     const uint8_t* bin_val;
-    const uint32_t* bin_pos;
-    void* results;
-    uint8_t* ok;
+    void* results;           // binned order: [r] (un-partitioned by k_unpartition)
+    uint8_t* ok;             // binned order
     uint32_t* err;
 };
 
@@ -520,9 +522,70 @@ __device__ __forceinline__ T delta_finish(int op, T base, T prefix) {
 }
 
 // OPT >= 0 fixes the op at compile time (hot paths); -1 reads it from the args.
-// Persistent over the work items of the plan (grid-stride).
+// Owner mode: one block per tile — load the tile into LDS, apply the tile's
+// records with LDS atomics, write it back. Kept free of the delta path's
+// register arrays so two 1024-thread blocks (2 x 64 KiB LDS) fit per CU.
 template <typename T, int OPT>
-__global__ __launch_bounds__(1024) void k_tile_apply(TileArgs a) {
+__global__ __launch_bounds__(1024, 2) void k_tile_owner(TileArgs a) {
+    using U = typename bits_of<T>::U;
+    using W = typename word_of<T>::W;
+    extern __shared__ __align__(16) uint8_t lds_raw[];
+    W* tile = reinterpret_cast<W*>(lds_raw);
+    const TileItem w = a.items[blockIdx.x];
+    if (w.mode != 0) return;
+    const int op = OPT >= 0 ? OPT : a.op;
+    const T cmp = from_bits<T>(U(a.cmp_bits)), eps = from_bits<T>(U(a.eps_bits));
+    const T sv = from_bits<T>(U(a.val_bits));
+    const int ret = a.ret;
+    const uint64_t base = uint64_t(w.tile) << a.tile_shift;
+    const uint32_t len = uint32_t(min(uint64_t(1) << a.tile_shift, a.shard_len - base));
+    T* shard = reinterpret_cast<T*>(a.shard) + base;
+    for (uint32_t e = threadIdx.x; e < len; e += blockDim.x) {
+        if constexpr (sizeof(T) >= 4) tile[e] = shard[e];          // W == T
+        else tile[e] = W(U(shard[e]));                              // widen the bits
+    }
+    __syncthreads();
+    // kOwnUnroll records per thread per round: all loads issued before the LDS atomics
+    constexpr int kOwnUnroll = 4;
+    for (uint32_t r0 = w.lo + threadIdx.x; r0 < w.hi; r0 += kOwnUnroll * 1024u) {
+        uint32_t l[kOwnUnroll];
+        T v[kOwnUnroll];
+#pragma unroll
+        for (int k = 0; k < kOwnUnroll; k++) {
+            const uint32_t r = r0 + uint32_t(k) * 1024u;
+            if (r < w.hi) {
+                l[k] = a.bin_lidx[r];
+                v[k] = a.scalar ? sv : reinterpret_cast<const T*>(a.bin_val)[r];
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < kOwnUnroll; k++) {
+            const uint32_t r = r0 + uint32_t(k) * 1024u;
+            if (r < w.hi) {
+                uint8_t ok = 0;
+                T old = rmw_lds<T>(tile + l[k], op, a.kind, v[k], cmp, eps, ok, a.err);
+                if (ret != LMR_RET_NONE) {
+                    reinterpret_cast<T*>(a.results)[r] = old;          // coalesced (binned order)
+                    if (ret == LMR_RET_RESULT) a.ok[r] = ok;
+                }
+            }
+        }
+    }
+    __syncthreads();
+    if (!op_is_read(op)) {
+        for (uint32_t e = threadIdx.x; e < len; e += blockDim.x) {
+            if constexpr (sizeof(T) >= 4) shard[e] = tile[e];
+            else shard[e] = T(U(tile[e]));
+        }
+    }
+}
+
+// Delta mode (combinable ops only; planned by k_tile_plan_count), persistent
+// over the delta list: combine kSplit records in an identity-initialised LDS
+// tile, push one device-scope atomic per touched element, rebuild fetch
+// results as base (+) the record's LDS prefix.
+template <typename T, int OPT>
+__global__ __launch_bounds__(1024) void k_tile_delta(TileArgs a) {
     using U = typename bits_of<T>::U;
     using W = typename word_of<T>::W;
     extern __shared__ __align__(16) uint8_t lds_raw[];
@@ -531,96 +594,91 @@ __global__ __launch_bounds__(1024) void k_tile_apply(TileArgs a) {
     const T cmp = from_bits<T>(U(a.cmp_bits)), eps = from_bits<T>(U(a.eps_bits));
     const T sv = from_bits<T>(U(a.val_bits));
     const int ret = a.ret;
-    // blocks [0, num_tiles): the tile's own first item; the rest: extra delta items, grid-stride
-    const uint32_t nt = a.num_tiles;
-    const uint32_t nextra = *a.item_count;
-    const bool own = blockIdx.x < nt;
-    uint32_t it = own ? blockIdx.x : nt + (blockIdx.x - nt);
-    const uint32_t end = own ? blockIdx.x + 1 : nt + nextra;
-    const uint32_t step = own ? 1u : gridDim.x - nt;
-    for (; it < end; it += step) {
-        const TileItem w = a.items[it];
-        if (w.mode == 2) break;
+    const uint32_t nitems = *a.delta_count;
+    const W ident = (op == LMR_OP_AND || op == LMR_OP_FETCH_AND) ? W(~U(0)) : W(0);
+    const U ident_bits = (op == LMR_OP_AND || op == LMR_OP_FETCH_AND) ? ~U(0) : U(0);
+    const int acc = delta_acc_op(op);
+    const int gop = delta_global_op(op);
+    for (uint32_t it = blockIdx.x; it < nitems; it += gridDim.x) {
+        const TileItem w = a.delta[it];
         const uint64_t base = uint64_t(w.tile) << a.tile_shift;
         const uint32_t len = uint32_t(min(uint64_t(1) << a.tile_shift, a.shard_len - base));
         T* shard = reinterpret_cast<T*>(a.shard) + base;
-        if (w.mode == 0) {
-            // ---- owner mode ----
-            for (uint32_t e = threadIdx.x; e < len; e += blockDim.x) {
-                if constexpr (sizeof(T) >= 4) tile[e] = shard[e];          // W == T
-                else tile[e] = W(U(shard[e]));                              // widen the bits
-            }
-            __syncthreads();
-            for (uint32_t r = w.lo + threadIdx.x; r < w.hi; r += blockDim.x) {
-                uint32_t l = a.bin_lidx[r];
-                T v = a.scalar ? sv : reinterpret_cast<const T*>(a.bin_val)[r];
-                uint8_t ok = 0;
-                T old = rmw_lds<T>(tile + l, op, a.kind, v, cmp, eps, ok, a.err);
-                if (ret != LMR_RET_NONE) {
-                    uint32_t p = a.bin_pos[r];
-                    reinterpret_cast<T*>(a.results)[p] = old;
-                    if (ret == LMR_RET_RESULT) a.ok[p] = ok;
-                }
-            }
-            __syncthreads();
-            if (!op_is_read(op)) {
-                for (uint32_t e = threadIdx.x; e < len; e += blockDim.x) {
-                    if constexpr (sizeof(T) >= 4) shard[e] = tile[e];
-                    else shard[e] = T(U(tile[e]));
-                }
-            }
-        } else {
-            // ---- delta mode (combinable ops only; planned by k_tile_plan_count) ----
-            const W ident = (op == LMR_OP_AND || op == LMR_OP_FETCH_AND) ? W(~U(0)) : W(0);
-            const U ident_bits = (op == LMR_OP_AND || op == LMR_OP_FETCH_AND) ? ~U(0) : U(0);
-            for (uint32_t e = threadIdx.x; e < len; e += blockDim.x) tile[e] = ident;
-            __syncthreads();
-            const int acc = delta_acc_op(op);
-            T pre[16];
-            uint32_t rec[16];
+        for (uint32_t e = threadIdx.x; e < len; e += blockDim.x) tile[e] = ident;
+        __syncthreads();
+        T pre[kSplit / 1024];
 #pragma unroll
-            for (int k = 0; k < 16; k++) {
+        for (int k = 0; k < int(kSplit / 1024); k++) {
+            const uint32_t r = w.lo + threadIdx.x + uint32_t(k) * 1024u;
+            if (r < w.hi) {
+                const uint32_t l = a.bin_lidx[r];
+                const T v = a.scalar ? sv : reinterpret_cast<const T*>(a.bin_val)[r];
+                uint8_t ok = 0;
+                pre[k] = rmw_lds<T>(tile + l, acc, a.kind, v, cmp, eps, ok, a.err);
+            }
+        }
+        __syncthreads();
+        for (uint32_t e = threadIdx.x; e < len; e += blockDim.x) {
+            T d;
+            if constexpr (sizeof(T) >= 4) d = tile[e];
+            else d = T(U(tile[e]));
+            uint8_t ok = 0;
+            T b;
+            if (U(to_bits(d)) != U(ident_bits)) b = rmw_global<T>(shard + e, gop, a.kind, d, cmp, eps, ok, a.err);
+            else if (ret != LMR_RET_NONE) b = rmw_global<T>(shard + e, LMR_OP_LOAD, a.kind, d, cmp, eps, ok, a.err);
+            else continue;
+            if (ret != LMR_RET_NONE) {
+                if constexpr (sizeof(T) >= 4) tile[e] = b;
+                else tile[e] = W(U(b));
+            }
+        }
+        if (ret != LMR_RET_NONE) {
+            __syncthreads();
+#pragma unroll
+            for (int k = 0; k < int(kSplit / 1024); k++) {
                 const uint32_t r = w.lo + threadIdx.x + uint32_t(k) * 1024u;
-                rec[k] = r;
                 if (r < w.hi) {
                     const uint32_t l = a.bin_lidx[r];
-                    const T v = a.scalar ? sv : reinterpret_cast<const T*>(a.bin_val)[r];
-                    uint8_t ok = 0;
-                    pre[k] = rmw_lds<T>(tile + l, acc, a.kind, v, cmp, eps, ok, a.err);
-                }
-            }
-            __syncthreads();
-            const int gop = delta_global_op(op);
-            for (uint32_t e = threadIdx.x; e < len; e += blockDim.x) {
-                T d;
-                if constexpr (sizeof(T) >= 4) d = tile[e];
-                else d = T(U(tile[e]));
-                uint8_t ok = 0;
-                T b;
-                if (U(to_bits(d)) != U(ident_bits)) b = rmw_global<T>(shard + e, gop, a.kind, d, cmp, eps, ok, a.err);
-                else if (ret != LMR_RET_NONE) b = rmw_global<T>(shard + e, LMR_OP_LOAD, a.kind, d, cmp, eps, ok, a.err);
-                else continue;
-                if (ret != LMR_RET_NONE) {
-                    if constexpr (sizeof(T) >= 4) tile[e] = b;
-                    else tile[e] = W(U(b));
-                }
-            }
-            if (ret != LMR_RET_NONE) {
-                __syncthreads();
-#pragma unroll
-                for (int k = 0; k < 16; k++) {
-                    const uint32_t r = rec[k];
-                    if (r < w.hi) {
-                        const uint32_t l = a.bin_lidx[r];
-                        T b;
-                        if constexpr (sizeof(T) >= 4) b = tile[l];
-                        else b = T(U(tile[l]));
-                        reinterpret_cast<T*>(a.results)[a.bin_pos[r]] = delta_finish<T>(op, b, pre[k]);
-                    }
+                    T b;
+                    if constexpr (sizeof(T) >= 4) b = tile[l];
+                    else b = T(U(tile[l]));
+                    reinterpret_cast<T*>(a.results)[r] = delta_finish<T>(op, b, pre[k]);
                 }
             }
         }
         __syncthreads();
+    }
+}
+
+// ---- un-partition of returned values ----------------------------------------
+// dst[k] = src[map[k]] over block-contiguous ranges of k (the forward pass's
+// chunks), so each block's reads stay within the runs its chunk produced and
+// hit L2; map[k] == ~0 marks an out-of-bounds record (left unwritten).
+template <int VB>
+__global__ __launch_bounds__(1024) void k_unpartition(const uint32_t* __restrict__ map, uint64_t n,
+                                                      const uint32_t* n_dev, uint64_t chunk,
+                                                      const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
+                                                      const uint8_t* __restrict__ ok_src, uint8_t* __restrict__ ok_dst) {
+    using V = typename idx_t<VB>::I;
+    const uint64_t m = n_dev ? uint64_t(*n_dev) : n;
+    const uint64_t lo = uint64_t(blockIdx.x) * chunk;
+    const uint64_t hi = min(lo + chunk, m);
+    const V* s = reinterpret_cast<const V*>(src);
+    V* d = reinterpret_cast<V*>(dst);
+    for (uint64_t k0 = lo + threadIdx.x; k0 < hi; k0 += 4 * 1024) {
+        uint32_t p[4];
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            const uint64_t k = k0 + uint64_t(j) * 1024;
+            p[j] = k < hi ? map[k] : 0xFFFFFFFFu;
+        }
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            if (p[j] == 0xFFFFFFFFu) continue;
+            const uint64_t k = k0 + uint64_t(j) * 1024;
+            d[k] = s[p[j]];
+            if (ok_src) ok_dst[k] = ok_src[p[j]];
+        }
     }
 }
 
@@ -705,7 +763,7 @@ size_t tiled_ws_bytes(uint64_t cap) {
     b += al((size_t(kMaxCoarse) * kMaxBinBlocks + 1) * 4);
     b += al(cap * 4) + al(cap * 8) + al(cap * 4);
     b += 2 * al((size_t(kMaxTiles) + 1) * 4) + al(size_t(kMaxTiles) / kScanItems * 4 + 256) + al(4);
-    b += al((size_t(kMaxTiles) + cap / kSplit + 2) * 16);
+    b += al((size_t(kMaxTiles) + 2 * (cap / kSplit) + 2) * 16);   // owner items + delta pieces
     return b;
 }
 
@@ -719,17 +777,17 @@ TiledWs carve_tiled_ws(uint8_t* base, uint64_t cap) {
     w.tile_start = reinterpret_cast<uint32_t*>(p); p += al((size_t(kMaxTiles) + 1) * 4);
     w.bin_lidx = reinterpret_cast<uint16_t*>(p); p += al(cap * 2);
     w.bin_val = p; p += al(cap * 8);
-    w.bin_pos = reinterpret_cast<uint32_t*>(p); p += al(cap * 4);
+    w.rpos = reinterpret_cast<uint32_t*>(p); p += al(cap * 4);
     w.total = reinterpret_cast<uint32_t*>(p); p += al(4);
     w.coarse_off = reinterpret_cast<uint32_t*>(p); p += al((size_t(kMaxCoarse) * kMaxBinBlocks + 1) * 4);
     w.tmp_idx = reinterpret_cast<uint32_t*>(p); p += al(cap * 4);
     w.tmp_val = p; p += al(cap * 8);
-    w.tmp_pos = reinterpret_cast<uint32_t*>(p); p += al(cap * 4);
+    w.qpos = reinterpret_cast<uint32_t*>(p); p += al(cap * 4);
     w.tile_items = reinterpret_cast<uint32_t*>(p); p += al((size_t(kMaxTiles) + 1) * 4);
     w.tile_items2 = reinterpret_cast<uint32_t*>(p); p += al((size_t(kMaxTiles) + 1) * 4);
     w.plan_partials = reinterpret_cast<uint32_t*>(p); p += al(size_t(kMaxTiles) / kScanItems * 4 + 256);
     w.item_count = reinterpret_cast<uint32_t*>(p); p += al(4);
-    w.items = p;
+    w.items = p;                                   // [kMaxTiles] owner items, then delta pieces
     return w;
 }
 
@@ -746,7 +804,7 @@ static int bin_blocks_cap() {
     return v;
 }
 static int tile_grid_cap() {
-    static int v = env_int("LMR_TILE_EXTRA_BLOCKS", 1024, 1, 1 << 24);
+    static int v = env_int("LMR_DELTA_BLOCKS", 1024, 1, 1 << 24);
     return v;
 }
 static int fine_blocks_cap() {
@@ -773,7 +831,8 @@ hipError_t launch_apply_tiled(int dtype, int index_size, const ApplyArgs& a, con
     b.chunk = (a.n + G - 1) / G;
     b.tile_shift = shift; b.num_tiles = uint32_t(num_tiles); b.G = uint32_t(G);
     b.counts = w.counts; b.bin_lidx = w.bin_lidx; b.bin_val = w.bin_val;
-    b.bin_pos = (a.ret != LMR_RET_NONE) ? w.bin_pos : nullptr;
+    const bool has_res = a.ret != LMR_RET_NONE;
+    b.rpos = has_res ? w.rpos : nullptr;
     b.err = a.err;
     const size_t hist_lds = size_t(num_tiles) * 4;
     hipError_t e;
@@ -803,8 +862,8 @@ hipError_t launch_apply_tiled(int dtype, int index_size, const ApplyArgs& a, con
         q.C = uint32_t((num_tiles + kFine - 1) / kFine);
         q.fine_off = w.counts; q.tile_start = w.tile_start; q.coarse_off = w.coarse_off;
         q.tmp_idx = w.tmp_idx; q.tmp_val = a.val ? w.tmp_val : nullptr;
-        q.tmp_pos = (a.ret != LMR_RET_NONE) ? w.tmp_pos : nullptr;
-        q.bin_lidx = w.bin_lidx; q.bin_val = w.bin_val; q.bin_pos = b.bin_pos;
+        q.qpos = has_res ? w.qpos : nullptr;
+        q.bin_lidx = w.bin_lidx; q.bin_val = w.bin_val; q.rpos = b.rpos;
         const uint64_t ncg = uint64_t(q.C) * G + 1;
         hipLaunchKernelGGL(k_coarse_offsets, dim3(unsigned((ncg + 255) / 256)), dim3(256), 0, s, q);
         e = dispatch_iw(index_size, [&](auto iw) {
@@ -854,30 +913,58 @@ hipError_t launch_apply_tiled(int dtype, int index_size, const ApplyArgs& a, con
                        w.tile_items2);
     e = scan_exclusive_u32(w.tile_items2, num_tiles, w.plan_partials, w.item_count, s);
     if (e != hipSuccess) return e;
+    TileItem* items = reinterpret_cast<TileItem*>(w.items);
     hipLaunchKernelGGL(k_tile_plan_fill, dim3(pg), dim3(256), 0, s, w.tile_start, uint32_t(num_tiles),
-                       w.tile_items2, w.tile_items, reinterpret_cast<TileItem*>(w.items));
+                       w.tile_items2, w.tile_items, items, items + kMaxTiles);
     TileArgs t;
     t.shard = a.shard; t.shard_len = a.shard_len; t.tile_shift = shift;
     t.kind = a.kind; t.op = a.op; t.ret = a.ret;
     t.cmp_bits = a.cmp_bits; t.eps_bits = a.eps_bits; t.val_bits = a.val_bits;
     t.scalar = (a.val == nullptr);
-    t.items = reinterpret_cast<const TileItem*>(w.items); t.item_count = w.item_count;
+    t.items = items; t.delta = items + kMaxTiles; t.delta_count = w.item_count;
     t.num_tiles = uint32_t(num_tiles);
     t.bin_lidx = w.bin_lidx; t.bin_val = w.bin_val;
-    t.bin_pos = w.bin_pos; t.results = a.results; t.ok = a.ok; t.err = a.err;
+    // results in binned order: reuse the temp buffers the partition is done with
+    uint8_t* res_bin = w.tmp_val;
+    uint8_t* ok_bin = reinterpret_cast<uint8_t*>(w.tmp_idx);
+    t.results = res_bin; t.ok = ok_bin; t.err = a.err;
     const size_t tile_lds = size_t(kTileBytes);
-    const uint64_t max_extra = op_combines(a.op) ? (a.n + kSplit - 1) / kSplit : 0;
-    const unsigned grid = unsigned(num_tiles + std::min<uint64_t>(max_extra, uint64_t(tile_grid_cap())));
-    return dispatch_dtype(dtype, [&](auto tag) {
+    const bool delta = op_combines(a.op) && a.n > thresh;
+    const unsigned dgrid = unsigned(std::min<uint64_t>(2 * ((a.n + kSplit - 1) / kSplit), uint64_t(tile_grid_cap())));
+    e = dispatch_dtype(dtype, [&](auto tag) {
         using T = decltype(tag);
-        if (a.op == LMR_OP_ADD)
-            hipLaunchKernelGGL((k_tile_apply<T, LMR_OP_ADD>), dim3(grid), dim3(1024), tile_lds, s, t);
-        else if (a.op == LMR_OP_FETCH_ADD)
-            hipLaunchKernelGGL((k_tile_apply<T, LMR_OP_FETCH_ADD>), dim3(grid), dim3(1024), tile_lds, s, t);
-        else
-            hipLaunchKernelGGL((k_tile_apply<T, -1>), dim3(grid), dim3(1024), tile_lds, s, t);
+        auto go = [&](auto opt) {
+            constexpr int OPT = decltype(opt)::value;
+            hipLaunchKernelGGL((k_tile_owner<T, OPT>), dim3(unsigned(num_tiles)), dim3(1024), tile_lds, s, t);
+            if (delta) hipLaunchKernelGGL((k_tile_delta<T, OPT>), dim3(dgrid), dim3(1024), tile_lds, s, t);
+        };
+        if (a.op == LMR_OP_ADD) go(std::integral_constant<int, LMR_OP_ADD>{});
+        else if (a.op == LMR_OP_FETCH_ADD) go(std::integral_constant<int, LMR_OP_FETCH_ADD>{});
+        else go(std::integral_constant<int, -1>{});
         return hipGetLastError();
     });
+    ps.end();
+    if (e != hipSuccess || !has_res) return e;
+    // un-partition: binned -> (temp ->) input order, each a block-contiguous gather
+    ProfScope pu(a.prof, LMR_STAGE_UNPARTITION, s);
+    const uint8_t* ok_src = (a.ret == LMR_RET_RESULT) ? ok_bin : nullptr;
+    auto gather = [&](const uint32_t* map, const uint32_t* n_dev, const uint8_t* src, uint8_t* dst,
+                      const uint8_t* oks, uint8_t* okd) {
+        switch (vb) {
+        case 1: hipLaunchKernelGGL((k_unpartition<1>), dim3(unsigned(G)), dim3(1024), 0, s, map, a.n, n_dev, b.chunk, src, dst, oks, okd); break;
+        case 2: hipLaunchKernelGGL((k_unpartition<2>), dim3(unsigned(G)), dim3(1024), 0, s, map, a.n, n_dev, b.chunk, src, dst, oks, okd); break;
+        case 4: hipLaunchKernelGGL((k_unpartition<4>), dim3(unsigned(G)), dim3(1024), 0, s, map, a.n, n_dev, b.chunk, src, dst, oks, okd); break;
+        default: hipLaunchKernelGGL((k_unpartition<8>), dim3(unsigned(G)), dim3(1024), 0, s, map, a.n, n_dev, b.chunk, src, dst, oks, okd); break;
+        }
+    };
+    if (num_tiles > uint64_t(kFine)) {
+        uint8_t* ok_tmp = ok_src ? reinterpret_cast<uint8_t*>(w.bin_lidx) : nullptr;
+        gather(w.rpos, w.total, res_bin, w.bin_val, ok_src, ok_tmp);                       // binned -> temp
+        gather(w.qpos, nullptr, w.bin_val, reinterpret_cast<uint8_t*>(a.results), ok_tmp, a.ok);  // temp -> input
+    } else {
+        gather(w.rpos, nullptr, res_bin, reinterpret_cast<uint8_t*>(a.results), ok_src, a.ok);
+    }
+    return hipGetLastError();
 }
 
 }  // namespace lmr

@@ -35,7 +35,8 @@ void prof_end(Prof* p, int stage, hipStream_t s);
 struct ProfScope {
     Prof* p; int st; hipStream_t s;
     ProfScope(Prof* p_, int st_, hipStream_t s_) : p(p_), st(st_), s(s_) { if (p) prof_begin(p, st, s); }
-    ~ProfScope() { if (p) prof_end(p, st, s); }
+    ~ProfScope() { end(); }
+    void end() { if (p) prof_end(p, st, s); p = nullptr; }
 };
 
 // Workspace carve-up of one tiled piece.
@@ -45,17 +46,17 @@ struct TiledWs {
     uint32_t* tile_start;  // [num_tiles + 1]
     uint16_t* bin_lidx;    // [cap]
     uint8_t* bin_val;      // [cap * 8]
-    uint32_t* bin_pos;     // [cap]
+    uint32_t* rpos;        // [cap] temp (two-level) or record (one-level) -> binned position
     uint32_t* total;       // [1]
     uint32_t* coarse_off;  // [kMaxTiles/128 * G + 1]  (two-level partition)
     uint32_t* tmp_idx;     // [cap]
     uint8_t* tmp_val;      // [cap * 8]
-    uint32_t* tmp_pos;     // [cap]
+    uint32_t* qpos;        // [cap] record -> temp position (two-level)
     uint32_t* tile_items;  // [kMaxTiles + 1] work items per tile, then their exclusive scan
     uint32_t* tile_items2; // [kMaxTiles + 1] work items per tile
     uint32_t* plan_partials;
     uint32_t* item_count;  // [1]
-    uint8_t* items;        // TileItem[kMaxTiles + cap / kSplit + 2]
+    uint8_t* items;        // TileItem[kMaxTiles] owner items, then delta pieces
 };
 size_t tiled_ws_bytes(uint64_t cap);
 TiledWs carve_tiled_ws(uint8_t* base, uint64_t cap);
