@@ -201,7 +201,6 @@ __global__ void k_tile_starts(const uint32_t* counts, uint32_t num_tiles, uint32
 // the per-block tile counts), so the tile apply is unchanged.
 constexpr int kFine = 128;
 constexpr int kFineShift = 7;
-constexpr int kRound = 4096;
 constexpr int kMaxCoarse = kMaxTiles / kFine;
 
 struct PartArgs {
@@ -265,9 +264,11 @@ __device__ __forceinline__ void small_excl_scan(const uint32_t* hist, uint32_t* 
 // Both passes are software-pipelined: the next round's global loads are issued
 // into registers right after the current round is staged in LDS, so they are
 // in flight while the staged round is written out.
-template <int IW, int VB>
+// RPT records per thread per round (kRound = RPT * 1024 records staged in LDS).
+template <int IW, int VB, int RPT>
 __global__ __launch_bounds__(1024) void k_coarse_scatter(PartArgs p) {
     using V = typename idx_t<VB>::I;
+    constexpr uint32_t kRound = RPT * 1024;
     __shared__ uint32_t hist[kMaxCoarse], base[kMaxCoarse], cursor[kMaxCoarse], tot;
     __shared__ uint32_t s_idx[kRound];
     __shared__ V s_val[kRound];
@@ -277,11 +278,11 @@ __global__ __launch_bounds__(1024) void k_coarse_scatter(PartArgs p) {
     for (uint32_t c = threadIdx.x; c < C; c += blockDim.x) cursor[c] = p.coarse_off[uint64_t(c) * p.G + g];
     const uint64_t lo = uint64_t(g) * p.chunk;
     const uint64_t hi = min(lo + p.chunk, p.n);
-    uint64_t m_raw[4];
-    V m_val[4];
+    uint64_t m_raw[RPT];
+    V m_val[RPT];
     auto load_round = [&](uint64_t r0) {
 #pragma unroll
-        for (int j = 0; j < 4; j++) {
+        for (int j = 0; j < RPT; j++) {
             const uint64_t k = r0 + uint64_t(j) * 1024 + threadIdx.x;
             const bool in = k < hi;
             m_raw[j] = in ? load_idx<IW>(p.idx, p.idx_stride, k) : ~uint64_t(0);
@@ -292,10 +293,10 @@ __global__ __launch_bounds__(1024) void k_coarse_scatter(PartArgs p) {
     for (uint64_t r0 = lo; r0 < hi; r0 += kRound) {
         for (uint32_t c = threadIdx.x; c < C; c += blockDim.x) hist[c] = 0;
         __syncthreads();
-        uint32_t m_rank[4], m_c[4];
-        bool m_ok[4];
+        uint32_t m_rank[RPT], m_c[RPT];
+        bool m_ok[RPT];
 #pragma unroll
-        for (int j = 0; j < 4; j++) {
+        for (int j = 0; j < RPT; j++) {
             m_ok[j] = m_raw[j] < p.shard_len;
             m_c[j] = uint32_t(m_raw[j] >> cshift);
             if (m_ok[j]) m_rank[j] = atomicAdd(&hist[m_c[j]], 1u);
@@ -304,7 +305,7 @@ __global__ __launch_bounds__(1024) void k_coarse_scatter(PartArgs p) {
         small_excl_scan(hist, base, C, &tot);
         __syncthreads();
 #pragma unroll
-        for (int j = 0; j < 4; j++) {
+        for (int j = 0; j < RPT; j++) {
             const uint64_t k = r0 + uint64_t(j) * 1024 + threadIdx.x;
             if (!m_ok[j]) {
                 if (p.qpos && k < hi) p.qpos[k] = 0xFFFFFFFFu;
@@ -333,20 +334,21 @@ __global__ __launch_bounds__(1024) void k_coarse_scatter(PartArgs p) {
 // Persistent over (coarse bucket c, producer block g) segments: block b takes
 // segments b, b + gridDim.x, ...; the first round of the next segment is
 // prefetched while the current segment's last round is written out.
-template <int VB>
+template <int VB, int RPT>
 __global__ __launch_bounds__(1024) void k_fine_scatter(PartArgs p) {
     using V = typename idx_t<VB>::I;
+    constexpr uint32_t kRound = RPT * 1024;
     __shared__ uint32_t hist[kFine], base[kFine], cursor[kFine], tot;
     __shared__ uint16_t s_l[kRound];
     __shared__ V s_val[kRound];
     __shared__ uint8_t s_f[kRound];
     const uint32_t nseg = p.C * p.G;
     const uint32_t lmask = (1u << p.tile_shift) - 1u;
-    uint32_t m_idx[4];
-    V m_val[4];
+    uint32_t m_idx[RPT];
+    V m_val[RPT];
     auto load_round = [&](uint32_t r0, uint32_t hi) {
 #pragma unroll
-        for (int j = 0; j < 4; j++) {
+        for (int j = 0; j < RPT; j++) {
             const uint32_t k = r0 + uint32_t(j) * 1024 + threadIdx.x;
             const bool in = k < hi;
             m_idx[j] = in ? p.tmp_idx[k] : 0xFFFFFFFFu;
@@ -370,10 +372,10 @@ __global__ __launch_bounds__(1024) void k_fine_scatter(PartArgs p) {
         for (uint32_t r0 = lo; r0 < hi; r0 += kRound) {
             for (uint32_t f = threadIdx.x; f < nf; f += blockDim.x) hist[f] = 0;
             __syncthreads();
-            uint32_t m_rank[4], m_f[4];
-            bool m_ok[4];
+            uint32_t m_rank[RPT], m_f[RPT];
+            bool m_ok[RPT];
 #pragma unroll
-            for (int j = 0; j < 4; j++) {
+            for (int j = 0; j < RPT; j++) {
                 m_ok[j] = r0 + uint32_t(j) * 1024 + threadIdx.x < hi;
                 m_f[j] = (m_idx[j] >> p.tile_shift) - t0;
                 if (m_ok[j]) m_rank[j] = atomicAdd(&hist[m_f[j]], 1u);
@@ -382,7 +384,7 @@ __global__ __launch_bounds__(1024) void k_fine_scatter(PartArgs p) {
             small_excl_scan(hist, base, nf, &tot);
             __syncthreads();
 #pragma unroll
-            for (int j = 0; j < 4; j++) {
+            for (int j = 0; j < RPT; j++) {
                 if (!m_ok[j]) continue;
                 const uint32_t q = base[m_f[j]] + m_rank[j];
                 s_l[q] = uint16_t(m_idx[j] & lmask);
@@ -807,6 +809,30 @@ static int tile_grid_cap() {
     static int v = env_int("LMR_DELTA_BLOCKS", 1024, 1, 1 << 24);
     return v;
 }
+// records per thread per round of the coarse / fine passes (LMR_COARSE_RPT, LMR_FINE_RPT: 4, 6 or 8)
+static int coarse_rpt() {
+    static int v = env_int("LMR_COARSE_RPT", 4, 4, 8);
+    return v;
+}
+static int fine_rpt() {
+    static int v = env_int("LMR_FINE_RPT", 4, 4, 8);
+    return v;
+}
+template <typename F>
+static void dispatch_vb_rpt(int vb, int rpt, F&& f) {
+    using std::integral_constant;
+    auto with_vb = [&](auto vbt) {
+        if (rpt >= 8) f(vbt, integral_constant<int, 8>{});
+        else if (rpt >= 6) f(vbt, integral_constant<int, 6>{});
+        else f(vbt, integral_constant<int, 4>{});
+    };
+    switch (vb) {
+    case 1: with_vb(integral_constant<int, 1>{}); break;
+    case 2: with_vb(integral_constant<int, 2>{}); break;
+    case 4: with_vb(integral_constant<int, 4>{}); break;
+    default: with_vb(integral_constant<int, 8>{}); break;
+    }
+}
 static int fine_blocks_cap() {
     static int v = env_int("LMR_FINE_BLOCKS", 512, 1, 1 << 20);
     return v;
@@ -868,12 +894,11 @@ hipError_t launch_apply_tiled(int dtype, int index_size, const ApplyArgs& a, con
         hipLaunchKernelGGL(k_coarse_offsets, dim3(unsigned((ncg + 255) / 256)), dim3(256), 0, s, q);
         e = dispatch_iw(index_size, [&](auto iw) {
             constexpr int IW = decltype(iw)::value;
-            switch (vb) {
-            case 1: hipLaunchKernelGGL((k_coarse_scatter<IW, 1>), dim3(unsigned(G)), dim3(1024), 0, s, q); break;
-            case 2: hipLaunchKernelGGL((k_coarse_scatter<IW, 2>), dim3(unsigned(G)), dim3(1024), 0, s, q); break;
-            case 4: hipLaunchKernelGGL((k_coarse_scatter<IW, 4>), dim3(unsigned(G)), dim3(1024), 0, s, q); break;
-            default: hipLaunchKernelGGL((k_coarse_scatter<IW, 8>), dim3(unsigned(G)), dim3(1024), 0, s, q); break;
-            }
+            auto go = [&](auto vbt, auto rpt) {
+                constexpr int VBc = decltype(vbt)::value, R = decltype(rpt)::value;
+                hipLaunchKernelGGL((k_coarse_scatter<IW, VBc, R>), dim3(unsigned(G)), dim3(1024), 0, s, q);
+            };
+            dispatch_vb_rpt(vb, coarse_rpt(), go);
             return hipGetLastError();
         });
         if (a.prof) prof_end(a.prof, LMR_STAGE_BIN_SCATTER, s);
@@ -881,12 +906,10 @@ hipError_t launch_apply_tiled(int dtype, int index_size, const ApplyArgs& a, con
         ProfScope pf(a.prof, LMR_STAGE_FINE_SCATTER, s);
         const uint64_t nseg = uint64_t(q.C) * G;
         const unsigned fgrid = unsigned(nseg < uint64_t(fine_blocks_cap()) ? nseg : fine_blocks_cap());
-        switch (vb) {
-        case 1: hipLaunchKernelGGL((k_fine_scatter<1>), dim3(fgrid), dim3(1024), 0, s, q); break;
-        case 2: hipLaunchKernelGGL((k_fine_scatter<2>), dim3(fgrid), dim3(1024), 0, s, q); break;
-        case 4: hipLaunchKernelGGL((k_fine_scatter<4>), dim3(fgrid), dim3(1024), 0, s, q); break;
-        default: hipLaunchKernelGGL((k_fine_scatter<8>), dim3(fgrid), dim3(1024), 0, s, q); break;
-        }
+        dispatch_vb_rpt(vb, fine_rpt(), [&](auto vbt, auto rpt) {
+            constexpr int VBc = decltype(vbt)::value, R = decltype(rpt)::value;
+            hipLaunchKernelGGL((k_fine_scatter<VBc, R>), dim3(fgrid), dim3(1024), 0, s, q);
+        });
         e = hipGetLastError();
     } else {
     ProfScope ps(a.prof, LMR_STAGE_BIN_SCATTER, s);

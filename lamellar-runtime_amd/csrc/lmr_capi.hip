@@ -411,10 +411,11 @@ int lmr_op_supported(uint32_t kind, uint32_t dtype, uint32_t op) {
 }
 
 // ---------------------------------------------------------------- pack
-lmr_status_t lmr_pack(lmr_ctx_t* ctx, const lmr_layout_t* layout, const uint64_t* d_gidx, uint64_t n,
-                      const void* d_vals, uint32_t dtype, uint32_t index_size, void* d_out_idx,
-                      void* d_out_vals, uint32_t* d_out_pos, uint64_t* d_dest_counts,
-                      uint64_t* d_dest_offsets, lmr_stream_t stream) {
+static lmr_status_t pack_common(lmr_ctx_t* ctx, const lmr_layout_t* layout, const uint64_t* d_gidx,
+                                uint64_t n, const void* d_vals, uint32_t dtype, uint32_t index_size,
+                                void* d_out_idx, void* d_out_vals, uint32_t* d_out_pos,
+                                uint64_t* d_dest_counts, uint64_t* d_dest_offsets, bool stable,
+                                lmr_stream_t stream) {
     if (!ctx || !valid_layout(layout) || !valid_iw(index_size) || dtype >= LMR_NUM_DTYPES ||
         !d_dest_offsets || n > 0xFFFFFFFFull || layout->num_pes > uint32_t(kMaxPackPes))
         return LMR_E_INVALID;
@@ -434,8 +435,25 @@ lmr_status_t lmr_pack(lmr_ctx_t* ctx, const lmr_layout_t* layout, const uint64_t
     a.dest_offsets = d_dest_offsets;
     a.err = ctx->d_err;
     a.prof = ctx->prof;
+    a.stable = stable;
     return hip_status(launch_pack(a, x.pack_counts, x.pack_partials, x.pack_total,
                                   reinterpret_cast<hipStream_t>(stream)));
+}
+
+lmr_status_t lmr_pack(lmr_ctx_t* ctx, const lmr_layout_t* layout, const uint64_t* d_gidx, uint64_t n,
+                      const void* d_vals, uint32_t dtype, uint32_t index_size, void* d_out_idx,
+                      void* d_out_vals, uint32_t* d_out_pos, uint64_t* d_dest_counts,
+                      uint64_t* d_dest_offsets, lmr_stream_t stream) {
+    return pack_common(ctx, layout, d_gidx, n, d_vals, dtype, index_size, d_out_idx, d_out_vals, d_out_pos,
+                       d_dest_counts, d_dest_offsets, true, stream);
+}
+
+lmr_status_t lmr_pack_unordered(lmr_ctx_t* ctx, const lmr_layout_t* layout, const uint64_t* d_gidx,
+                                uint64_t n, const void* d_vals, uint32_t dtype, uint32_t index_size,
+                                void* d_out_idx, void* d_out_vals, uint32_t* d_out_pos,
+                                uint64_t* d_dest_counts, uint64_t* d_dest_offsets, lmr_stream_t stream) {
+    return pack_common(ctx, layout, d_gidx, n, d_vals, dtype, index_size, d_out_idx, d_out_vals, d_out_pos,
+                       d_dest_counts, d_dest_offsets, false, stream);
 }
 
 // ---------------------------------------------------------------- apply

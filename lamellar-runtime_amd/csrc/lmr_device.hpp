@@ -112,6 +112,59 @@ __host__ __device__ inline bool pe_and_offset(const lmr_layout_t& L, uint64_t in
     return true;
 }
 
+// Same mapping with the runtime 64-bit divisions replaced by a double-precision
+// reciprocal and a one-step correction (exact for dividends below 2^52; larger
+// ones take the generic path). A u64 `/` is a ~100-instruction sequence on
+// CDNA, and the pack divides every record twice.
+struct FastLayout {
+    lmr_layout_t L;
+    uint64_t a, b, rem_index;          // orig_elem_per_pe + 1, orig_elem_per_pe, rem * a
+    double inv_a, inv_b, inv_np;
+};
+
+__host__ inline FastLayout make_fast_layout(const lmr_layout_t& L) {
+    FastLayout f;
+    f.L = L;
+    f.a = L.orig_elem_per_pe + 1;
+    f.b = L.orig_elem_per_pe;
+    f.rem_index = L.orig_remaining_elems * f.a;
+    f.inv_a = 1.0 / double(f.a);
+    f.inv_b = f.b ? 1.0 / double(f.b) : 0.0;
+    f.inv_np = L.num_pes ? 1.0 / double(L.num_pes) : 0.0;
+    return f;
+}
+
+__host__ __device__ __forceinline__ void fast_divmod(uint64_t n, uint64_t d, double inv, uint64_t& q,
+                                                     uint64_t& r) {
+    if (n < (uint64_t(1) << 52)) {
+        q = uint64_t(double(n) * inv);
+        r = n - q * d;
+        if (int64_t(r) < 0) { q--; r += d; }
+        else if (r >= d) { q++; r -= d; }
+    } else {
+        q = n / d;
+        r = n - q * d;
+    }
+}
+
+__host__ __device__ __forceinline__ bool pe_and_offset_fast(const FastLayout& f, uint64_t index,
+                                                            uint64_t& pe, uint64_t& off) {
+    if (f.L.sub) return pe_and_offset(f.L, index, pe, off);
+    if (!(f.L.size > index)) return false;
+    if (f.L.distribution == LMR_DIST_BLOCK) {
+        if (index < f.rem_index) {
+            fast_divmod(index, f.a, f.inv_a, pe, off);
+        } else {
+            uint64_t tp;
+            fast_divmod(index - f.rem_index, f.b, f.inv_b, tp, off);
+            pe = f.L.orig_remaining_elems + tp;
+        }
+    } else {
+        fast_divmod(index, f.L.num_pes, f.inv_np, off, pe);
+    }
+    return true;
+}
+
 // ---------------------------------------------------------------- errors
 __device__ __forceinline__ void raise_err(uint32_t* err, uint32_t bit) {
     if (err) __hip_atomic_fetch_or(err, bit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);

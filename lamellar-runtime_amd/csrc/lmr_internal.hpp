@@ -112,6 +112,7 @@ struct PackArgs {
     uint64_t* dest_offsets;  // [npes + 1]
     uint32_t* err;
     Prof* prof;
+    bool stable;             // true: input order within a PE (lmr_pack); false: LDS-staged runs
 };
 hipError_t launch_pack(const PackArgs& a, uint32_t* counts, uint32_t* partials, uint32_t* total,
                        hipStream_t s);

@@ -15,11 +15,14 @@
 // (indices, values, positions): coalesced for the apply kernels and for RCCL.
 #include "lmr_internal.hpp"
 #include "lmr_device.hpp"
+#include <stdlib.h>
+#include <type_traits>
 
 namespace lmr {
 
 struct PackK {
     lmr_layout_t L;
+    FastLayout F;
     const uint64_t* gidx;
     const uint8_t* vals;
     uint32_t vb;
@@ -35,17 +38,56 @@ struct PackK {
     uint32_t* err;
 };
 
+// Wave-aggregated LDS counting: one atomic per distinct key in the wave instead
+// of one per lane (a batch spreads over few PEs, so per-lane atomics on
+// hist[pe] serialise 64/npes-deep). Returns each active lane's rank among the
+// records counted so far under its key. Wave-uniform loop: every lane takes part
+// in the ballots.
+__device__ __forceinline__ uint32_t wave_agg_rank(uint32_t* hist, uint32_t key, bool active) {
+    const int lane = threadIdx.x & 63;
+    const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+    uint64_t todo = __ballot(active);
+    uint32_t rank = 0;
+    while (todo) {
+        const int leader = __ffsll((unsigned long long)todo) - 1;
+        const uint32_t x = __shfl(key, leader, 64);
+        const uint64_t m = __ballot(active && key == x);
+        uint32_t base = 0;
+        if (lane == leader) base = atomicAdd(&hist[x], uint32_t(__popcll(m)));
+        base = __shfl(base, leader, 64);
+        if (active && key == x) rank = base + uint32_t(__popcll(m & lt));
+        todo &= ~m;
+    }
+    return rank;
+}
+
 __global__ __launch_bounds__(1024) void k_pack_count(PackK p) {
     extern __shared__ uint32_t cnt[];
     for (uint32_t i = threadIdx.x; i < p.npes; i += blockDim.x) cnt[i] = 0;
     __syncthreads();
     const uint64_t lo = uint64_t(blockIdx.x) * p.chunk;
     const uint64_t hi = min(lo + p.chunk, p.n);
+    const bool agg = p.npes <= 16;
     bool oob = false;
-    for (uint64_t k = lo + threadIdx.x; k < hi; k += blockDim.x) {
-        uint64_t pe, off;
-        if (!pe_and_offset(p.L, p.gidx[k], pe, off)) { oob = true; continue; }
-        atomicAdd(&cnt[uint32_t(pe)], 1u);
+    constexpr int U = 4;
+    for (uint64_t b0 = lo; b0 < hi; b0 += U * 1024) {       // block-uniform: ballots need every lane
+        const uint64_t k0 = b0 + threadIdx.x;
+        uint64_t g[U];
+#pragma unroll
+        for (int j = 0; j < U; j++) {
+            const uint64_t k = k0 + uint64_t(j) * 1024;
+            g[j] = k < hi ? p.gidx[k] : ~uint64_t(0);
+        }
+#pragma unroll
+        for (int j = 0; j < U; j++) {
+            const uint64_t k = k0 + uint64_t(j) * 1024;
+            uint64_t pe = 0, off;
+            const bool in = k < hi;
+            const bool ok = in && pe_and_offset_fast(p.F, g[j], pe, off);
+            oob |= in && !ok;
+            if (agg) (void)wave_agg_rank(cnt, uint32_t(pe), ok);
+            else if (ok) atomicAdd(&cnt[uint32_t(pe)], 1u);
+        }
     }
     if (oob) raise_err(p.err, LMR_ERRBIT_OOB);
     __syncthreads();
@@ -90,7 +132,7 @@ __global__ __launch_bounds__(1024) void k_pack_scatter(PackK p) {
         __syncthreads();
         const uint64_t k = r0 + threadIdx.x;
         uint64_t pe = 0, off = 0;
-        bool valid = (k < hi) && pe_and_offset(p.L, p.gidx[k], pe, off);
+        bool valid = (k < hi) && pe_and_offset_fast(p.F, p.gidx[k], pe, off);
         const uint32_t mype = valid ? uint32_t(pe) : 0xFFFFFFFFu;
         // group lanes by PE (match-any by repeated ballot over distinct values)
         uint64_t remaining = __ballot(true);
@@ -128,6 +170,100 @@ __global__ __launch_bounds__(1024) void k_pack_scatter(PackK p) {
     }
 }
 
+// LDS-staged scatter for npes <= kStageMaxPes (the common case): rounds of
+// RPT * 1024 records are ranked per PE with LDS atomics, staged in LDS in PE
+// order and written out as long per-PE runs (~round/npes records), like the
+// apply's coarse pass. Not stable within a PE: no caller depends on the order of
+// records inside one destination's buffer (the apply is a parallel, per-element
+// atomic application, as the reference's concurrent AMs are).
+constexpr uint32_t kStageMaxPes = 128;
+
+__device__ __forceinline__ void stage_scan(const uint32_t* hist, uint32_t* base, uint32_t m) {
+    if (threadIdx.x < 64) {
+        const uint32_t l = threadIdx.x;
+        uint32_t a = (2 * l < m) ? hist[2 * l] : 0u, b = (2 * l + 1 < m) ? hist[2 * l + 1] : 0u;
+        uint32_t x = a + b, inc = x;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            uint32_t y = __shfl_up(inc, d, 64);
+            if (int(l) >= d) inc += y;
+        }
+        uint32_t ex = inc - x;
+        if (2 * l < m) base[2 * l] = ex;
+        if (2 * l + 1 < m) base[2 * l + 1] = ex + a;
+        if (l == 63) base[kStageMaxPes] = inc;
+    }
+}
+
+template <int IW, int VB, int RPT>
+__global__ __launch_bounds__(1024) void k_pack_stage(PackK p) {
+    using I = typename idx_t<IW>::I;
+    using V = typename idx_t<VB>::I;
+    constexpr uint32_t kRound = RPT * 1024;
+    __shared__ uint32_t hist[kStageMaxPes], base[kStageMaxPes + 1], cursor[kStageMaxPes];
+    __shared__ I s_off[kRound];
+    __shared__ V s_val[kRound];
+    __shared__ uint32_t s_pos[kRound];
+    __shared__ uint8_t s_pe[kRound];
+    const uint32_t np = p.npes;
+    const bool agg = np <= 16;
+    for (uint32_t i = threadIdx.x; i < np; i += blockDim.x) cursor[i] = p.counts[uint64_t(i) * p.G + blockIdx.x];
+    const uint64_t lo = uint64_t(blockIdx.x) * p.chunk;
+    const uint64_t hi = min(lo + p.chunk, p.n);
+    const V* vals = reinterpret_cast<const V*>(p.vals);
+    uint64_t m_g[RPT];
+    V m_v[RPT];
+    auto load_round = [&](uint64_t r0) {
+#pragma unroll
+        for (int j = 0; j < RPT; j++) {
+            const uint64_t k = r0 + uint64_t(j) * 1024 + threadIdx.x;
+            const bool in = k < hi;
+            m_g[j] = in ? p.gidx[k] : ~uint64_t(0);
+            m_v[j] = (in && vals) ? vals[k] : V(0);
+        }
+    };
+    load_round(lo);
+    for (uint64_t r0 = lo; r0 < hi; r0 += kRound) {
+        for (uint32_t i = threadIdx.x; i < np; i += blockDim.x) hist[i] = 0;
+        __syncthreads();
+        uint32_t m_rank[RPT], m_pe[RPT];
+        uint64_t m_off[RPT];
+#pragma unroll
+        for (int j = 0; j < RPT; j++) {
+            uint64_t pe = 0, off = 0;
+            const bool ok = (r0 + uint64_t(j) * 1024 + threadIdx.x < hi) && pe_and_offset_fast(p.F, m_g[j], pe, off);
+            m_pe[j] = ok ? uint32_t(pe) : 0xFFFFFFFFu;
+            m_off[j] = off;
+            if (agg) m_rank[j] = wave_agg_rank(hist, uint32_t(pe), ok);
+            else if (ok) m_rank[j] = atomicAdd(&hist[pe], 1u);
+        }
+        __syncthreads();
+        stage_scan(hist, base, np);
+        __syncthreads();
+#pragma unroll
+        for (int j = 0; j < RPT; j++) {
+            if (m_pe[j] == 0xFFFFFFFFu) continue;
+            const uint32_t q = base[m_pe[j]] + m_rank[j];
+            s_off[q] = I(m_off[j]);
+            s_val[q] = m_v[j];
+            if (p.out_pos) s_pos[q] = uint32_t(r0 + uint64_t(j) * 1024 + threadIdx.x);
+            s_pe[q] = uint8_t(m_pe[j]);
+        }
+        if (r0 + kRound < hi) load_round(r0 + kRound);
+        __syncthreads();
+        const uint32_t total = base[kStageMaxPes];
+        for (uint32_t q = threadIdx.x; q < total; q += blockDim.x) {
+            const uint32_t e = s_pe[q];
+            const uint32_t dst = cursor[e] + q - base[e];
+            reinterpret_cast<I*>(p.out_idx)[dst] = s_off[q];
+            if (vals) reinterpret_cast<V*>(p.out_vals)[dst] = s_val[q];
+            if (p.out_pos) p.out_pos[dst] = s_pos[q];
+        }
+        __syncthreads();
+        for (uint32_t i = threadIdx.x; i < np; i += blockDim.x) cursor[i] += hist[i];
+    }
+}
+
 __global__ void k_dest_offsets(const uint32_t* counts, uint32_t npes, uint32_t G, const uint32_t* total,
                                uint64_t* dest_offsets, uint64_t* dest_counts) {
     uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -141,6 +277,25 @@ __global__ void k_dest_offsets(const uint32_t* counts, uint32_t npes, uint32_t G
     }
 }
 
+template <typename F>
+static void dispatch_pack_stage(int iw, int vb, F&& f) {
+    using std::integral_constant;
+    auto with_iw = [&](auto iwt) {
+        switch (vb) {
+        case 1: f(iwt, integral_constant<int, 1>{}); break;
+        case 2: f(iwt, integral_constant<int, 2>{}); break;
+        case 4: f(iwt, integral_constant<int, 4>{}); break;
+        default: f(iwt, integral_constant<int, 8>{}); break;
+        }
+    };
+    switch (iw) {
+    case 1: with_iw(integral_constant<int, 1>{}); break;
+    case 2: with_iw(integral_constant<int, 2>{}); break;
+    case 4: with_iw(integral_constant<int, 4>{}); break;
+    default: with_iw(integral_constant<int, 8>{}); break;
+    }
+}
+
 hipError_t launch_pack(const PackArgs& a, uint32_t* counts, uint32_t* partials, uint32_t* total,
                        hipStream_t s) {
     const uint32_t npes = a.layout.num_pes;
@@ -149,7 +304,7 @@ hipError_t launch_pack(const PackArgs& a, uint32_t* counts, uint32_t* partials, 
     if (G > uint64_t(kMaxBinBlocks)) G = kMaxBinBlocks;
     if (G < 1) G = 1;
     PackK p;
-    p.L = a.layout; p.gidx = a.gidx; p.vals = a.vals; p.vb = a.val_bytes; p.n = a.n;
+    p.L = a.layout; p.F = make_fast_layout(a.layout); p.gidx = a.gidx; p.vals = a.vals; p.vb = a.val_bytes; p.n = a.n;
     p.iw = a.index_size; p.chunk = (a.n + G - 1) / G; if (p.chunk == 0) p.chunk = 1;
     p.G = uint32_t(G); p.npes = npes; p.counts = counts;
     p.out_idx = a.out_idx; p.out_vals = a.out_vals; p.out_pos = a.out_pos; p.err = a.err;
@@ -162,8 +317,17 @@ hipError_t launch_pack(const PackArgs& a, uint32_t* counts, uint32_t* partials, 
     }
     hipError_t e = scan_exclusive_u32(counts, uint64_t(npes) * G, partials, total, s);
     if (e != hipSuccess) return e;
-    if (a.n > 0)
-        hipLaunchKernelGGL(k_pack_scatter, dim3(unsigned(G)), dim3(1024), size_t(npes) * 17 * 4, s, p);
+    if (a.n > 0) {
+        if (!a.stable && npes <= kStageMaxPes) {
+            const int vbk = a.vals ? int(a.val_bytes) : 1;
+            dispatch_pack_stage(int(a.index_size), vbk, [&](auto iw, auto vb) {
+                hipLaunchKernelGGL((k_pack_stage<decltype(iw)::value, decltype(vb)::value, 4>), dim3(unsigned(G)),
+                                   dim3(1024), 0, s, p);
+            });
+        } else {
+            hipLaunchKernelGGL(k_pack_scatter, dim3(unsigned(G)), dim3(1024), size_t(npes) * 17 * 4, s, p);
+        }
+    }
     hipLaunchKernelGGL(k_dest_offsets, dim3((npes + 1 + 255) / 256), dim3(256),
                        0, s, counts, npes, uint32_t(G), total, a.dest_offsets, a.dest_counts);
     return hipGetLastError();

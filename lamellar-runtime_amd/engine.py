@@ -9,18 +9,21 @@ the local offset (Block, Cyclic and sub-arrays alike), bounds-checked on the
 device.
 
 N PEs (one per GPU): a collective step replaces the shmem lamellae:
-  lmr_pack (device, stable by destination PE, IndexSize-narrowed offsets)
+  lmr_pack_unordered (device, grouped by destination PE, IndexSize-narrowed offsets)
   -> header all-to-all (per destination: count, MVSI index, scalar value)
   -> all-to-all-v of indices and values (RCCL over xGMI)
   -> apply of every received segment (device)
   -> [fetch / result ops] reverse all-to-all-v of results + lmr_scatter_results
      back into input order (operations/handle.rs:315-317).
+The step is cut into chunks and software-pipelined over a pack stream, the
+RCCL stream and an apply stream (_distributed).
 Every PE must issue the same sequence of batch calls (a PE with nothing to
 send passes an empty batch): the exchange is collective where the reference's
 AMs are one-sided.
 """
 from __future__ import annotations
 
+import contextlib
 import numbers
 import os
 
@@ -163,81 +166,205 @@ def _local(arr, k, dt, op, i_scalar, idx, v_scalar, vals, n, mvsi, results, ok, 
                 vals if v_scalar else 0, n, results, ok, cmp_bits, eps_bits)
 
 
+def _exchange_chunk() -> int:
+    """Records per exchange chunk (LAMELLAR_EXCHANGE_CHUNK, default 2^26), at most
+    2^27 so one chunk's value bytes stay below 2^31 per peer."""
+    return min(1 << 27, max(1, int(os.environ.get("LAMELLAR_EXCHANGE_CHUNK", str(1 << 26)))))
+
+
+class _Streams:
+    """Pack/exchange and apply streams of one batch on a device (no-ops on CPU)."""
+
+    def __init__(self, k):
+        self.dev = getattr(k, "is_device", True) and k.device.type == "cuda"
+        if self.dev:
+            self.main = torch.cuda.current_stream(k.device)
+            self.pack = torch.cuda.Stream(k.device)
+            self.apply = torch.cuda.Stream(k.device)
+            self.pack.wait_stream(self.main)
+            self.apply.wait_stream(self.main)
+
+    def on(self, which):
+        if not self.dev:
+            return contextlib.nullcontext()
+        return torch.cuda.stream(getattr(self, which))
+
+    def used_on(self, which, *tensors):
+        """Tell the caching allocator that `tensors` are read/written on stream `which`."""
+        if self.dev:
+            st = getattr(self, which)
+            for t in tensors:
+                if t is not None and t.is_cuda:
+                    t.record_stream(st)
+
+    def join(self):
+        if self.dev:
+            self.main.wait_stream(self.pack)
+            self.main.wait_stream(self.apply)
+
+
 def _distributed(arr, k, dt, op, ret, i_scalar, idx, v_scalar, vals, n, mvsi, results, ok,
                  cmp_bits, eps_bits):
+    """Chunked, software-pipelined exchange.
+
+    The batch is cut into chunks of LAMELLAR_EXCHANGE_CHUNK records. Per chunk j:
+    pack (pack stream) -> header all-to-all (counts, MVSI index, scalar value)
+    -> async all-to-all-v of indices and values (RCCL stream) -> the apply
+    stream waits for the exchange and applies every source's records in one
+    call. Chunk j's exchange overlaps chunk j+1's pack and chunk j-1's apply;
+    returned values of chunk j travel back (async) after chunk j+1's exchange
+    has been issued, then lmr_scatter_results puts them in input order.
+
+    Collective: every PE issues the same sequence. PEs agree on the chunk count
+    through the first header (column 4 = the sender's chunk count); a PE past
+    its own last chunk sends empty chunks.
+    """
     team = arr.team
     npes = team.num_pes()
     iw = arr.index_size()
     eb = dt.bytes
-    header = torch.zeros(npes, 4, dtype=torch.int64)
-    # ---- pack (sender side) ----
+    returning = ret != BatchReturnType.None_
+    st = _Streams(k)
+    chunk = _exchange_chunk()
     if mvsi:
-        pe, off = _host_map(arr, idx)
-        header[pe, 0] = n
-        header[:, 1] = -1
-        header[pe, 1] = off
-        send_idx = k.empty(0, torch.uint8)
-        send_vals = vals.view(torch.uint8) if vals.dtype != torch.uint8 else vals
-        pos = None
+        my_k = 1
+        mvsi_pe, mvsi_off = _host_map(arr, idx)
     else:
         if i_scalar:
             idx = torch.tensor([idx], dtype=torch.int64, device=k.device)
         m = int(idx.numel())
-        send_idx, send_vals, pos, counts_t = k.pack(arr.layout, idx, m, None if v_scalar else vals, dt, iw)
-        header[:, 0] = counts_t.cpu()
-        header[:, 1] = -1
-        if v_scalar:
-            header[:, 2] = 1
-            header[:, 3] = torch.tensor(np.array([vals & 0xFFFFFFFFFFFFFFFF], dtype=np.uint64).view(np.int64))
-        if send_vals is None:
-            send_vals = k.empty(0, torch.uint8)
-    send_counts = header[:, 0].tolist()
-    # ---- exchange (collective) ----
-    rh = team.alltoall_header(header)
-    recv_counts = rh[:, 0].tolist()
-    idx_send_splits = [c * iw if header[p, 1] < 0 else 0 for p, c in enumerate(send_counts)]
-    idx_recv_splits = [c * iw if rh[p, 1] < 0 else 0 for p, c in enumerate(recv_counts)]
-    val_send_splits = [0 if header[p, 2] else c * eb for p, c in enumerate(send_counts)]
-    val_recv_splits = [0 if rh[p, 2] else c * eb for p, c in enumerate(recv_counts)]
-    r_idx = team.alltoallv(send_idx, idx_send_splits, idx_recv_splits)
-    r_vals = team.alltoallv(send_vals, val_send_splits, val_recv_splits)
-    # ---- apply every received segment ----
-    total_recv = int(sum(recv_counts))
-    r_res = k.empty(total_recv * eb, torch.uint8) if ret != BatchReturnType.None_ else None
-    r_ok = k.empty(total_recv, torch.uint8) if ret == BatchReturnType.Result else None
+        my_k = max(1, -(-m // chunk))
+    sbits = (vals & 0xFFFFFFFFFFFFFFFF) if (v_scalar and not mvsi) else 0
     shard, slen = arr.local_shard(), arr.num_elems_local()
+    empty_u8 = k.empty(0, torch.uint8)
+
+    def pack_chunk(j):
+        """-> (send_idx, send_vals, pos, counts (device or host), lo, hi)"""
+        if mvsi:
+            if j > 0:
+                return empty_u8, empty_u8, None, torch.zeros(npes, dtype=torch.int64), 0, 0
+            c = torch.zeros(npes, dtype=torch.int64)
+            c[mvsi_pe] = n
+            sv = vals.view(torch.uint8) if vals.dtype != torch.uint8 else vals
+            return empty_u8, sv, None, c, 0, n
+        lo, hi = min(m, j * chunk), min(m, (j + 1) * chunk)
+        with st.on("pack"):
+            si, sv, pos, counts = k.pack(arr.layout, idx[lo:hi], hi - lo,
+                                         None if v_scalar else vals[lo:hi], dt, iw,
+                                         stable=False, want_pos=returning)
+        return si, (sv if sv is not None else empty_u8), pos, counts, lo, hi
+
+    def send_back(p):
+        """Reverse exchange of a chunk's returned values + scatter into input order."""
+        r_res, r_ok, recv_counts, send_counts, pos, lo, hi = p
+        with st.on("apply"):
+            back, wb = team.alltoallv_async(r_res, [c * eb for c in recv_counts],
+                                            [c * eb for c in send_counts], eb)
+            back_ok, wo = (team.alltoallv_async(r_ok, recv_counts, send_counts)
+                           if r_ok is not None else (None, None))
+            wb.wait()
+            if wo is not None:
+                wo.wait()
+            st.used_on("apply", back, back_ok, pos)
+            nsent = int(sum(send_counts))
+            if mvsi:
+                results.view(torch.uint8)[:nsent * eb].copy_(back[:nsent * eb])
+                if ok is not None:
+                    ok[:nsent].copy_(back_ok[:nsent])
+            elif nsent:
+                k.scatter_results(back, pos, nsent, eb, results[lo:hi], back_ok,
+                                  ok[lo:hi] if ok is not None else None)
+
+    nchunks = my_k
+    nxt = pack_chunk(0)
+    pending = None
+    j = 0
+    while j < nchunks:
+        send_idx, send_vals, pos, counts, lo, hi = nxt
+        with st.on("pack"):
+            send_counts = counts.cpu() if counts.is_cuda else counts      # waits for this pack only
+        header = torch.zeros(npes, 5, dtype=torch.int64)
+        header[:, 0] = send_counts
+        header[:, 1] = -1
+        if mvsi and j == 0:
+            header[mvsi_pe, 1] = mvsi_off
+        if v_scalar and not mvsi:
+            header[:, 2] = 1
+            header[:, 3] = torch.tensor(np.array([sbits], dtype=np.uint64).view(np.int64))
+        header[:, 4] = my_k
+        with st.on("pack"):
+            rh = team.alltoall_header(header)
+        if j == 0:
+            nchunks = int(rh[:, 4].max())
+        send_counts = header[:, 0].tolist()
+        recv_counts = rh[:, 0].tolist()
+        idx_ss = [c * iw if header[p, 1] < 0 else 0 for p, c in enumerate(send_counts)]
+        idx_rs = [c * iw if rh[p, 1] < 0 else 0 for p, c in enumerate(recv_counts)]
+        val_ss = [0 if header[p, 2] else c * eb for p, c in enumerate(send_counts)]
+        val_rs = [0 if rh[p, 2] else c * eb for p, c in enumerate(recv_counts)]
+        with st.on("pack"):
+            r_idx, w_i = team.alltoallv_async(send_idx, idx_ss, idx_rs, iw)
+            r_vals, w_v = team.alltoallv_async(send_vals, val_ss, val_rs, eb)
+        # next chunk's pack runs while this chunk is on the wire
+        nxt = pack_chunk(j + 1) if j + 1 < nchunks else None
+        if pending is not None:
+            send_back(pending)
+            pending = None
+        total = int(sum(recv_counts))
+        with st.on("apply"):
+            w_i.wait()
+            w_v.wait()
+            st.used_on("apply", r_idx, r_vals)
+            r_res = k.empty(total * eb, torch.uint8) if returning else None
+            r_ok = k.empty(total, torch.uint8) if ret == BatchReturnType.Result else None
+            _apply_received(k, arr, dt, op, shard, slen, rh, recv_counts, iw, eb, r_idx, r_vals,
+                            r_res, r_ok, cmp_bits, eps_bits)
+        if returning:
+            pending = (r_res, r_ok, recv_counts, send_counts, pos, lo, hi)
+        j += 1
+    if pending is not None:
+        send_back(pending)
+    st.join()
+
+
+def _apply_received(k, arr, dt, op, shard, slen, rh, recv_counts, iw, eb, r_idx, r_vals, r_res, r_ok,
+                    cmp_bits, eps_bits):
+    """Apply one chunk's received records: consecutive sources with the same
+    value form (array values / the same scalar) go in one call; MVSI sources
+    one by one (their block is applied as one atomic unit)."""
+    npes = len(recv_counts)
     io = vo = ro = 0
-    for s in range(npes):
+    s = 0
+    while s < npes:
         c = int(recv_counts[s])
         if c == 0:
+            s += 1
             continue
-        seg_res = r_res[ro * eb:(ro + c) * eb] if r_res is not None else None
-        seg_ok = r_ok[ro:ro + c] if r_ok is not None else None
         if rh[s, 1] >= 0:
             k.apply_mvsi(shard, slen, arr.kind, dt, op, r_vals[vo:vo + c * eb], c, int(rh[s, 1]),
-                         seg_res, seg_ok, cmp_bits, eps_bits)
+                         r_res[ro * eb:(ro + c) * eb] if r_res is not None else None,
+                         r_ok[ro:ro + c] if r_ok is not None else None, cmp_bits, eps_bits)
             vo += c * eb
+            ro += c
+            s += 1
+            continue
+        scalar, bits = int(rh[s, 2]), int(rh[s, 3])
+        e, cnt = s, 0
+        while e < npes and (int(recv_counts[e]) == 0 or
+                            (rh[e, 1] < 0 and int(rh[e, 2]) == scalar and (not scalar or int(rh[e, 3]) == bits))):
+            cnt += int(recv_counts[e])
+            e += 1
+        seg_idx = r_idx[io:io + cnt * iw]
+        seg_res = r_res[ro * eb:(ro + cnt) * eb] if r_res is not None else None
+        seg_ok = r_ok[ro:ro + cnt] if r_ok is not None else None
+        if scalar:
+            ubits = int(np.array([bits], dtype=np.int64).view(np.uint64)[0])
+            k.apply_soa(shard, slen, arr.kind, dt, op, seg_idx, iw, None, ubits, cnt, seg_res, seg_ok,
+                        cmp_bits, eps_bits)
         else:
-            seg_idx = r_idx[io:io + c * iw]
-            io += c * iw
-            if rh[s, 2]:
-                bits = int(np.array([int(rh[s, 3])], dtype=np.int64).view(np.uint64)[0])
-                k.apply_soa(shard, slen, arr.kind, dt, op, seg_idx, iw, None, bits, c, seg_res, seg_ok,
-                            cmp_bits, eps_bits)
-            else:
-                k.apply_soa(shard, slen, arr.kind, dt, op, seg_idx, iw, r_vals[vo:vo + c * eb], 0, c,
-                            seg_res, seg_ok, cmp_bits, eps_bits)
-                vo += c * eb
-        ro += c
-    if ret == BatchReturnType.None_:
-        return
-    # ---- results back to the sender, into input order ----
-    back = team.alltoallv(r_res, [c * eb for c in recv_counts], [c * eb for c in send_counts])
-    back_ok = team.alltoallv(r_ok, recv_counts, send_counts) if r_ok is not None else None
-    nsent = int(sum(send_counts))
-    if mvsi:
-        results.view(torch.uint8)[:nsent * eb].copy_(back[:nsent * eb])
-        if ok is not None:
-            ok[:nsent].copy_(back_ok[:nsent])
-    else:
-        k.scatter_results(back, pos, nsent, eb, results, back_ok, ok)
+            k.apply_soa(shard, slen, arr.kind, dt, op, seg_idx, iw, r_vals[vo:vo + cnt * eb], 0, cnt,
+                        seg_res, seg_ok, cmp_bits, eps_bits)
+            vo += cnt * eb
+        io += cnt * iw
+        ro += cnt
+        s = e

@@ -71,7 +71,7 @@ class DeviceKernels:
         """Grow the tiled-apply workspace (allocation: call outside timed regions)."""
         n = min(int(n), self.max_ws_records)
         if n > self.reserved:
-            torch.cuda.current_stream(self.device).synchronize()
+            torch.cuda.synchronize(self.device)     # the workspace may be in use on any stream
             check(self.lib.lmr_ctx_reserve(self.ctx, n), "lmr_ctx_reserve")
             self.reserved = n
 
@@ -161,18 +161,19 @@ class DeviceKernels:
                                      _p(ok), self.stream())
         check(st, "lmr_apply_mvsi")
 
-    def pack(self, layout, gidx, n, vals, dt, iw):
-        """Stable partition by destination PE -> (idx, vals, pos, counts[int64 host list])."""
+    def pack(self, layout, gidx, n, vals, dt, iw, stable=True, want_pos=True):
+        """Partition by destination PE -> (idx, vals, pos, counts[int64 device]).
+        stable=False: lmr_pack_unordered (no order inside a PE's range)."""
         npes = layout.num_pes
         out_idx = self.empty(n * iw, torch.uint8)
         out_vals = self.empty(n * dt.bytes, torch.uint8) if vals is not None else None
-        out_pos = self.empty(n, torch.int32)
+        out_pos = self.empty(n, torch.int32) if want_pos else None
         counts = self.empty(npes, torch.int64)
         offsets = self.empty(npes + 1, torch.int64)
-        st = self.lib.lmr_pack(self.ctx, byref(layout), _p(gidx), int(n), _p(vals), int(dt.code), int(iw),
-                               _p(out_idx), _p(out_vals), _p(out_pos), _p(counts), _p(offsets),
-                               self.stream())
-        check(st, "lmr_pack")
+        fn = self.lib.lmr_pack if stable else self.lib.lmr_pack_unordered
+        st = fn(self.ctx, byref(layout), _p(gidx), int(n), _p(vals), int(dt.code), int(iw),
+                _p(out_idx), _p(out_vals), _p(out_pos), _p(counts), _p(offsets), self.stream())
+        check(st, "lmr_pack" if stable else "lmr_pack_unordered")
         return out_idx, out_vals, out_pos, counts
 
     def scatter_results(self, res_in, pos, n, eb, res_out, ok_in=None, ok_out=None):

@@ -27,6 +27,35 @@ def _env_int(*names, default=None):
     return default
 
 
+_WIDE = {8: torch.int64, 4: torch.int32, 2: torch.int16, 1: torch.uint8}
+_MAX_SPLIT = (1 << 31) - 1
+
+
+def _widen(send, recv, send_splits, recv_splits, unit):
+    """View 1-D uint8 buffers as `unit`-byte integers (unit 4 or 8: the record
+    field width, the same on every PE, so all ranks agree on the element type)
+    so per-peer element counts stay below 2^31 (RCCL/NCCL all-to-all-v counts
+    are signed 32-bit); split sizes converted to elements."""
+    ss = [int(x) for x in send_splits]
+    rs = [int(x) for x in recv_splits]
+    if unit in (4, 8) and send.dtype == torch.uint8 and recv.dtype == torch.uint8:
+        if send.storage_offset() % unit:
+            send = send.clone()
+        send, recv = send.view(_WIDE[unit]), recv.view(_WIDE[unit])
+        ss, rs = [x // unit for x in ss], [x // unit for x in rs]
+    if max(ss + rs + [0]) > _MAX_SPLIT:
+        raise ValueError("exchange split of %d elements exceeds 2^31 - 1; lower LAMELLAR_EXCHANGE_CHUNK"
+                         % max(ss + rs))
+    return send, recv, ss, rs
+
+
+class _Done:
+    """Work handle of an exchange that has already completed."""
+
+    def wait(self):
+        return True
+
+
 class LamellarTeam:
     def __init__(self, num_pes, my_pe, device, kernels, group=None):
         self._num_pes = num_pes
@@ -60,7 +89,7 @@ class LamellarTeam:
         dist.all_to_all_single(r, s, group=self.group)
         return r.cpu()
 
-    def alltoallv(self, send: torch.Tensor, send_splits, recv_splits) -> torch.Tensor:
+    def alltoallv(self, send: torch.Tensor, send_splits, recv_splits, unit=1) -> torch.Tensor:
         """Byte / element all-to-all-v of a 1-D tensor with per-PE split sizes."""
         total = int(sum(recv_splits))
         if not self._collective():
@@ -68,9 +97,25 @@ class LamellarTeam:
         dev = send.device
         s = send.to(self.comm_device).contiguous()
         r = torch.empty(total, dtype=send.dtype, device=self.comm_device)
-        dist.all_to_all_single(r, s, output_split_sizes=[int(x) for x in recv_splits],
-                               input_split_sizes=[int(x) for x in send_splits], group=self.group)
+        sw, rw, ss, rs = _widen(s, r, send_splits, recv_splits, unit)
+        dist.all_to_all_single(rw, sw, output_split_sizes=rs, input_split_sizes=ss, group=self.group)
         return r.to(dev)
+
+    def alltoallv_async(self, send: torch.Tensor, send_splits, recv_splits, unit=1):
+        """Asynchronous alltoallv -> (recv tensor, work). work.wait() orders the
+        caller's current stream after the transfer (RCCL) or blocks until it is
+        done (gloo). The recv tensor lives on the comm device."""
+        total = int(sum(recv_splits))
+        if not self._collective():
+            return send[:total].clone(), _Done()
+        if send.device != self.comm_device:
+            # host-side backend (gloo) with device tensors: synchronous round trip
+            return self.alltoallv(send, send_splits, recv_splits, unit), _Done()
+        r = torch.empty(total, dtype=send.dtype, device=self.comm_device)
+        sw, rw, ss, rs = _widen(send.contiguous(), r, send_splits, recv_splits, unit)
+        w = dist.all_to_all_single(rw, sw, output_split_sizes=rs, input_split_sizes=ss, group=self.group,
+                                   async_op=True)
+        return r, w
 
     def _collective(self):
         # a 1-PE world still goes through the collective when a process group

@@ -51,7 +51,7 @@ class CpuTestKernels:
             from lamellar_runtime_amd import LamellarError
             raise LamellarError(2, "test double error")
 
-    def pack(self, layout, gidx, n, vals, dt, iw):
+    def pack(self, layout, gidx, n, vals, dt, iw, stable=True, want_pos=True):
         g = gidx.numpy().view(np.uint64)[:n]
         pes, offs = np.zeros(n, np.int64), np.zeros(n, np.uint64)
         for j in range(n):
@@ -121,11 +121,13 @@ class CpuTestKernels:
             ok_out.numpy()[p] = ok_in.numpy()[:n]
 
 
-def _worker(rank, ws, port, outdir, dist_kind):
+def _worker(rank, ws, port, outdir, dist_kind, chunk=None, ragged=False):
     sys.path.insert(0, ROOT)
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
                       WORLD_SIZE=str(ws), LOCAL_RANK=str(rank))
+    if chunk:
+        os.environ["LAMELLAR_EXCHANGE_CHUNK"] = str(chunk)
     from _lamellar_bootstrap import load_package
     lam = load_package()
     from test_dist_gloo import CpuTestKernels
@@ -136,8 +138,9 @@ def _worker(rank, ws, port, outdir, dist_kind):
     arr = lam.AtomicArray(world.team(), n_len, dist_kind, "u64")
     res = {}
     # MVMI add with collisions
-    gi = rng.integers(0, n_len, 3000).astype(np.uint64)
-    gv = rng.integers(0, 2**40, 3000).astype(np.uint64)
+    nrec = 3000 if (me == 0 or not ragged) else 1234      # ragged: PEs with different chunk counts
+    gi = rng.integers(0, n_len, nrec).astype(np.uint64)
+    gv = rng.integers(0, 2**40, nrec).astype(np.uint64)
     arr.batch_add(gi, gv).block()
     world.barrier()
     res["after_add"] = arr.to_numpy()
@@ -151,6 +154,14 @@ def _worker(rank, ws, port, outdir, dist_kind):
     arr.batch_add(5, np.arange(1, 11, dtype=np.uint64)).block()
     world.barrier()
     res["after_mvsi"] = arr.to_numpy()
+    if ragged:
+        # mixed shapes in one collective call: PE 0 MVSI, PE 1 MVMI
+        if me == 0:
+            arr.batch_add(7, np.arange(1, 5, dtype=np.uint64)).block()
+        else:
+            arr.batch_add(np.array([1, 2, 3], dtype=np.uint64), np.array([100, 200, 300], dtype=np.uint64)).block()
+        world.barrier()
+        res["after_mixed"] = arr.to_numpy()
     # compare_exchange on PE-owned indices: all succeed
     ci = np.arange(me, n_len, ws, dtype=np.uint64)
     cur = res["after_mvsi"][ci]
@@ -165,12 +176,17 @@ def _worker(rank, ws, port, outdir, dist_kind):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("dist_kind", [0, 1], ids=["Block", "Cyclic"])
-def test_two_pe_exchange_gloo(orc, dist_kind):
+@pytest.mark.parametrize("dist_kind,chunk,ragged", [(0, None, False), (1, None, False), (0, 700, True),
+                                                     (1, 256, True)],
+                         ids=["Block", "Cyclic", "Block-chunked-ragged", "Cyclic-chunked-ragged"])
+def test_two_pe_exchange_gloo(orc, dist_kind, chunk, ragged):
+    """chunk: LAMELLAR_EXCHANGE_CHUNK (several pipelined chunks per batch); ragged:
+    PEs with different batch lengths (different chunk counts) and a call where one
+    PE passes an MVSI shape and the other an MVMI one."""
     ws = 2
-    port = 29600 + dist_kind * 7 + (os.getpid() % 200)
+    port = 29600 + dist_kind * 7 + (13 if ragged else 0) + (os.getpid() % 200)
     with tempfile.TemporaryDirectory() as d:
-        mp.spawn(_worker, args=(ws, port, d, dist_kind), nprocs=ws, join=True)
+        mp.spawn(_worker, args=(ws, port, d, dist_kind, chunk, ragged), nprocs=ws, join=True)
         pe = [dict(np.load(os.path.join(d, f"pe{r}.npz"))) for r in range(ws)]
     # oracle: both PEs' batch_add applied (order-independent wrapping add)
     from simworld import SimArray
@@ -197,5 +213,11 @@ def test_two_pe_exchange_gloo(orc, dist_kind):
     exp3[5] += np.uint64(2 * 55)
     assert np.array_equal(pe[1]["after_mvsi"], exp3)
     # compare_exchange(current=0): ok exactly where the element was 0
+    if ragged:
+        exp4 = exp3.copy()
+        exp4[7] += np.uint64(10)
+        exp4[[1, 2, 3]] += np.array([100, 200, 300], dtype=np.uint64)
+        for r in range(ws):
+            assert np.array_equal(pe[r]["after_mixed"], exp4)
     for r in range(ws):
         assert np.array_equal(pe[r]["cas_ok"].astype(bool), pe[r]["cas_cur"] == 0)

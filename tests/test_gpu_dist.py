@@ -98,7 +98,19 @@ def test_two_pes_one_gpu_gloo_exchange(orc, dist_kind):
         _check(orc, d, 2, dist_kind)
 
 
-def test_rccl_exchange_calls_one_rank(orc):
+@pytest.mark.parametrize("chunk", [None, 7000], ids=["one-chunk", "chunked"])
+def test_rccl_exchange_calls_one_rank(orc, chunk):
+    """chunked: LAMELLAR_EXCHANGE_CHUNK=7000 pipelines 29 chunks of the add and 3
+    of the fetch_add over the pack / RCCL / apply streams."""
+    env = {"LAMELLAR_FORCE_EXCHANGE": "1", "LAMELLAR_COMM_BACKEND": "nccl"}
+    if chunk:
+        env["LAMELLAR_EXCHANGE_CHUNK"] = str(chunk)
     with tempfile.TemporaryDirectory() as d:
-        _run(1, {"LAMELLAR_FORCE_EXCHANGE": "1", "LAMELLAR_COMM_BACKEND": "nccl"}, d, 0)
+        _run(1, env, d, 0)
         _check(orc, d, 1, 0)
+
+
+def test_two_pes_one_gpu_gloo_chunked(orc):
+    with tempfile.TemporaryDirectory() as d:
+        _run(2, {"LAMELLAR_COMM_BACKEND": "gloo", "LAMELLAR_EXCHANGE_CHUNK": "9000"}, d, 1)
+        _check(orc, d, 2, 1)

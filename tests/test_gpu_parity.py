@@ -273,6 +273,57 @@ def test_pack_matches_oracle(world, orc, lam):
         assert k.errors() == 0
 
 
+def test_pack_unordered_matches_oracle_per_pe(world, orc, lam):
+    """lmr_pack_unordered: same per-PE record sets as the reference's op buffers
+    (order inside a PE free; each record keeps its input position)."""
+    k = world.team().kernels
+    rng = np.random.default_rng(22)
+    import ctypes
+    from lamellar_runtime_amd import _capi
+    from opgen import record_dtype
+    for npes, dist, size, nrec, dt in [(2, 0, 1000, 20000, "u64"), (3, 1, 997, 20000, "u32"),
+                                       (8, 0, 1 << 20, 300000, "u64"), (8, 1, 65536 * 3 + 5, 100000, "u16"),
+                                       (5, 0, 300000, 70000, "f64"), (128, 1, 1 << 22, 200000, "u8"),
+                                       (200, 0, 1 << 20, 50000, "u64"), (7, 0, 7, 1000, "i32")]:
+        Lo = orc.layout_new(size, npes, 0, dist)
+        Ld = _capi.lmr_layout_t()
+        _capi.lib().lmr_layout_new(ctypes.byref(Ld), size, npes, 0, dist)
+        iw = orc.index_size(Lo)
+        npt = NP[dt]
+        gidx = rng.integers(0, size, nrec).astype(np.uint64)
+        vals = rng.integers(0, 120, nrec).astype(npt)
+        st, ams = orc.pack(Lo, CODE[dt], npt, gidx, vals, iw)
+        assert st == 0
+        dt_obj = lam.dtype_of(dt)
+        for with_vals in (True, False):
+            out_idx, out_vals, out_pos, counts = k.pack(Ld, to_dev(gidx).view(torch.int64), nrec,
+                                                        to_dev(vals) if with_vals else None, dt_obj, iw,
+                                                        stable=False)
+            k.synchronize()
+            counts = counts.cpu().numpy()
+            oi = out_idx.cpu().numpy().view({1: np.uint8, 2: np.uint16, 4: np.uint32, 8: np.uint64}[iw])
+            ov = out_vals.cpu().numpy().view(npt) if with_vals else None
+            op_ = out_pos.cpu().numpy().view(np.uint32)
+            rb, vo = orc.record_bytes(iw, CODE[dt]), orc.record_val_offset(iw, CODE[dt])
+            off = 0
+            for p in range(npes):
+                recs = [a for a in ams if a[0] == p]
+                c = int(sum(len(a[2]) for a in recs))
+                assert counts[p] == c, (npes, p)
+                if c == 0:
+                    continue
+                b = np.concatenate([a[1] for a in recs]).view(record_dtype(iw, dt, rb, vo))
+                pos = np.concatenate([a[2] for a in recs])
+                order = np.argsort(op_[off:off + c], kind="stable")
+                assert np.array_equal(op_[off:off + c][order].astype(np.uint64), pos), (npes, dist, p)
+                assert np.array_equal(oi[off:off + c][order], b["i"]), (npes, dist, p)
+                if with_vals:
+                    assert np.array_equal(ov[off:off + c][order], b["v"])
+                off += c
+            assert off == nrec
+        assert k.errors() == 0
+
+
 def test_scatter_results(world):
     k = world.team().kernels
     rng = np.random.default_rng(2)
