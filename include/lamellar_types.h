@@ -82,6 +82,10 @@ typedef enum {
 /* Distribution — src/array.rs:247-252. */
 typedef enum { LMR_DIST_BLOCK = 0, LMR_DIST_CYCLIC = 1 } lmr_distribution_t;
 
+/* Built-in array reductions (impl/src/array_reduce.rs:283-319: "sum", "prod",
+ * "max", "min"; src/array/unsafe.rs:1414-1557). */
+typedef enum { LMR_REDUCE_SUM = 0, LMR_REDUCE_PROD = 1, LMR_REDUCE_MAX = 2, LMR_REDUCE_MIN = 3 } lmr_reduce_op_t;
+
 /* Array kinds that carry the op path (src/array/atomic.rs:28-41, 524-533;
  * impl/src/array_ops.rs:546-572). On the device every kind applies each record
  * atomically per element; the kind only changes the CompareExchangeEps return

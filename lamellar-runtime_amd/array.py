@@ -124,6 +124,59 @@ class ArrayResultOpHandle(_Handle):
         return Ok(v[0]) if ok[0] else Err(v[0])
 
 
+REDUCE_OPS = {"sum": 0, "prod": 1, "max": 2, "min": 3}    # lmr_reduce_op_t
+
+
+def _reduce_combine(op, dt, a, b):
+    """One step of the reference's reduction closures (impl/src/array_reduce.rs:283-319)
+    in the element type: integers wrap, floats round as T."""
+    x, y = np.array([a], dtype=dt.np), np.array([b], dtype=dt.np)
+    with np.errstate(over="ignore", invalid="ignore"):
+        if op == "sum":
+            return (x + y)[0]
+        if op == "prod":
+            return (x * y)[0]
+    if op == "max":
+        return a if a > b else b
+    return a if a < b else b
+
+
+def _reduce_tree(op, dt, parts, lo, hi):
+    """The cross-PE tree of the reduction AM (impl/src/array_reduce.rs:90-107):
+    [lo, hi] splits at mid; None (an empty PE) is the identity."""
+    if lo == hi:
+        return parts[lo]
+    mid = (lo + hi) // 2
+    left = _reduce_tree(op, dt, parts, lo, mid)
+    right = _reduce_tree(op, dt, parts, mid + 1, hi)
+    if left is None:
+        return right
+    if right is None:
+        return left
+    return _reduce_combine(op, dt, left, right)
+
+
+class ReduceHandle:
+    """AmHandle<Option<T>> of UnsafeArray::reduce (src/array/unsafe.rs:1414-1557).
+    Collective here (every PE calls it; every PE gets the value) where the
+    reference's is one-sided."""
+
+    def __init__(self, array, op):
+        if op not in REDUCE_OPS:
+            raise LamellarError(LmrStatus.UNSUPPORTED, f"unknown reduction {op!r} (sum, prod, max, min)")
+        self._array, self._op = array, op
+
+    def block(self):
+        a = self._array
+        k = a.team.kernels
+        has, bits = k.reduce(a.local_data(), a.num_elems_local(), a.dtype, REDUCE_OPS[self._op])
+        mine = a.dtype.from_bits(bits) if has else None
+        parts = a.team.all_gather_object(mine)
+        return _reduce_tree(self._op, a.dtype, parts, 0, len(parts) - 1)
+
+    spawn = block
+
+
 # ------------------------------------------------------------------ arrays
 class LamellarArray:
     KIND = ArrayKind.Unsafe
@@ -271,6 +324,23 @@ class LamellarArray:
 
     def print(self):
         print(f"{type(self).__name__}<{self.dtype.name}> pe {self.my_pe()}: {self.local_numpy()}")
+
+    # ---- reductions (src/array/unsafe.rs:1414-1557) ----
+    def reduce(self, op: str) -> ReduceHandle:
+        """array.reduce("sum"|"prod"|"max"|"min").block() -> value, or None for an empty array."""
+        return ReduceHandle(self, op)
+
+    def sum(self) -> ReduceHandle:
+        return self.reduce("sum")
+
+    def prod(self) -> ReduceHandle:
+        return self.reduce("prod")
+
+    def max(self) -> ReduceHandle:
+        return self.reduce("max")
+
+    def min(self) -> ReduceHandle:
+        return self.reduce("min")
 
     # ---- op plumbing ----
     def _batch(self, op, index, val, current=None, eps=None):

@@ -148,10 +148,21 @@ __global__ __launch_bounds__(kBinBlock) void k_bin_count(BinArgs b) {
     const uint64_t lo = uint64_t(blockIdx.x) * b.chunk;
     const uint64_t hi = min(lo + b.chunk, b.n);
     bool oob = false;
-    for (uint64_t k = lo + threadIdx.x; k < hi; k += blockDim.x) {
-        uint64_t idx = load_idx<IW>(b.idx, b.idx_stride, k);
-        if (idx >= b.shard_len) { oob = true; continue; }
-        atomicAdd(&hist[uint32_t(idx >> b.tile_shift)], 1u);
+    constexpr int U = 4;                      // U loads in flight per thread before the LDS atomics
+    for (uint64_t k0 = lo + threadIdx.x; k0 < hi; k0 += U * uint64_t(blockDim.x)) {
+        uint64_t ix[U];
+#pragma unroll
+        for (int j = 0; j < U; j++) {
+            const uint64_t k = k0 + uint64_t(j) * blockDim.x;
+            ix[j] = k < hi ? load_idx<IW>(b.idx, b.idx_stride, k) : ~uint64_t(0);
+        }
+#pragma unroll
+        for (int j = 0; j < U; j++) {
+            const uint64_t k = k0 + uint64_t(j) * blockDim.x;
+            if (k >= hi) continue;
+            if (ix[j] >= b.shard_len) { oob = true; continue; }
+            atomicAdd(&hist[uint32_t(ix[j] >> b.tile_shift)], 1u);
+        }
     }
     if (oob) raise_err(b.err, LMR_ERRBIT_OOB);
     __syncthreads();
@@ -528,7 +539,7 @@ __device__ __forceinline__ T delta_finish(int op, T base, T prefix) {
 // records with LDS atomics, write it back. Kept free of the delta path's
 // register arrays so two 1024-thread blocks (2 x 64 KiB LDS) fit per CU.
 template <typename T, int OPT>
-__global__ __launch_bounds__(1024, 2) void k_tile_owner(TileArgs a) {
+__global__ __launch_bounds__(1024, 8) void k_tile_owner(TileArgs a) {
     using U = typename bits_of<T>::U;
     using W = typename word_of<T>::W;
     extern __shared__ __align__(16) uint8_t lds_raw[];

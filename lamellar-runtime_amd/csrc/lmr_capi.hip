@@ -50,11 +50,14 @@ struct CtxExtra {
     uint32_t* pack_counts = nullptr;
     uint32_t* pack_partials = nullptr;
     uint32_t* pack_total = nullptr;
+    uint64_t* red_part = nullptr;      // [kReduceBlocks]
+    uint8_t* red_has = nullptr;        // [kReduceBlocks]
 };
 
-// The small pack scratch lives right after the error word in one allocation.
+// The small pack / reduce scratch lives right after the error word in one allocation.
 size_t pack_scratch_bytes() {
-    return 256 + kPackScratchCounts * 4 + 256 + (kPackScratchCounts / kScanItems + 1) * 4 + 256;
+    return 256 + kPackScratchCounts * 4 + 256 + (kPackScratchCounts / kScanItems + 1) * 4 + 256 +
+           size_t(kReduceBlocks) * 9 + 512;
 }
 
 CtxExtra pack_scratch(lmr_ctx* c) {
@@ -65,6 +68,10 @@ CtxExtra pack_scratch(lmr_ctx* c) {
     x.pack_partials = reinterpret_cast<uint32_t*>(p);
     p += (((kPackScratchCounts / kScanItems + 1) * 4 + 255) & ~size_t(255));
     x.pack_total = reinterpret_cast<uint32_t*>(p);
+    p += 256;
+    x.red_part = reinterpret_cast<uint64_t*>(p);
+    p += size_t(kReduceBlocks) * 8;
+    x.red_has = p;
     return x;
 }
 
@@ -454,6 +461,16 @@ lmr_status_t lmr_pack_unordered(lmr_ctx_t* ctx, const lmr_layout_t* layout, cons
                                 uint64_t* d_dest_counts, uint64_t* d_dest_offsets, lmr_stream_t stream) {
     return pack_common(ctx, layout, d_gidx, n, d_vals, dtype, index_size, d_out_idx, d_out_vals, d_out_pos,
                        d_dest_counts, d_dest_offsets, false, stream);
+}
+
+// ---------------------------------------------------------------- reduce
+lmr_status_t lmr_reduce(lmr_ctx_t* ctx, uint32_t dtype, uint32_t op, const void* d_shard, uint64_t len,
+                        uint64_t* d_out, uint8_t* d_has, lmr_stream_t stream) {
+    if (!ctx || dtype >= LMR_NUM_DTYPES || op > LMR_REDUCE_MIN || !d_out || (len > 0 && !d_shard))
+        return LMR_E_INVALID;
+    CtxExtra x = pack_scratch(ctx);
+    return hip_status(launch_reduce(int(dtype), int(op), d_shard, len, d_out, d_has, x.red_part, x.red_has,
+                                    reinterpret_cast<hipStream_t>(stream)));
 }
 
 // ---------------------------------------------------------------- apply

@@ -165,6 +165,37 @@ __host__ __device__ __forceinline__ bool pe_and_offset_fast(const FastLayout& f,
     return true;
 }
 
+// Layout mode resolved once on the host so the per-record mapping is branch-free:
+// 0 = full Block array, 1 = full Cyclic array, 2 = anything else (sub-arrays).
+enum { LMR_MAP_BLOCK = 0, LMR_MAP_CYCLIC = 1, LMR_MAP_GENERIC = 2 };
+
+__host__ inline int layout_map_mode(const lmr_layout_t& L) {
+    if (L.sub) return LMR_MAP_GENERIC;
+    return L.distribution == LMR_DIST_BLOCK ? LMR_MAP_BLOCK : LMR_MAP_CYCLIC;
+}
+
+template <int MODE>
+__host__ __device__ __forceinline__ bool pe_and_offset_mode(const FastLayout& f, uint64_t index, uint64_t& pe,
+                                                            uint64_t& off) {
+    if constexpr (MODE == LMR_MAP_GENERIC) {
+        return pe_and_offset(f.L, index, pe, off);
+    } else {
+        if (!(f.L.size > index)) return false;
+        if constexpr (MODE == LMR_MAP_BLOCK) {
+            if (index < f.rem_index) {
+                fast_divmod(index, f.a, f.inv_a, pe, off);
+            } else {
+                uint64_t tp;
+                fast_divmod(index - f.rem_index, f.b, f.inv_b, tp, off);
+                pe = f.L.orig_remaining_elems + tp;
+            }
+        } else {
+            fast_divmod(index, f.L.num_pes, f.inv_np, off, pe);
+        }
+        return true;
+    }
+}
+
 // ---------------------------------------------------------------- errors
 __device__ __forceinline__ void raise_err(uint32_t* err, uint32_t bit) {
     if (err) __hip_atomic_fetch_or(err, bit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);

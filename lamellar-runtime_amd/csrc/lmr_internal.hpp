@@ -116,6 +116,9 @@ struct PackArgs {
 };
 hipError_t launch_pack(const PackArgs& a, uint32_t* counts, uint32_t* partials, uint32_t* total,
                        hipStream_t s);
+constexpr int kReduceBlocks = 1024;
+hipError_t launch_reduce(int dtype, int op, const void* x, uint64_t n, uint64_t* out, uint8_t* has,
+                         void* part, uint8_t* part_has, hipStream_t s);
 hipError_t launch_scatter_results(const uint8_t* in, const uint32_t* pos, uint64_t n,
                                   uint32_t elem_bytes, uint8_t* out, const uint8_t* ok_in,
                                   uint8_t* ok_out, Prof* prof, hipStream_t s);

@@ -8,11 +8,13 @@
 // input position j (the reference's res_buffs, used to put fetch results back
 // in input order, operations/handle.rs:315-317).
 //
-// The device version is a stable counting sort by PE: per-block PE counts ->
-// exclusive scan over (PE, block) -> scatter with wave-ballot ranks, so each
-// PE's buffer holds its records in input order — the concatenation, in order,
-// of the reference's per-PE op buffers. Output is structure-of-arrays
-// (indices, values, positions): coalesced for the apply kernels and for RCCL.
+// The device version is a counting sort by PE: per-block PE counts -> exclusive
+// scan over (PE, block) -> scatter. lmr_pack's scatter ranks with wave ballots
+// and is stable, so each PE's buffer holds its records in input order (the
+// concatenation, in order, of the reference's per-PE op buffers);
+// lmr_pack_unordered's stages rounds in LDS and writes long per-PE runs.
+// Output is structure-of-arrays (indices, values, positions): coalesced for the
+// apply kernels and for RCCL.
 #include "lmr_internal.hpp"
 #include "lmr_device.hpp"
 #include <stdlib.h>
@@ -61,6 +63,20 @@ __device__ __forceinline__ uint32_t wave_agg_rank(uint32_t* hist, uint32_t key, 
     return rank;
 }
 
+// count-only form: no rank, no return value needed from the LDS atomic
+__device__ __forceinline__ void wave_agg_count(uint32_t* hist, uint32_t key, bool active) {
+    const int lane = threadIdx.x & 63;
+    uint64_t todo = __ballot(active);
+    while (todo) {
+        const int leader = __ffsll((unsigned long long)todo) - 1;
+        const uint32_t x = __shfl(key, leader, 64);
+        const uint64_t m = __ballot(active && key == x);
+        if (lane == leader) atomicAdd(&hist[x], uint32_t(__popcll(m)));
+        todo &= ~m;
+    }
+}
+
+template <int MODE>
 __global__ __launch_bounds__(1024) void k_pack_count(PackK p) {
     extern __shared__ uint32_t cnt[];
     for (uint32_t i = threadIdx.x; i < p.npes; i += blockDim.x) cnt[i] = 0;
@@ -83,9 +99,9 @@ __global__ __launch_bounds__(1024) void k_pack_count(PackK p) {
             const uint64_t k = k0 + uint64_t(j) * 1024;
             uint64_t pe = 0, off;
             const bool in = k < hi;
-            const bool ok = in && pe_and_offset_fast(p.F, g[j], pe, off);
+            const bool ok = in && pe_and_offset_mode<MODE>(p.F, g[j], pe, off);
             oob |= in && !ok;
-            if (agg) (void)wave_agg_rank(cnt, uint32_t(pe), ok);
+            if (agg) wave_agg_count(cnt, uint32_t(pe), ok);
             else if (ok) atomicAdd(&cnt[uint32_t(pe)], 1u);
         }
     }
@@ -118,6 +134,7 @@ __device__ __forceinline__ void copy_val(uint8_t* dst, const uint8_t* src, uint3
 // order); inside a round, wave w holds records [64w, 64w+64). Rank of a record
 // = records of the same PE in earlier rounds (cursor) + in earlier waves of
 // this round (wave_base) + in earlier lanes of this wave (ballot popcount).
+template <int MODE>
 __global__ __launch_bounds__(1024) void k_pack_scatter(PackK p) {
     extern __shared__ uint32_t sm[];
     uint32_t* cursor = sm;                     // [npes]
@@ -132,7 +149,7 @@ __global__ __launch_bounds__(1024) void k_pack_scatter(PackK p) {
         __syncthreads();
         const uint64_t k = r0 + threadIdx.x;
         uint64_t pe = 0, off = 0;
-        bool valid = (k < hi) && pe_and_offset_fast(p.F, p.gidx[k], pe, off);
+        bool valid = (k < hi) && pe_and_offset_mode<MODE>(p.F, p.gidx[k], pe, off);
         const uint32_t mype = valid ? uint32_t(pe) : 0xFFFFFFFFu;
         // group lanes by PE (match-any by repeated ballot over distinct values)
         uint64_t remaining = __ballot(true);
@@ -195,8 +212,8 @@ __device__ __forceinline__ void stage_scan(const uint32_t* hist, uint32_t* base,
     }
 }
 
-template <int IW, int VB, int RPT>
-__global__ __launch_bounds__(1024) void k_pack_stage(PackK p) {
+template <int IW, int VB, int RPT, int MODE>
+__global__ __launch_bounds__(1024, 8) void k_pack_stage(PackK p) {
     using I = typename idx_t<IW>::I;
     using V = typename idx_t<VB>::I;
     constexpr uint32_t kRound = RPT * 1024;
@@ -231,7 +248,7 @@ __global__ __launch_bounds__(1024) void k_pack_stage(PackK p) {
 #pragma unroll
         for (int j = 0; j < RPT; j++) {
             uint64_t pe = 0, off = 0;
-            const bool ok = (r0 + uint64_t(j) * 1024 + threadIdx.x < hi) && pe_and_offset_fast(p.F, m_g[j], pe, off);
+            const bool ok = (r0 + uint64_t(j) * 1024 + threadIdx.x < hi) && pe_and_offset_mode<MODE>(p.F, m_g[j], pe, off);
             m_pe[j] = ok ? uint32_t(pe) : 0xFFFFFFFFu;
             m_off[j] = off;
             if (agg) m_rank[j] = wave_agg_rank(hist, uint32_t(pe), ok);
@@ -309,8 +326,18 @@ hipError_t launch_pack(const PackArgs& a, uint32_t* counts, uint32_t* partials, 
     p.G = uint32_t(G); p.npes = npes; p.counts = counts;
     p.out_idx = a.out_idx; p.out_vals = a.out_vals; p.out_pos = a.out_pos; p.err = a.err;
     ProfScope ps(a.prof, LMR_STAGE_PACK, s);
+    const int mode = layout_map_mode(a.layout);
+    auto by_mode = [&](auto f) {
+        using std::integral_constant;
+        if (mode == LMR_MAP_BLOCK) f(integral_constant<int, LMR_MAP_BLOCK>{});
+        else if (mode == LMR_MAP_CYCLIC) f(integral_constant<int, LMR_MAP_CYCLIC>{});
+        else f(integral_constant<int, LMR_MAP_GENERIC>{});
+    };
     if (a.n > 0) {
-        hipLaunchKernelGGL(k_pack_count, dim3(unsigned(G)), dim3(1024), size_t(npes) * 4, s, p);
+        by_mode([&](auto m) {
+            hipLaunchKernelGGL((k_pack_count<decltype(m)::value>), dim3(unsigned(G)), dim3(1024), size_t(npes) * 4,
+                               s, p);
+        });
     } else {
         hipError_t e0 = hipMemsetAsync(counts, 0, size_t(npes) * G * 4, s);
         if (e0 != hipSuccess) return e0;
@@ -321,11 +348,16 @@ hipError_t launch_pack(const PackArgs& a, uint32_t* counts, uint32_t* partials, 
         if (!a.stable && npes <= kStageMaxPes) {
             const int vbk = a.vals ? int(a.val_bytes) : 1;
             dispatch_pack_stage(int(a.index_size), vbk, [&](auto iw, auto vb) {
-                hipLaunchKernelGGL((k_pack_stage<decltype(iw)::value, decltype(vb)::value, 4>), dim3(unsigned(G)),
-                                   dim3(1024), 0, s, p);
+                by_mode([&](auto m) {
+                    hipLaunchKernelGGL((k_pack_stage<decltype(iw)::value, decltype(vb)::value, 4, decltype(m)::value>),
+                                       dim3(unsigned(G)), dim3(1024), 0, s, p);
+                });
             });
         } else {
-            hipLaunchKernelGGL(k_pack_scatter, dim3(unsigned(G)), dim3(1024), size_t(npes) * 17 * 4, s, p);
+            by_mode([&](auto m) {
+                hipLaunchKernelGGL((k_pack_scatter<decltype(m)::value>), dim3(unsigned(G)), dim3(1024),
+                                   size_t(npes) * 17 * 4, s, p);
+            });
         }
     }
     hipLaunchKernelGGL(k_dest_offsets, dim3((npes + 1 + 255) / 256), dim3(256),

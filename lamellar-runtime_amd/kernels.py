@@ -176,6 +176,16 @@ class DeviceKernels:
         check(st, "lmr_pack" if stable else "lmr_pack_unordered")
         return out_idx, out_vals, out_pos, counts
 
+    def reduce(self, data, n, dt, op):
+        """lmr_reduce over n elements -> (has, value bits) (one 9-byte readback)."""
+        out = self.empty(2, torch.int64)
+        has = out[1:].view(torch.uint8)[:1]
+        st = self.lib.lmr_reduce(self.ctx, int(dt.code), int(op), _p(data), int(n), _p(out), _p(has),
+                                 self.stream())
+        check(st, "lmr_reduce")
+        h = out.cpu()
+        return bool(h[1].item() & 0xFF), int(h[0].item()) & 0xFFFFFFFFFFFFFFFF
+
     def scatter_results(self, res_in, pos, n, eb, res_out, ok_in=None, ok_out=None):
         st = self.lib.lmr_scatter_results(_p(res_in), _p(pos), int(n), int(eb), _p(res_out),
                                           _p(ok_in), _p(ok_out), self.stream())

@@ -113,6 +113,24 @@ class CpuTestKernels:
         idx = torch.from_numpy(np.full(n, index, dtype=np.uint64).view(np.uint8))
         self.apply_soa(shard, shard_len, kind, dt, op, idx, 8, vals, 0, n, results, ok, cmp_bits, eps_bits)
 
+    def reduce(self, data, n, dt, op):
+        a = data.numpy().view(dt.np)[:n]
+        if n == 0:
+            return False, 0
+        with np.errstate(over="ignore"):
+            acc = a[0]
+            for x in a[1:]:
+                if op == 0:
+                    acc = (np.array([acc]) + np.array([x]))[0]
+                elif op == 1:
+                    acc = (np.array([acc]) * np.array([x]))[0]
+                elif op == 2:
+                    acc = acc if acc > x else x
+                else:
+                    acc = acc if acc < x else x
+        u = {1: np.uint8, 2: np.uint16, 4: np.uint32, 8: np.uint64}[dt.bytes]
+        return True, int(np.array([acc], dtype=dt.np).view(u)[0])
+
     def scatter_results(self, res_in, pos, n, eb, res_out, ok_in=None, ok_out=None):
         u = {1: np.uint8, 2: np.uint16, 4: np.uint32, 8: np.uint64}[eb]
         p = pos.numpy().view(np.int32)[:n]
@@ -144,6 +162,8 @@ def _worker(rank, ws, port, outdir, dist_kind, chunk=None, ragged=False):
     arr.batch_add(gi, gv).block()
     world.barrier()
     res["after_add"] = arr.to_numpy()
+    res["red"] = np.array([arr.sum().block(), arr.max().block(), arr.min().block(), arr.prod().block()],
+                          dtype=np.uint64)
     # SVMI fetch_add (single value) -> olds come back in input order
     fi = rng.permutation(n_len)[:500].astype(np.uint64)
     olds = arr.batch_fetch_add(fi, 7).block()
@@ -196,6 +216,12 @@ def test_two_pe_exchange_gloo(orc, dist_kind, chunk, ragged):
     exp = a.to_numpy()
     for r in range(ws):
         assert np.array_equal(pe[r]["after_add"], exp)
+    with np.errstate(over="ignore"):
+        prod = np.uint64(1)
+        for x in exp:
+            prod = prod * x
+    for r in range(ws):     # wrapping sum / product, max, min of the whole array on every PE
+        assert list(pe[r]["red"]) == [exp.sum(dtype=np.uint64), exp.max(), exp.min(), prod]
     # fetch_add of 7: final = exp + 7 * (#PEs that touched the index); olds linearizable
     cnt = np.zeros(1003, np.uint64)
     for r in range(ws):
