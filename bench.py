@@ -394,9 +394,51 @@ def e2e(lam, team, W, args):
         olds_h.copy_(h._res.vals, non_blocking=True)
     torch.cuda.synchronize(dev)
     t2 = time.perf_counter()
-    return {"batch_add_ops_per_s": W.npes * W.n * args.steps / (t1 - t0),
-            "batch_fetch_add_ops_per_s": W.npes * W.n * args.steps / (t2 - t1),
-            "note": "pinned host idx+vals -> H2D -> device op (-> D2H olds for fetch_add), u64"}
+    out = {"batch_add_ops_per_s": W.npes * W.n * args.steps / (t1 - t0),
+           "batch_fetch_add_ops_per_s": W.npes * W.n * args.steps / (t2 - t1),
+           "note": "pinned host idx+vals -> H2D -> device op (-> D2H olds for fetch_add), u64"}
+    if W.npes == 1:
+        out["wire"] = e2e_wire(lam, team, W, args)
+    return out
+
+
+def e2e_wire(lam, team, W, args):
+    """The reference's own op-buffer bytes in host memory: IdxVal<u32,u64> records
+    (16 B, repr(C)), applied by lmr_apply_mvmi_host (pieces uploaded / applied /
+    results downloaded on three streams); fetch_add olds land in a registered
+    host array. At one PE a global index is the local offset."""
+    from lamellar_runtime_amd import _capi
+    from lamellar_runtime_amd.types import ArrayOpCmd
+    k = team.kernels
+    dt = lam.dtype_of("u64")
+    iw = 4
+    rb, vo = _capi.lib().lmr_record_bytes(iw, dt.code), _capi.lib().lmr_record_val_offset(iw, dt.code)
+    assert (rb, vo) == (16, 8)
+    rec = np.zeros(W.n, dtype=[("i", "<u4"), ("pad", "<u4"), ("v", "<u8")])
+    rec["i"] = W.idx.cpu().numpy().astype(np.uint32)
+    rec["v"] = W.vals.cpu().numpy().view(np.uint64)
+    buf = rec.view(np.uint8).reshape(-1)
+    olds = np.empty(W.n, dtype=np.uint64)
+    k.host_register(buf)
+    k.host_register(olds)
+    try:
+        shard, slen = W.arr.local_shard(), W.arr.num_elems_local()
+        kind = int(W.arr.kind)
+        k.apply_mvmi_host(shard, slen, kind, dt, int(ArrayOpCmd.Add), buf, iw)      # warm
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            k.apply_mvmi_host(shard, slen, kind, dt, int(ArrayOpCmd.Add), buf, iw)
+        t1 = time.perf_counter()
+        for _ in range(args.steps):
+            k.apply_mvmi_host(shard, slen, kind, dt, int(ArrayOpCmd.FetchAdd), buf, iw, olds)
+        t2 = time.perf_counter()
+    finally:
+        k.host_unregister(buf)
+        k.host_unregister(olds)
+    return {"batch_add_ops_per_s": W.n * args.steps / (t1 - t0),
+            "batch_fetch_add_ops_per_s": W.n * args.steps / (t2 - t1),
+            "h2d_GBps": W.n * rb * args.steps / (t1 - t0) / 1e9,
+            "note": "host IdxVal<u32,u64> op buffer (registered) -> lmr_apply_mvmi_host; olds -> host"}
 
 
 if __name__ == "__main__":

@@ -75,6 +75,10 @@ SIGNATURES = {
     "lmr_op_supported": (c_int, [c_uint32, c_uint32, c_uint32]),
     "lmr_pack": (c_int, [c_void_p, POINTER(lmr_layout_t), c_void_p, c_uint64, c_void_p, c_uint32,
                          c_uint32, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
+    "lmr_host_register": (c_int, [c_void_p, c_uint64]),
+    "lmr_host_unregister": (c_int, [c_void_p]),
+    "lmr_apply_mvmi_host": (c_int, [c_void_p, POINTER(lmr_apply_desc_t), c_void_p, c_uint64, c_uint32,
+                                    c_void_p, c_void_p, c_void_p]),
     "lmr_reduce": (c_int, [c_void_p, c_uint32, c_uint32, c_void_p, c_uint64, c_void_p, c_void_p, c_void_p]),
     "lmr_pack_unordered": (c_int, [c_void_p, POINTER(lmr_layout_t), c_void_p, c_uint64, c_void_p, c_uint32,
                                    c_uint32, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),

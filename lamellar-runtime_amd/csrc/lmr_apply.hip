@@ -342,9 +342,9 @@ __global__ __launch_bounds__(1024) void k_coarse_scatter(PartArgs p) {
     }
 }
 
-// Persistent over (coarse bucket c, producer block g) segments: block b takes
-// segments b, b + gridDim.x, ...; the first round of the next segment is
-// prefetched while the current segment's last round is written out.
+// Persistent over (coarse bucket c, producer block g) segments, a contiguous
+// record-balanced range of them per block; the first round of the next segment
+// is prefetched while the current segment's last round is written out.
 template <int VB, int RPT>
 __global__ __launch_bounds__(1024) void k_fine_scatter(PartArgs p) {
     using V = typename idx_t<VB>::I;
@@ -366,16 +366,31 @@ __global__ __launch_bounds__(1024) void k_fine_scatter(PartArgs p) {
             m_val[j] = (in && p.tmp_val) ? reinterpret_cast<const V*>(p.tmp_val)[k] : V(0);
         }
     };
-    uint32_t cg = blockIdx.x;
-    if (cg < nseg) load_round(p.coarse_off[cg], p.coarse_off[cg + 1]);
-    for (; cg < nseg; cg += gridDim.x) {
+    // Block b owns the segments whose records start in [total*b/B, total*(b+1)/B)
+    // (coarse_off is monotone in cg = c*G + g): a contiguous run of producers
+    // g of one bucket, so each tile's output run keeps growing from one CU (one
+    // XCD's L2 merges its partial lines) and work is balanced by records.
+    const uint64_t total_recs = p.coarse_off[nseg];
+    auto seg_lower_bound = [&](uint64_t target) {
+        uint32_t lo_s = 0, hi_s = nseg;
+        while (lo_s < hi_s) {
+            const uint32_t mid = (lo_s + hi_s) >> 1;
+            if (uint64_t(p.coarse_off[mid]) < target) lo_s = mid + 1; else hi_s = mid;
+        }
+        return lo_s;
+    };
+    const uint32_t cg_begin = seg_lower_bound(total_recs * blockIdx.x / gridDim.x);
+    const uint32_t cg_end = (blockIdx.x + 1 == gridDim.x) ? nseg
+                                                          : seg_lower_bound(total_recs * (blockIdx.x + 1) / gridDim.x);
+    uint32_t cg = cg_begin;
+    if (cg < cg_end) load_round(p.coarse_off[cg], p.coarse_off[cg + 1]);
+    for (; cg < cg_end; cg++) {
         const uint32_t c = cg / p.G, g = cg % p.G;
         const uint32_t t0 = c * kFine;
         const uint32_t nf = min(uint32_t(kFine), p.num_tiles - t0);
         const uint32_t lo = p.coarse_off[cg], hi = p.coarse_off[cg + 1];
         if (lo == hi) {   // empty segment: its (all-invalid) prefetch is replaced by the next one's
-            if (cg + gridDim.x < nseg)
-                load_round(p.coarse_off[cg + gridDim.x], p.coarse_off[cg + gridDim.x + 1]);
+            if (cg + 1 < cg_end) load_round(p.coarse_off[cg + 1], p.coarse_off[cg + 2]);
             continue;
         }
         for (uint32_t f = threadIdx.x; f < nf; f += blockDim.x)
@@ -405,9 +420,8 @@ __global__ __launch_bounds__(1024) void k_fine_scatter(PartArgs p) {
             }
             if (r0 + kRound < hi) {
                 load_round(r0 + kRound, hi);
-            } else if (cg + gridDim.x < nseg) {
-                const uint32_t nx = cg + gridDim.x;
-                load_round(p.coarse_off[nx], p.coarse_off[nx + 1]);
+            } else if (cg + 1 < cg_end) {
+                load_round(p.coarse_off[cg + 1], p.coarse_off[cg + 2]);
             }
             __syncthreads();
             const uint32_t total = tot;

@@ -231,6 +231,7 @@ lmr_status_t lmr_ctx_create(int device, lmr_ctx_t** out) {
 lmr_status_t lmr_ctx_destroy(lmr_ctx_t* ctx) {
     if (!ctx) return LMR_E_INVALID;
     (void)hipSetDevice(ctx->device);
+    host_stage_free(ctx->host);
     if (ctx->ws) (void)hipFree(ctx->ws);
     if (ctx->d_err) (void)hipFree(ctx->d_err);
     if (ctx->prof) {

@@ -1,0 +1,155 @@
+// lmr_host.hip — host-buffer ingestion of op buffers.
+//
+// In the reference the packed IdxVal<I,T> records of an op AM live in host
+// memory: the shmem lamellae heap or a socket buffer
+// (src/lamellae/shmem/shmem_comm.rs:302-352; the AM body deserialised in
+// src/active_messaging/registered_active_message.rs:260-304, 443-497) and the
+// fetch results go back as a host Vec<T>. lmr_apply_mvmi_host takes those host
+// bytes as they are and pipelines them through the device:
+//
+//   h2d stream : copy piece i into slot i%2            (waits until slot's apply i-2 is done)
+//   stream     : apply piece i (lmr_apply_mvmi)        (waits for copy i, and for slot's results D2H i-2)
+//   d2h stream : copy piece i's results / Ok flags out (waits for apply i)
+//
+// so piece i+1's upload and piece i-1's result download overlap piece i's
+// apply; PCIe (full duplex) is the bound. Registering the host buffer
+// (lmr_host_register = hipHostRegister of the lamellae heap) lets the DMA
+// engines read it in place, without a bounce through pageable staging.
+#include "lmr_internal.hpp"
+#include "../../include/lamellar_gpu_ops.h"
+#include <stdlib.h>
+
+namespace lmr {
+
+struct HostStage {
+    hipStream_t h2d = nullptr, d2h = nullptr;
+    uint8_t* d_rec[2] = {nullptr, nullptr};
+    uint8_t* d_res[2] = {nullptr, nullptr};
+    uint8_t* d_ok[2] = {nullptr, nullptr};
+    hipEvent_t copied[2] = {}, applied[2] = {}, drained[2] = {};
+    uint64_t piece_recs = 0;
+    uint64_t rec_bytes_cap = 0;   // bytes per record slot capacity (largest record size supported: 16)
+};
+
+void host_stage_free(HostStage* h) {
+    if (!h) return;
+    if (h->h2d) (void)hipStreamSynchronize(h->h2d);
+    if (h->d2h) (void)hipStreamSynchronize(h->d2h);
+    for (int b = 0; b < 2; b++) {
+        if (h->d_rec[b]) (void)hipFree(h->d_rec[b]);
+        if (h->d_res[b]) (void)hipFree(h->d_res[b]);
+        if (h->d_ok[b]) (void)hipFree(h->d_ok[b]);
+        if (h->copied[b]) (void)hipEventDestroy(h->copied[b]);
+        if (h->applied[b]) (void)hipEventDestroy(h->applied[b]);
+        if (h->drained[b]) (void)hipEventDestroy(h->drained[b]);
+    }
+    if (h->h2d) (void)hipStreamDestroy(h->h2d);
+    if (h->d2h) (void)hipStreamDestroy(h->d2h);
+    delete h;
+}
+
+static uint64_t host_piece_records() {
+    const char* v = getenv("LMR_HOST_PIECE_RECORDS");
+    uint64_t x = (v && *v) ? strtoull(v, nullptr, 10) : (uint64_t(1) << 22);
+    if (x < 1024) x = 1024;
+    if (x > (uint64_t(1) << 26)) x = uint64_t(1) << 26;
+    return x;
+}
+
+static hipError_t host_stage_get(lmr_ctx* ctx, HostStage** out) {
+    if (ctx->host) { *out = ctx->host; return hipSuccess; }
+    HostStage* h = new HostStage();
+    h->piece_recs = host_piece_records();
+    h->rec_bytes_cap = 16;
+    hipError_t e = hipStreamCreateWithFlags(&h->h2d, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&h->d2h, hipStreamNonBlocking);
+    for (int b = 0; b < 2 && e == hipSuccess; b++) {
+        e = hipMalloc(&h->d_rec[b], h->piece_recs * h->rec_bytes_cap);
+        if (e == hipSuccess) e = hipMalloc(&h->d_res[b], h->piece_recs * 8);
+        if (e == hipSuccess) e = hipMalloc(&h->d_ok[b], h->piece_recs);
+        if (e == hipSuccess) e = hipEventCreateWithFlags(&h->copied[b], hipEventDisableTiming);
+        if (e == hipSuccess) e = hipEventCreateWithFlags(&h->applied[b], hipEventDisableTiming);
+        if (e == hipSuccess) e = hipEventCreateWithFlags(&h->drained[b], hipEventDisableTiming);
+    }
+    if (e != hipSuccess) { host_stage_free(h); return e; }
+    ctx->host = h;
+    *out = h;
+    return hipSuccess;
+}
+
+}  // namespace lmr
+
+using namespace lmr;
+
+extern "C" {
+
+lmr_status_t lmr_host_register(void* ptr, uint64_t bytes) {
+    if (!ptr || bytes == 0) return LMR_E_INVALID;
+    return hipHostRegister(ptr, bytes, hipHostRegisterDefault) == hipSuccess ? LMR_OK : LMR_E_HIP;
+}
+
+lmr_status_t lmr_host_unregister(void* ptr) {
+    if (!ptr) return LMR_E_INVALID;
+    return hipHostUnregister(ptr) == hipSuccess ? LMR_OK : LMR_E_HIP;
+}
+
+lmr_status_t lmr_apply_mvmi_host(lmr_ctx_t* ctx, const lmr_apply_desc_t* desc, const void* h_idx_vals,
+                                 uint64_t nbytes, uint32_t index_size, void* h_results, uint8_t* h_ok,
+                                 lmr_stream_t stream) {
+    if (!ctx || !desc) return LMR_E_INVALID;
+    if (index_size != 1 && index_size != 2 && index_size != 4 && index_size != 8) return LMR_E_INVALID;
+    if (desc->dtype >= LMR_NUM_DTYPES) return LMR_E_INVALID;
+    const uint32_t rb = lmr_record_bytes(index_size, desc->dtype);
+    const uint32_t eb = rb ? uint32_t(dtype_bytes(int(desc->dtype))) : 0;
+    if (rb == 0 || rb > 16) return LMR_E_INVALID;
+    const uint64_t n = nbytes / rb;
+    if (n == 0) return LMR_OK;
+    if (!h_idx_vals) return LMR_E_INVALID;
+    (void)hipSetDevice(ctx->device);
+    HostStage* h = nullptr;
+    if (host_stage_get(ctx, &h) != hipSuccess) return LMR_E_HIP;
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    const uint64_t P = h->piece_recs;
+    if (desc->strategy != LMR_STRATEGY_DIRECT && P >= 65536 && ctx->rec_cap < P) {
+        (void)hipDeviceSynchronize();
+        lmr_status_t st = lmr_ctx_reserve(ctx, P);
+        if (st != LMR_OK) return st;
+    }
+    const uint32_t ret = lmr_op_ret_kind(desc->op);
+    const bool want_res = h_results && ret != LMR_RET_NONE;
+    const bool want_ok = h_ok && ret == LMR_RET_RESULT;
+    const uint8_t* src = reinterpret_cast<const uint8_t*>(h_idx_vals);
+    uint64_t i = 0;
+    for (uint64_t r0 = 0; r0 < n; r0 += P, i++) {
+        const int b = int(i & 1);
+        const uint64_t m = (n - r0 < P) ? n - r0 : P;
+        // upload: the slot's previous apply must have consumed its records
+        if (hipStreamWaitEvent(h->h2d, h->applied[b], 0) != hipSuccess) return LMR_E_HIP;
+        if (hipMemcpyAsync(h->d_rec[b], src + r0 * rb, m * rb, hipMemcpyHostToDevice, h->h2d) != hipSuccess)
+            return LMR_E_HIP;
+        if (hipEventRecord(h->copied[b], h->h2d) != hipSuccess) return LMR_E_HIP;
+        // apply on the caller's stream (after the upload and the slot's previous download)
+        if (hipStreamWaitEvent(s, h->copied[b], 0) != hipSuccess) return LMR_E_HIP;
+        if (hipStreamWaitEvent(s, h->drained[b], 0) != hipSuccess) return LMR_E_HIP;
+        lmr_status_t st = lmr_apply_mvmi(ctx, desc, h->d_rec[b], m * rb, index_size,
+                                         want_res ? h->d_res[b] : nullptr, want_ok ? h->d_ok[b] : nullptr, stream);
+        if (st != LMR_OK) return st;
+        if (hipEventRecord(h->applied[b], s) != hipSuccess) return LMR_E_HIP;
+        // download of the returned values
+        if (want_res || want_ok) {
+            if (hipStreamWaitEvent(h->d2h, h->applied[b], 0) != hipSuccess) return LMR_E_HIP;
+            if (want_res && hipMemcpyAsync(reinterpret_cast<uint8_t*>(h_results) + r0 * eb, h->d_res[b], m * eb,
+                                           hipMemcpyDeviceToHost, h->d2h) != hipSuccess)
+                return LMR_E_HIP;
+            if (want_ok && hipMemcpyAsync(h_ok + r0, h->d_ok[b], m, hipMemcpyDeviceToHost, h->d2h) != hipSuccess)
+                return LMR_E_HIP;
+            if (hipEventRecord(h->drained[b], h->d2h) != hipSuccess) return LMR_E_HIP;
+        }
+    }
+    // completion on the caller's stream covers the downloads too
+    for (int b = 0; b < 2; b++)
+        if (hipStreamWaitEvent(s, h->drained[b], 0) != hipSuccess) return LMR_E_HIP;
+    return LMR_OK;
+}
+
+}  // extern "C"

@@ -8,6 +8,8 @@
 
 namespace lmr { struct Prof; }
 
+namespace lmr { struct HostStage; void host_stage_free(HostStage* h); }
+
 struct lmr_ctx {
     int device = 0;
     uint32_t* d_err = nullptr;     // device error word (LMR_ERRBIT_*)
@@ -17,6 +19,7 @@ struct lmr_ctx {
     uint64_t rec_cap = 0;          // records one tiled piece may hold
     int num_cus = 256;
     lmr::Prof* prof = nullptr;     // stage timing (lmr_ctx_profile), null when off
+    lmr::HostStage* host = nullptr;  // host-buffer ingestion staging (lmr_apply_mvmi_host), lazily made
 };
 
 namespace lmr {

@@ -213,7 +213,7 @@ __device__ __forceinline__ void stage_scan(const uint32_t* hist, uint32_t* base,
 }
 
 template <int IW, int VB, int RPT, int MODE>
-__global__ __launch_bounds__(1024, 8) void k_pack_stage(PackK p) {
+__global__ __launch_bounds__(1024, (IW == 8 && VB == 8) ? 4 : 8) void k_pack_stage(PackK p) {
     using I = typename idx_t<IW>::I;
     using V = typename idx_t<VB>::I;
     constexpr uint32_t kRound = RPT * 1024;

@@ -145,6 +145,25 @@ class DeviceKernels:
                                      _p(results), _p(ok), self.stream())
         check(st, "lmr_apply_mvmi")
 
+    def apply_mvmi_host(self, shard, shard_len, kind, dt, op, h_records, iw, h_results=None, h_ok=None,
+                        cmp_bits=0, eps_bits=0):
+        """Apply a host-resident op buffer (numpy uint8 IdxVal<I,T> bytes); fetch results / Ok
+        flags land in the host numpy arrays h_results / h_ok (lmr_apply_mvmi_host). Synchronous:
+        returns when the host results are valid."""
+        d = self._desc(shard, shard_len, kind, dt, op, cmp_bits, eps_bits)
+        st = self.lib.lmr_apply_mvmi_host(self.ctx, byref(d), h_records.ctypes.data, int(h_records.nbytes),
+                                          int(iw), None if h_results is None else h_results.ctypes.data,
+                                          None if h_ok is None else h_ok.ctypes.data, self.stream())
+        check(st, "lmr_apply_mvmi_host")
+        torch.cuda.current_stream(self.device).synchronize()
+
+    def host_register(self, arr):
+        """Page-lock a host numpy buffer for DMA (lmr_host_register)."""
+        check(self.lib.lmr_host_register(arr.ctypes.data, int(arr.nbytes)), "lmr_host_register")
+
+    def host_unregister(self, arr):
+        check(self.lib.lmr_host_unregister(arr.ctypes.data), "lmr_host_unregister")
+
     def apply_svmi(self, shard, shard_len, kind, dt, op, scalar_bits, indices, n, iw,
                    results=None, ok=None, cmp_bits=0, eps_bits=0):
         self._maybe_reserve(n)
