@@ -235,6 +235,12 @@ struct PartArgs {
     uint16_t* bin_lidx;
     uint8_t* bin_val;
     uint32_t* rpos;               // [total] temp position -> binned position; null: no results
+    // round-major partition (k_coarse_rm / k_fine_rm)
+    uint32_t* counts;             // [num_tiles][G] per-block tile counts (written by k_coarse_rm)
+    uint16_t* rhist;              // [n/kRmRound rows][C] per-round bucket counts
+    uint16_t* rbase;              // [rows][C] per-round bucket offsets inside the round region
+    uint32_t R;                   // rounds per full block (chunk / kRmRound)
+    uint32_t* err;
 };
 
 // coarse_off[c][g] = start of block g's coarse-c records in the temp buffer
@@ -339,6 +345,232 @@ __global__ __launch_bounds__(1024) void k_coarse_scatter(PartArgs p) {
         }
         __syncthreads();
         for (uint32_t c = threadIdx.x; c < C; c += blockDim.x) cursor[c] += hist[c];
+    }
+}
+
+// ---- round-major two-level partition (no count pass) -------------------------
+// k_coarse_rm: block g reads its chunk (a multiple of kRmRound records) in rounds;
+// each round is counting-sorted by coarse bucket in LDS and written as ONE
+// contiguous bucket-sorted region at the round's own input position (fully
+// coalesced stores, no global offsets needed), with the round's bucket counts /
+// offsets (u16) beside it. The per-(tile, block) counts the fine pass needs are
+// built on the way in LDS (packed u16 pairs, flushed every 15 rounds so they
+// never overflow): the separate count pass over the input is gone.
+// k_fine_rm: segment (c, g) = bucket c's piece of every round of block g; a
+// piece table (prefix of piece lengths) maps the segment's flat record index to
+// its temp slot, and the tile sort / output is that of k_fine_scatter.
+constexpr uint32_t kRmRound = 4096;
+constexpr uint32_t kRmMaxRounds = 128;     // piece tables are scanned by one wave (<= 128 entries)
+constexpr int kRmFlush = 15;               // rounds between u16 tile-counter flushes (15 * 4096 < 65536)
+
+template <int IW, int VB>
+__global__ __launch_bounds__(1024, 8) void k_coarse_rm(PartArgs p) {
+    using V = typename idx_t<VB>::I;
+    constexpr int RPT = kRmRound / 1024;
+    extern __shared__ uint32_t th[];                         // packed u16 tile counters
+    __shared__ uint32_t hist[kMaxCoarse], base[kMaxCoarse], tot;
+    __shared__ uint32_t s_idx[kRmRound];
+    __shared__ V s_val[kRmRound];
+    const uint32_t g = blockIdx.x, C = p.C;
+    const int cshift = p.tile_shift + kFineShift;
+    const uint32_t nw = (p.num_tiles + 1) >> 1;
+    for (uint32_t i = threadIdx.x; i < nw; i += blockDim.x) th[i] = 0;
+    const uint64_t lo = uint64_t(g) * p.chunk;
+    const uint64_t hi = min(lo + p.chunk, p.n);
+    uint64_t m_raw[RPT];
+    V m_val[RPT];
+    auto load_round = [&](uint64_t r0) {
+#pragma unroll
+        for (int j = 0; j < RPT; j++) {
+            const uint64_t k = r0 + uint64_t(j) * 1024 + threadIdx.x;
+            const bool in = k < hi;
+            m_raw[j] = in ? load_idx<IW>(p.idx, p.idx_stride, k) : ~uint64_t(0);
+            m_val[j] = (in && p.val) ? *reinterpret_cast<const V*>(p.val + k * p.val_stride) : V(0);
+        }
+    };
+    bool flushed = false;
+    auto flush = [&]() {
+        for (uint32_t i = threadIdx.x; i < nw; i += blockDim.x) {
+            const uint32_t x = th[i];
+            th[i] = 0;
+            const uint32_t t0 = 2 * i;
+            uint32_t* c0 = p.counts + uint64_t(t0) * p.G + g;
+            *c0 = (flushed ? *c0 : 0u) + (x & 0xFFFFu);
+            if (t0 + 1 < p.num_tiles) {
+                uint32_t* c1 = p.counts + uint64_t(t0 + 1) * p.G + g;
+                *c1 = (flushed ? *c1 : 0u) + (x >> 16);
+            }
+        }
+        flushed = true;
+    };
+    load_round(lo);
+    bool oob = false;
+    uint32_t r = 0;
+    for (uint64_t r0 = lo; r0 < hi; r0 += kRmRound, r++) {
+        for (uint32_t c = threadIdx.x; c < C; c += blockDim.x) hist[c] = 0;
+        __syncthreads();
+        uint32_t m_rank[RPT], m_c[RPT];
+        bool m_ok[RPT];
+#pragma unroll
+        for (int j = 0; j < RPT; j++) {
+            const bool in = r0 + uint64_t(j) * 1024 + threadIdx.x < hi;
+            m_ok[j] = m_raw[j] < p.shard_len;
+            oob |= in && !m_ok[j];
+            m_c[j] = uint32_t(m_raw[j] >> cshift);
+            if (m_ok[j]) {
+                m_rank[j] = atomicAdd(&hist[m_c[j]], 1u);
+                const uint32_t t = uint32_t(m_raw[j] >> p.tile_shift);
+                atomicAdd(&th[t >> 1], 1u << ((t & 1u) * 16));
+            }
+        }
+        __syncthreads();
+        small_excl_scan(hist, base, C, &tot);
+        __syncthreads();
+#pragma unroll
+        for (int j = 0; j < RPT; j++) {
+            const uint64_t k = r0 + uint64_t(j) * 1024 + threadIdx.x;
+            if (!m_ok[j]) {
+                if (p.qpos && k < hi) p.qpos[k] = 0xFFFFFFFFu;
+                continue;
+            }
+            const uint32_t q = base[m_c[j]] + m_rank[j];
+            s_idx[q] = uint32_t(m_raw[j]);
+            s_val[q] = m_val[j];
+            if (p.qpos) p.qpos[k] = uint32_t(r0) + q;               // coalesced in k
+        }
+        if (r0 + kRmRound < hi) load_round(r0 + kRmRound);        // prefetch the next round
+        const uint64_t row = (r0 / kRmRound) * C;
+        for (uint32_t c = threadIdx.x; c < C; c += blockDim.x) {
+            p.rhist[row + c] = uint16_t(hist[c]);
+            p.rbase[row + c] = uint16_t(base[c]);
+        }
+        __syncthreads();
+        const uint32_t total = tot;
+        for (uint32_t q = threadIdx.x; q < total; q += blockDim.x) {
+            p.tmp_idx[r0 + q] = s_idx[q];
+            if (p.val) reinterpret_cast<V*>(p.tmp_val)[r0 + q] = s_val[q];
+        }
+        if ((r % kRmFlush) == kRmFlush - 1 || r0 + kRmRound >= hi) flush();
+        __syncthreads();
+    }
+    if (oob) raise_err(p.err, LMR_ERRBIT_OOB);
+}
+
+// segment sizes in (c, g) order: seg[c*G + g] = sum over block g's rounds of rhist[.][c]
+__global__ void k_rm_seg_sizes(PartArgs p, uint32_t* seg) {
+    const uint64_t i = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+    const uint64_t cg = uint64_t(p.C) * p.G;
+    if (i < cg) {
+        const uint32_t c = uint32_t(i / p.G), g = uint32_t(i % p.G);
+        const uint64_t lo = uint64_t(g) * p.chunk, hi = min(lo + p.chunk, p.n);
+        const uint32_t nr = uint32_t((hi - lo + kRmRound - 1) / kRmRound);
+        const uint64_t row0 = lo / kRmRound;
+        uint32_t s = 0;
+        for (uint32_t r = 0; r < nr; r++) s += p.rhist[(row0 + r) * p.C + c];
+        seg[i] = s;
+    } else if (i == cg) {
+        seg[i] = 0;
+    }
+}
+
+template <int VB>
+__global__ __launch_bounds__(1024, 8) void k_fine_rm(PartArgs p) {
+    using V = typename idx_t<VB>::I;
+    constexpr int RPT = 4;
+    constexpr uint32_t kRound = RPT * 1024;
+    __shared__ uint32_t hist[kFine], base[kFine], cursor[kFine], tot;
+    __shared__ uint32_t pp[kRmMaxRounds + 1], pstart[kRmMaxRounds], plen[kRmMaxRounds], ptot;
+    __shared__ uint16_t s_l[kRound];
+    __shared__ V s_val[kRound];
+    __shared__ uint8_t s_f[kRound];
+    const uint32_t nseg = p.C * p.G;
+    const uint32_t lmask = (1u << p.tile_shift) - 1u;
+    const uint64_t total_recs = p.coarse_off[nseg];
+    auto seg_lower_bound = [&](uint64_t target) {
+        uint32_t a = 0, b = nseg;
+        while (a < b) {
+            const uint32_t mid = (a + b) >> 1;
+            if (uint64_t(p.coarse_off[mid]) < target) a = mid + 1; else b = mid;
+        }
+        return a;
+    };
+    const uint32_t cg_begin = seg_lower_bound(total_recs * blockIdx.x / gridDim.x);
+    const uint32_t cg_end = (blockIdx.x + 1 == gridDim.x) ? nseg
+                                                          : seg_lower_bound(total_recs * (blockIdx.x + 1) / gridDim.x);
+    for (uint32_t cg = cg_begin; cg < cg_end; cg++) {
+        const uint32_t seg_len = p.coarse_off[cg + 1] - p.coarse_off[cg];
+        if (seg_len == 0) continue;
+        const uint32_t c = cg / p.G, g = cg % p.G;
+        const uint32_t t0 = c * kFine;
+        const uint32_t nf = min(uint32_t(kFine), p.num_tiles - t0);
+        const uint64_t lo = uint64_t(g) * p.chunk, hi = min(lo + p.chunk, p.n);
+        const uint32_t nr = uint32_t((hi - lo + kRmRound - 1) / kRmRound);
+        const uint64_t row0 = lo / kRmRound;
+        // piece table of this segment
+        for (uint32_t r = threadIdx.x; r < nr; r += blockDim.x) {
+            const uint64_t row = (row0 + r) * p.C + c;
+            plen[r] = p.rhist[row];
+            pstart[r] = uint32_t(lo + uint64_t(r) * kRmRound) + p.rbase[row];
+        }
+        for (uint32_t f = threadIdx.x; f < nf; f += blockDim.x)
+            cursor[f] = p.fine_off[uint64_t(t0 + f) * p.G + g];
+        __syncthreads();
+        small_excl_scan(plen, pp, nr, &ptot);
+        __syncthreads();
+        for (uint32_t f0 = 0; f0 < seg_len; f0 += kRound) {
+            for (uint32_t f = threadIdx.x; f < nf; f += blockDim.x) hist[f] = 0;
+            uint32_t m_idx[RPT], m_src[RPT];
+            V m_val[RPT];
+#pragma unroll
+            for (int j = 0; j < RPT; j++) {
+                const uint32_t fl = f0 + uint32_t(j) * 1024 + threadIdx.x;
+                m_src[j] = 0xFFFFFFFFu;
+                if (fl < seg_len) {
+                    uint32_t a = 0, b = nr;               // last piece r with pp[r] <= fl
+                    while (b - a > 1) {
+                        const uint32_t mid = (a + b) >> 1;
+                        if (pp[mid] <= fl) a = mid; else b = mid;
+                    }
+                    m_src[j] = pstart[a] + (fl - pp[a]);
+                }
+            }
+#pragma unroll
+            for (int j = 0; j < RPT; j++) {
+                const bool in = m_src[j] != 0xFFFFFFFFu;
+                m_idx[j] = in ? p.tmp_idx[m_src[j]] : 0u;
+                m_val[j] = (in && p.tmp_val) ? reinterpret_cast<const V*>(p.tmp_val)[m_src[j]] : V(0);
+            }
+            __syncthreads();
+            uint32_t m_rank[RPT], m_f[RPT];
+#pragma unroll
+            for (int j = 0; j < RPT; j++) {
+                m_f[j] = (m_idx[j] >> p.tile_shift) - t0;
+                if (m_src[j] != 0xFFFFFFFFu) m_rank[j] = atomicAdd(&hist[m_f[j]], 1u);
+            }
+            __syncthreads();
+            small_excl_scan(hist, base, nf, &tot);
+            __syncthreads();
+#pragma unroll
+            for (int j = 0; j < RPT; j++) {
+                if (m_src[j] == 0xFFFFFFFFu) continue;
+                const uint32_t q = base[m_f[j]] + m_rank[j];
+                s_l[q] = uint16_t(m_idx[j] & lmask);
+                s_val[q] = m_val[j];
+                s_f[q] = uint8_t(m_f[j]);
+                if (p.rpos) p.rpos[m_src[j]] = cursor[m_f[j]] + m_rank[j];
+            }
+            __syncthreads();
+            const uint32_t total = tot;
+            for (uint32_t q = threadIdx.x; q < total; q += blockDim.x) {
+                const uint32_t f = s_f[q];
+                const uint32_t dst = cursor[f] + q - base[f];
+                p.bin_lidx[dst] = s_l[q];
+                if (p.tmp_val) reinterpret_cast<V*>(p.bin_val)[dst] = s_val[q];
+            }
+            __syncthreads();
+            for (uint32_t f = threadIdx.x; f < nf; f += blockDim.x) cursor[f] += hist[f];
+        }
+        __syncthreads();
     }
 }
 
@@ -683,11 +915,12 @@ __global__ __launch_bounds__(1024) void k_tile_delta(TileArgs a) {
 // hit L2; map[k] == ~0 marks an out-of-bounds record (left unwritten).
 template <int VB>
 __global__ __launch_bounds__(1024) void k_unpartition(const uint32_t* __restrict__ map, uint64_t n,
-                                                      const uint32_t* n_dev, uint64_t chunk,
+                                                      const uint32_t* n_dev, const uint32_t* bound_dev, uint64_t chunk,
                                                       const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
                                                       const uint8_t* __restrict__ ok_src, uint8_t* __restrict__ ok_dst) {
     using V = typename idx_t<VB>::I;
     const uint64_t m = n_dev ? uint64_t(*n_dev) : n;
+    const uint32_t bound = bound_dev ? *bound_dev : 0xFFFFFFFFu;   // round-major temp slots may be holes
     const uint64_t lo = uint64_t(blockIdx.x) * chunk;
     const uint64_t hi = min(lo + chunk, m);
     const V* s = reinterpret_cast<const V*>(src);
@@ -701,7 +934,7 @@ __global__ __launch_bounds__(1024) void k_unpartition(const uint32_t* __restrict
         }
 #pragma unroll
         for (int j = 0; j < 4; j++) {
-            if (p[j] == 0xFFFFFFFFu) continue;
+            if (p[j] == 0xFFFFFFFFu || p[j] >= bound) continue;
             const uint64_t k = k0 + uint64_t(j) * 1024;
             d[k] = s[p[j]];
             if (ok_src) ok_dst[k] = ok_src[p[j]];
@@ -791,6 +1024,7 @@ size_t tiled_ws_bytes(uint64_t cap) {
     b += al(cap * 4) + al(cap * 8) + al(cap * 4);
     b += 2 * al((size_t(kMaxTiles) + 1) * 4) + al(size_t(kMaxTiles) / kScanItems * 4 + 256) + al(4);
     b += al((size_t(kMaxTiles) + 2 * (cap / kSplit) + 2) * 16);   // owner items + delta pieces
+    b += 2 * al((cap / 4096 + 2) * size_t(kMaxCoarse) * 2);         // round-major rhist / rbase
     return b;
 }
 
@@ -815,6 +1049,9 @@ TiledWs carve_tiled_ws(uint8_t* base, uint64_t cap) {
     w.plan_partials = reinterpret_cast<uint32_t*>(p); p += al(size_t(kMaxTiles) / kScanItems * 4 + 256);
     w.item_count = reinterpret_cast<uint32_t*>(p); p += al(4);
     w.items = p;                                   // [kMaxTiles] owner items, then delta pieces
+    p += al((size_t(kMaxTiles) + 2 * (cap / kSplit) + 2) * 16);
+    w.rhist = reinterpret_cast<uint16_t*>(p); p += al((cap / 4096 + 2) * size_t(kMaxCoarse) * 2);
+    w.rbase = reinterpret_cast<uint16_t*>(p);
     return w;
 }
 
@@ -858,6 +1095,11 @@ static void dispatch_vb_rpt(int vb, int rpt, F&& f) {
     default: with_vb(integral_constant<int, 8>{}); break;
     }
 }
+// LMR_PARTITION=rm selects the round-major two-level partition (no count pass)
+static bool partition_rm_enabled() {      // read per call: tests switch it within one process
+    const char* e = getenv("LMR_PARTITION");
+    return e && e[0] == 'r' && e[1] == 'm';
+}
 static int fine_blocks_cap() {
     static int v = env_int("LMR_FINE_BLOCKS", 512, 1, 1 << 20);
     return v;
@@ -887,6 +1129,72 @@ hipError_t launch_apply_tiled(int dtype, int index_size, const ApplyArgs& a, con
     b.err = a.err;
     const size_t hist_lds = size_t(num_tiles) * 4;
     hipError_t e;
+    // Round-major two-level partition (LMR_PARTITION=rm): no count pass. Block
+    // chunks become multiples of kRmRound with at most kRmMaxRounds rounds each.
+    bool rm = false;
+    if (num_tiles > uint64_t(kFine) && partition_rm_enabled()) {
+        uint64_t ch = ((a.n + G - 1) / G + kRmRound - 1) / kRmRound * kRmRound;
+        const uint64_t ch_max = uint64_t(kRmMaxRounds) * kRmRound;
+        if (ch > ch_max) ch = ch_max;
+        const uint64_t Gr = (a.n + ch - 1) / ch;
+        if (Gr <= uint64_t(kMaxBinBlocks)) {
+            rm = true;
+            G = Gr;
+            b.G = uint32_t(G);
+            b.chunk = ch;
+        }
+    }
+    if (rm) {
+        PartArgs q;
+        q.idx = a.idx; q.idx_stride = a.idx_stride; q.val = a.val; q.val_stride = a.val_stride;
+        q.n = a.n; q.shard_len = a.shard_len; q.chunk = b.chunk; q.tile_shift = shift;
+        q.num_tiles = uint32_t(num_tiles); q.G = uint32_t(G);
+        q.C = uint32_t((num_tiles + kFine - 1) / kFine);
+        q.fine_off = w.counts; q.tile_start = w.tile_start; q.coarse_off = w.coarse_off;
+        q.tmp_idx = w.tmp_idx; q.tmp_val = a.val ? w.tmp_val : nullptr;
+        q.qpos = has_res ? w.qpos : nullptr;
+        q.bin_lidx = w.bin_lidx; q.bin_val = w.bin_val; q.rpos = b.rpos;
+        q.counts = w.counts; q.rhist = w.rhist; q.rbase = w.rbase;
+        q.R = uint32_t(b.chunk / kRmRound); q.err = a.err;
+        {
+        ProfScope ps(a.prof, LMR_STAGE_BIN_SCATTER, s);
+        const size_t th_lds = size_t((num_tiles + 1) / 2) * 4;
+        e = dispatch_iw(index_size, [&](auto iw) {
+            constexpr int IW = decltype(iw)::value;
+            switch (vb) {
+            case 1: hipLaunchKernelGGL((k_coarse_rm<IW, 1>), dim3(unsigned(G)), dim3(1024), th_lds, s, q); break;
+            case 2: hipLaunchKernelGGL((k_coarse_rm<IW, 2>), dim3(unsigned(G)), dim3(1024), th_lds, s, q); break;
+            case 4: hipLaunchKernelGGL((k_coarse_rm<IW, 4>), dim3(unsigned(G)), dim3(1024), th_lds, s, q); break;
+            default: hipLaunchKernelGGL((k_coarse_rm<IW, 8>), dim3(unsigned(G)), dim3(1024), th_lds, s, q); break;
+            }
+            return hipGetLastError();
+        });
+        }
+        if (e != hipSuccess) return e;
+        {
+        ProfScope ps(a.prof, LMR_STAGE_SCAN, s);
+        const uint64_t ncg = uint64_t(q.C) * G;
+        hipLaunchKernelGGL(k_rm_seg_sizes, dim3(unsigned((ncg + 1 + 255) / 256)), dim3(256), 0, s, q, w.coarse_off);
+        e = scan_exclusive_u32(w.coarse_off, ncg + 1, w.partials, w.total, s);
+        if (e != hipSuccess) return e;
+        e = scan_exclusive_u32(w.counts, num_tiles * G, w.partials, w.total, s);
+        if (e != hipSuccess) return e;
+        hipLaunchKernelGGL(k_tile_starts, dim3(unsigned((num_tiles + 1 + 255) / 256)), dim3(256), 0, s,
+                           w.counts, uint32_t(num_tiles), uint32_t(G), w.total, w.tile_start);
+        }
+        {
+        ProfScope pf(a.prof, LMR_STAGE_FINE_SCATTER, s);
+        const uint64_t nseg = uint64_t(q.C) * G;
+        const unsigned fgrid = unsigned(nseg < uint64_t(fine_blocks_cap()) ? nseg : fine_blocks_cap());
+        switch (vb) {
+        case 1: hipLaunchKernelGGL((k_fine_rm<1>), dim3(fgrid), dim3(1024), 0, s, q); break;
+        case 2: hipLaunchKernelGGL((k_fine_rm<2>), dim3(fgrid), dim3(1024), 0, s, q); break;
+        case 4: hipLaunchKernelGGL((k_fine_rm<4>), dim3(fgrid), dim3(1024), 0, s, q); break;
+        default: hipLaunchKernelGGL((k_fine_rm<8>), dim3(fgrid), dim3(1024), 0, s, q); break;
+        }
+        e = hipGetLastError();
+        }
+    } else {
     {
     ProfScope ps(a.prof, LMR_STAGE_BIN_COUNT, s);
     e = dispatch_iw(index_size, [&](auto iw) {
@@ -949,6 +1257,7 @@ hipError_t launch_apply_tiled(int dtype, int index_size, const ApplyArgs& a, con
         return hipGetLastError();
     });
     }
+    }   // count-based partition
     if (e != hipSuccess) return e;
     ProfScope ps(a.prof, LMR_STAGE_TILE_APPLY, s);
     // work plan: owner items, and delta items for hot tiles of combinable ops
@@ -996,21 +1305,24 @@ hipError_t launch_apply_tiled(int dtype, int index_size, const ApplyArgs& a, con
     // un-partition: binned -> (temp ->) input order, each a block-contiguous gather
     ProfScope pu(a.prof, LMR_STAGE_UNPARTITION, s);
     const uint8_t* ok_src = (a.ret == LMR_RET_RESULT) ? ok_bin : nullptr;
-    auto gather = [&](const uint32_t* map, const uint32_t* n_dev, const uint8_t* src, uint8_t* dst,
-                      const uint8_t* oks, uint8_t* okd) {
+    auto gather = [&](const uint32_t* map, const uint32_t* n_dev, const uint32_t* bound_dev, const uint8_t* src,
+                      uint8_t* dst, const uint8_t* oks, uint8_t* okd) {
         switch (vb) {
-        case 1: hipLaunchKernelGGL((k_unpartition<1>), dim3(unsigned(G)), dim3(1024), 0, s, map, a.n, n_dev, b.chunk, src, dst, oks, okd); break;
-        case 2: hipLaunchKernelGGL((k_unpartition<2>), dim3(unsigned(G)), dim3(1024), 0, s, map, a.n, n_dev, b.chunk, src, dst, oks, okd); break;
-        case 4: hipLaunchKernelGGL((k_unpartition<4>), dim3(unsigned(G)), dim3(1024), 0, s, map, a.n, n_dev, b.chunk, src, dst, oks, okd); break;
-        default: hipLaunchKernelGGL((k_unpartition<8>), dim3(unsigned(G)), dim3(1024), 0, s, map, a.n, n_dev, b.chunk, src, dst, oks, okd); break;
+        case 1: hipLaunchKernelGGL((k_unpartition<1>), dim3(unsigned(G)), dim3(1024), 0, s, map, a.n, n_dev, bound_dev, b.chunk, src, dst, oks, okd); break;
+        case 2: hipLaunchKernelGGL((k_unpartition<2>), dim3(unsigned(G)), dim3(1024), 0, s, map, a.n, n_dev, bound_dev, b.chunk, src, dst, oks, okd); break;
+        case 4: hipLaunchKernelGGL((k_unpartition<4>), dim3(unsigned(G)), dim3(1024), 0, s, map, a.n, n_dev, bound_dev, b.chunk, src, dst, oks, okd); break;
+        default: hipLaunchKernelGGL((k_unpartition<8>), dim3(unsigned(G)), dim3(1024), 0, s, map, a.n, n_dev, bound_dev, b.chunk, src, dst, oks, okd); break;
         }
     };
     if (num_tiles > uint64_t(kFine)) {
         uint8_t* ok_tmp = ok_src ? reinterpret_cast<uint8_t*>(w.bin_lidx) : nullptr;
-        gather(w.rpos, w.total, res_bin, w.bin_val, ok_src, ok_tmp);                       // binned -> temp
-        gather(w.qpos, nullptr, w.bin_val, reinterpret_cast<uint8_t*>(a.results), ok_tmp, a.ok);  // temp -> input
+        if (rm)   // temp slots are input positions (holes where records were out of bounds)
+            gather(w.rpos, nullptr, w.total, res_bin, w.bin_val, ok_src, ok_tmp);
+        else
+            gather(w.rpos, w.total, nullptr, res_bin, w.bin_val, ok_src, ok_tmp);          // binned -> temp
+        gather(w.qpos, nullptr, nullptr, w.bin_val, reinterpret_cast<uint8_t*>(a.results), ok_tmp, a.ok);  // temp -> input
     } else {
-        gather(w.rpos, nullptr, res_bin, reinterpret_cast<uint8_t*>(a.results), ok_src, a.ok);
+        gather(w.rpos, nullptr, nullptr, res_bin, reinterpret_cast<uint8_t*>(a.results), ok_src, a.ok);
     }
     return hipGetLastError();
 }

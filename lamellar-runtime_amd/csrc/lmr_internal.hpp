@@ -60,6 +60,8 @@ struct TiledWs {
     uint32_t* plan_partials;
     uint32_t* item_count;  // [1]
     uint8_t* items;        // TileItem[kMaxTiles] owner items, then delta pieces
+    uint16_t* rhist;       // round-major partition: per-round bucket counts
+    uint16_t* rbase;       //                         per-round bucket offsets
 };
 size_t tiled_ws_bytes(uint64_t cap);
 TiledWs carve_tiled_ws(uint8_t* base, uint64_t cap);

@@ -372,8 +372,19 @@ def test_device_errors(world, lam, strategy):
         k.strategy = old
 
 
+@pytest.fixture(params=["count", "rm"])
+def partition(request, monkeypatch):
+    """Two-level partition variant: count pass + bucket-major temp ("count") or the
+    round-major temp with the tile counts built in the coarse pass ("rm")."""
+    if request.param == "rm":
+        monkeypatch.setenv("LMR_PARTITION", "rm")
+    else:
+        monkeypatch.delenv("LMR_PARTITION", raising=False)
+    return request.param
+
+
 @pytest.mark.parametrize("dt", ["u64", "u32", "u8", "i16", "i64", "f32", "f64"])
-def test_tiled_two_level_partition_bit_exact(world, orc, lam, dt):
+def test_tiled_two_level_partition_bit_exact(world, orc, lam, dt, partition):
     """> 128 tiles: coarse + fine LDS-staged partition before the tile apply."""
     k = world.team().kernels
     k.reserve(1 << 21)
@@ -390,7 +401,7 @@ def test_tiled_two_level_partition_bit_exact(world, orc, lam, dt):
             assert np.array_equal(c.ok_d, c.ok_o)
 
 
-def test_tiled_two_level_collisions(world, orc, lam):
+def test_tiled_two_level_collisions(world, orc, lam, partition):
     """Colliding u64 fetch_add over > 128 tiles: exact final state; each element's olds
     are exactly init, init+1, ..., init+m-1 (v = 1)."""
     k = world.team().kernels
@@ -412,7 +423,7 @@ def test_tiled_two_level_collisions(world, orc, lam):
 
 
 @pytest.mark.parametrize("dt", ["u64", "i32", "u16", "f64", "f32"])
-def test_hot_tile_delta_mode(world, orc, lam, dt):
+def test_hot_tile_delta_mode(world, orc, lam, dt, partition):
     """Skewed stream: one element takes ~40 % of all records, so its tile is split into
     delta-mode work items (LDS combine + one global atomic per element per item).
     Integer ops: exact final state, fetch olds a valid chain; floats: exact with 1.0."""
@@ -445,3 +456,37 @@ def test_hot_tile_delta_mode(world, orc, lam, dt):
                  (np.arange(m, dtype=np.int64) * step).astype(np.uint64)).astype(t)
             exp = np.sort(exp.astype(np.float64) if IS_FLOAT[dt] else exp.astype(np.uint64))
             assert np.array_equal(olds, exp), (dt, op)
+
+
+def test_two_level_out_of_bounds_fetch(world, orc, lam, partition):
+    """Out-of-bounds records in a two-level tiled fetch_add: the error bit is raised, every
+    in-bounds record is applied exactly once and returns a valid old value, and the
+    un-partition never reads a hole (round-major temp slots of dropped records)."""
+    k = world.team().kernels
+    k.reserve(1 << 21)
+    rng = np.random.default_rng(77)
+    shard_len = (1 << 21) + 3
+    n = 1 << 20
+    idx = rng.permutation(shard_len)[:n].astype(np.uint64)
+    bad = rng.random(n) < 0.01
+    idx[bad] = shard_len + rng.integers(0, 1000, int(bad.sum())).astype(np.uint64)
+    shard0 = rng.integers(0, 2**40, shard_len).astype(np.uint64)
+    vals = rng.integers(0, 2**20, n).astype(np.uint64)
+    d_shard = to_dev(shard0)
+    d_res = torch.zeros(n * 8, dtype=torch.uint8, device="cuda")
+    old = k.strategy
+    k.strategy = 2
+    try:
+        k.apply_soa(d_shard, shard_len, 1, lam.dtype_of("u64"), FETCH_ADD, to_dev(idx), 8, to_dev(vals), 0, n,
+                    d_res, None)
+        k.synchronize()
+        assert k.errors(clear=True) & 1
+    finally:
+        k.strategy = old
+    got = d_shard.cpu().numpy().view(np.uint64)[:shard_len]
+    exp = shard0.copy()
+    good = ~bad
+    exp[idx[good].astype(np.int64)] += vals[good]
+    assert np.array_equal(got, exp)
+    res = d_res.cpu().numpy().view(np.uint64)
+    assert np.array_equal(res[good], shard0[idx[good].astype(np.int64)])
