@@ -363,14 +363,25 @@ constexpr uint32_t kRmRound = 4096;
 constexpr uint32_t kRmMaxRounds = 128;     // piece tables are scanned by one wave (<= 128 entries)
 constexpr int kRmFlush = 15;               // rounds between u16 tile-counter flushes (15 * 4096 < 65536)
 
+// block copy of `total` LDS elements to 16-B-aligned global memory, 16 bytes per lane
+template <typename T>
+__device__ __forceinline__ void copy_out_16(const T* lds, T* g, uint32_t total) {
+    constexpr uint32_t per = 16 / sizeof(T);
+    const uint32_t nv = total / per;
+    const uint4* src = reinterpret_cast<const uint4*>(lds);
+    uint4* dst = reinterpret_cast<uint4*>(g);
+    for (uint32_t v = threadIdx.x; v < nv; v += blockDim.x) dst[v] = src[v];
+    for (uint32_t q = nv * per + threadIdx.x; q < total; q += blockDim.x) g[q] = lds[q];
+}
+
 template <int IW, int VB>
 __global__ __launch_bounds__(1024, 8) void k_coarse_rm(PartArgs p) {
     using V = typename idx_t<VB>::I;
     constexpr int RPT = kRmRound / 1024;
     extern __shared__ uint32_t th[];                         // packed u16 tile counters
     __shared__ uint32_t hist[kMaxCoarse], base[kMaxCoarse], tot;
-    __shared__ uint32_t s_idx[kRmRound];
-    __shared__ V s_val[kRmRound];
+    __shared__ __align__(16) uint32_t s_idx[kRmRound];
+    __shared__ __align__(16) V s_val[kRmRound];
     const uint32_t g = blockIdx.x, C = p.C;
     const int cshift = p.tile_shift + kFineShift;
     const uint32_t nw = (p.num_tiles + 1) >> 1;
@@ -446,10 +457,9 @@ __global__ __launch_bounds__(1024, 8) void k_coarse_rm(PartArgs p) {
         }
         __syncthreads();
         const uint32_t total = tot;
-        for (uint32_t q = threadIdx.x; q < total; q += blockDim.x) {
-            p.tmp_idx[r0 + q] = s_idx[q];
-            if (p.val) reinterpret_cast<V*>(p.tmp_val)[r0 + q] = s_val[q];
-        }
+        // the round's region starts at input position r0 (a multiple of kRmRound): 16-B aligned
+        copy_out_16(s_idx, p.tmp_idx + r0, total);
+        if (p.val) copy_out_16(s_val, reinterpret_cast<V*>(p.tmp_val) + r0, total);
         if ((r % kRmFlush) == kRmFlush - 1 || r0 + kRmRound >= hi) flush();
         __syncthreads();
     }
@@ -799,9 +809,20 @@ __global__ __launch_bounds__(1024, 8) void k_tile_owner(TileArgs a) {
     const uint64_t base = uint64_t(w.tile) << a.tile_shift;
     const uint32_t len = uint32_t(min(uint64_t(1) << a.tile_shift, a.shard_len - base));
     T* shard = reinterpret_cast<T*>(a.shard) + base;
-    for (uint32_t e = threadIdx.x; e < len; e += blockDim.x) {
-        if constexpr (sizeof(T) >= 4) tile[e] = shard[e];          // W == T
-        else tile[e] = W(U(shard[e]));                              // widen the bits
+    // 16 B per lane when the shard is 16-B aligned (sub-array views may not be)
+    const bool vec = sizeof(T) >= 4 && (reinterpret_cast<uintptr_t>(shard) & 15) == 0;
+    if constexpr (sizeof(T) >= 4) {
+        if (vec) {
+            constexpr uint32_t per = 16 / sizeof(T);
+            const uint32_t nv = len / per;
+            for (uint32_t v = threadIdx.x; v < nv; v += blockDim.x)
+                reinterpret_cast<uint4*>(tile)[v] = reinterpret_cast<const uint4*>(shard)[v];
+            for (uint32_t e = nv * per + threadIdx.x; e < len; e += blockDim.x) tile[e] = shard[e];
+        } else {
+            for (uint32_t e = threadIdx.x; e < len; e += blockDim.x) tile[e] = shard[e];   // W == T
+        }
+    } else {
+        for (uint32_t e = threadIdx.x; e < len; e += blockDim.x) tile[e] = W(U(shard[e]));   // widen the bits
     }
     __syncthreads();
     // kOwnUnroll records per thread per round: all loads issued before the LDS atomics
@@ -832,9 +853,18 @@ __global__ __launch_bounds__(1024, 8) void k_tile_owner(TileArgs a) {
     }
     __syncthreads();
     if (!op_is_read(op)) {
-        for (uint32_t e = threadIdx.x; e < len; e += blockDim.x) {
-            if constexpr (sizeof(T) >= 4) shard[e] = tile[e];
-            else shard[e] = T(U(tile[e]));
+        if constexpr (sizeof(T) >= 4) {
+            if (vec) {
+                constexpr uint32_t per = 16 / sizeof(T);
+                const uint32_t nv = len / per;
+                for (uint32_t v = threadIdx.x; v < nv; v += blockDim.x)
+                    reinterpret_cast<uint4*>(shard)[v] = reinterpret_cast<const uint4*>(tile)[v];
+                for (uint32_t e = nv * per + threadIdx.x; e < len; e += blockDim.x) shard[e] = tile[e];
+            } else {
+                for (uint32_t e = threadIdx.x; e < len; e += blockDim.x) shard[e] = tile[e];
+            }
+        } else {
+            for (uint32_t e = threadIdx.x; e < len; e += blockDim.x) shard[e] = T(U(tile[e]));
         }
     }
 }

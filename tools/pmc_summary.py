@@ -13,17 +13,18 @@ import json
 import os
 import sys
 
-# stage -> (anchor kernel, kernels whose bytes belong to the stage)
+# stage -> (anchor kernels, first one present counts invocations; kernels whose bytes belong to the stage)
 STAGES = {
-    "bin_count": ("k_bin_count", ("k_bin_count",)),
-    "bin_scatter": ("k_coarse_scatter", ("k_coarse_scatter", "k_coarse_offsets", "k_bin_scatter")),
-    "fine_scatter": ("k_fine_scatter", ("k_fine_scatter",)),
-    "tile_apply": ("k_tile_owner", ("k_tile_owner", "k_tile_delta", "k_tile_plan_count", "k_tile_plan_extra",
-                                    "k_tile_plan_fill")),
-    "unpartition": ("k_tile_owner", ("k_unpartition",)),
-    "direct": ("k_apply_direct", ("k_apply_direct",)),
-    "pack": ("k_pack_count", ("k_pack_count", "k_pack_scatter", "k_pack_stage", "k_dest_offsets")),
-    "scatter_results": ("k_scatter_results", ("k_scatter_results",)),
+    "bin_count": (("k_bin_count",), ("k_bin_count",)),
+    "bin_scatter": (("k_coarse_scatter", "k_coarse_rm", "k_bin_scatter"),
+                    ("k_coarse_scatter", "k_coarse_offsets", "k_bin_scatter", "k_coarse_rm")),
+    "fine_scatter": (("k_fine_scatter", "k_fine_rm"), ("k_fine_scatter", "k_fine_rm", "k_rm_seg_sizes")),
+    "tile_apply": (("k_tile_owner",), ("k_tile_owner", "k_tile_delta", "k_tile_plan_count", "k_tile_plan_extra",
+                                       "k_tile_plan_fill")),
+    "unpartition": (("k_tile_owner",), ("k_unpartition",)),
+    "direct": (("k_apply_direct",), ("k_apply_direct",)),
+    "pack": (("k_pack_count",), ("k_pack_count", "k_pack_scatter", "k_pack_stage", "k_dest_offsets")),
+    "scatter_results": (("k_scatter_results",), ("k_scatter_results",)),
 }
 
 
@@ -53,8 +54,9 @@ def main():
         tot[b] += fb + wb
         cnt[b] += n
     out = {}
-    for st, (anchor, ks) in STAGES.items():
-        if cnt.get(anchor):
+    for st, (anchors, ks) in STAGES.items():
+        anchor = next((a for a in anchors if cnt.get(a)), None)
+        if anchor:
             out[st] = sum(tot.get(x, 0.0) for x in ks) / cnt[anchor]
             print(f"stage {st:16s} {out[st] / 1e6:10.1f} MB per invocation")
     if len(sys.argv) > 2:
