@@ -630,6 +630,57 @@ int orc_batch_op(const lmr_layout_t* L, void* const* pe_slices, uint32_t kind,
     return st;
 }
 
+/* ---- reductions: array_reduce.rs:82-88 (per-PE fold), :90-107 (cross-PE tree), :283-319 (ops) */
+#define RED_STEP(T, UT, a, b, op)                                                        \
+    ((op) == 0 ? (T)((UT)(a) + (UT)(b)) : (op) == 1 ? (T)((UT)(a) * (UT)(b))            \
+     : (op) == 2 ? ((a) > (b) ? (a) : (b)) : ((a) < (b) ? (a) : (b)))
+#define FRED_STEP(a, b, op)                                                              \
+    ((op) == 0 ? (a) + (b) : (op) == 1 ? (a) * (b) : (op) == 2 ? ((a) > (b) ? (a) : (b)) \
+     : ((a) < (b) ? (a) : (b)))
+
+static void red_combine(uint32_t dtype, uint32_t op, void* acc, const void* v) {
+    switch (dtype) {
+#define RC(CODE, T, UT) case CODE: { T a, b; memcpy(&a, acc, sizeof a); memcpy(&b, v, sizeof b); \
+        T r = RED_STEP(T, UT, a, b, op); memcpy(acc, &r, sizeof r); break; }
+    RC(LMR_U8, uint8_t, uint8_t) RC(LMR_U16, uint16_t, uint16_t) RC(LMR_U32, uint32_t, uint32_t)
+    RC(LMR_U64, uint64_t, uint64_t) RC(LMR_I8, int8_t, uint8_t) RC(LMR_I16, int16_t, uint16_t)
+    RC(LMR_I32, int32_t, uint32_t) RC(LMR_I64, int64_t, uint64_t)
+#undef RC
+    case LMR_F32: { float a, b; memcpy(&a, acc, 4); memcpy(&b, v, 4); float r = FRED_STEP(a, b, op); memcpy(acc, &r, 4); break; }
+    case LMR_F64: { double a, b; memcpy(&a, acc, 8); memcpy(&b, v, 8); double r = FRED_STEP(a, b, op); memcpy(acc, &r, 8); break; }
+    default: break;
+    }
+}
+
+void orc_reduce(uint32_t dtype, uint32_t op, const void* data, uint64_t n, void* out, uint8_t* has) {
+    const size_t eb = orc_dtype_bytes(dtype);
+    *has = n > 0;
+    if (!n) return;
+    memcpy(out, data, eb);
+    for (uint64_t k = 1; k < n; k++) red_combine(dtype, op, out, (const uint8_t*)data + k * eb);
+}
+
+static int red_tree(uint32_t dtype, uint32_t op, const uint8_t* vals, const uint8_t* has, uint32_t lo,
+                    uint32_t hi, uint8_t* out) {
+    const size_t eb = orc_dtype_bytes(dtype);
+    if (lo == hi) {
+        if (has[lo]) memcpy(out, vals + lo * eb, eb);
+        return has[lo] != 0;
+    }
+    const uint32_t mid = (lo + hi) / 2;
+    uint8_t r[8];
+    const int hl = red_tree(dtype, op, vals, has, lo, mid, out);
+    const int hr = red_tree(dtype, op, vals, has, mid + 1, hi, r);
+    if (!hl) { if (hr) memcpy(out, r, eb); return hr; }
+    if (hr) red_combine(dtype, op, out, r);
+    return 1;
+}
+
+void orc_reduce_tree(uint32_t dtype, uint32_t op, const void* vals, const uint8_t* has, uint32_t npes,
+                     void* out, uint8_t* out_has) {
+    *out_has = npes ? (uint8_t)red_tree(dtype, op, (const uint8_t*)vals, has, 0, npes - 1, (uint8_t*)out) : 0;
+}
+
 void orc_scatter_results(const void* res_in, const uint64_t* res_pos, uint64_t n,
                          uint32_t elem_bytes, void* res_out) {
     for (uint64_t k = 0; k < n; k++)

@@ -103,6 +103,17 @@ int orc_batch_op(const lmr_layout_t* L, void* const* pe_slices, uint32_t kind,
                  const uint64_t* gidx, uint64_t i_len, const void* vals, uint64_t v_len,
                  void* results, uint8_t* ok);
 
+/* ---- reductions (impl/src/array_reduce.rs; UnsafeArray::reduce, unsafe.rs:1414-1557) ----
+ * orc_reduce: one PE's step, `local_data().iter().reduce(op)` (array_reduce.rs:82-88) — a
+ * sequential left fold with the closures of :283-319 (`acc + val`, `acc * val` wrapping as
+ * release-mode Rust; `if a > b {a} else {b}`; `if a < b {a} else {b}`). *has = 0 for an
+ * empty slice (None). op: 0 sum, 1 prod, 2 max, 3 min.
+ * orc_reduce_tree: the cross-PE tree of :90-107 over per-PE (has, value) pairs: [lo, hi]
+ * splits at mid = (lo + hi) / 2, a None side is the identity, op(left, right) otherwise. */
+void orc_reduce(uint32_t dtype, uint32_t op, const void* data, uint64_t n, void* out, uint8_t* has);
+void orc_reduce_tree(uint32_t dtype, uint32_t op, const void* vals, const uint8_t* has, uint32_t npes,
+                     void* out, uint8_t* out_has);
+
 /* result reorder: ArrayFetchBatchOpHandle (operations/handle.rs:315-317) */
 void orc_scatter_results(const void* res_in, const uint64_t* res_pos, uint64_t n,
                          uint32_t elem_bytes, void* res_out);

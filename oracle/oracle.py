@@ -75,6 +75,8 @@ def lib():
             "orc_batch_op": (c_int, [L, c_void_p, c_uint32, c_uint32, c_uint32, c_void_p, c_void_p,
                                      c_void_p, c_uint64, c_void_p, c_uint64, c_void_p, c_void_p]),
             "orc_scatter_results": (None, [c_void_p, c_void_p, c_uint64, c_uint32, c_void_p]),
+            "orc_reduce": (None, [c_uint32, c_uint32, c_void_p, c_uint64, c_void_p, c_void_p]),
+            "orc_reduce_tree": (None, [c_uint32, c_uint32, c_void_p, c_void_p, c_uint32, c_void_p, c_void_p]),
             "cpu_baseline_run": (c_int, [c_uint32, c_uint32, c_void_p, c_uint64, c_void_p, c_void_p,
                                          c_void_p, c_uint64, c_uint32, c_uint64, c_void_p,
                                          POINTER(CpuTimes)]),
@@ -229,3 +231,28 @@ def cpu_baseline(dtype_code, np_dtype, op, shard, gidx, vals, threads, threshold
     st = lib().cpu_baseline_run(dtype_code, op, shard.ctypes.data, shard.size, _ptr(gidx), _ptr(v),
                                 _ptr(sv), n, threads, threshold, _ptr(res), ctypes.byref(t))
     return st, t, res
+
+
+REDUCE_OPS = {"sum": 0, "prod": 1, "max": 2, "min": 3}
+
+
+def reduce(dtype_code, np_dtype, op, data):
+    """One PE's reduction step (array_reduce.rs:82-88): value or None."""
+    a = np.ascontiguousarray(np.asarray(data, dtype=np_dtype))
+    out = np.zeros(1, dtype=np_dtype)
+    has = np.zeros(1, dtype=np.uint8)
+    lib().orc_reduce(dtype_code, REDUCE_OPS[op], a.ctypes.data if a.size else None, a.size, out.ctypes.data,
+                     has.ctypes.data)
+    return out[0] if has[0] else None
+
+
+def reduce_tree(dtype_code, np_dtype, op, per_pe):
+    """Cross-PE tree (array_reduce.rs:90-107) over per-PE values (None = empty PE)."""
+    n = len(per_pe)
+    vals = np.array([0 if v is None else v for v in per_pe], dtype=np_dtype)
+    has = np.array([v is not None for v in per_pe], dtype=np.uint8)
+    out = np.zeros(1, dtype=np_dtype)
+    oh = np.zeros(1, dtype=np.uint8)
+    lib().orc_reduce_tree(dtype_code, REDUCE_OPS[op], vals.ctypes.data, has.ctypes.data, n, out.ctypes.data,
+                          oh.ctypes.data)
+    return out[0] if oh[0] else None

@@ -1,6 +1,7 @@
 """lmr_reduce: the per-PE step of array.sum / prod / max / min
 (src/array/unsafe.rs:1414-1557, impl/src/array_reduce.rs:82-88, 283-319),
-against a sequential numpy fold of the same elements. Integers (wrapping) and
+against the oracle's sequential fold of the same elements (orc_reduce, pinned
+by dist_array_reduce.rs's known answer in test_oracle_known_answers.py). Integers (wrapping) and
 max / min are bit-exact; float sum / prod within a relative tolerance of
 n * eps (the device folds in a tree order)."""
 import numpy as np
@@ -14,19 +15,13 @@ pytestmark = pytest.mark.gpu
 DTS = ["u8", "u16", "u32", "u64", "i8", "i16", "i32", "i64", "f32", "f64"]
 
 
-def seq_fold(op, a):
-    if a.size == 0:
-        return None
-    with np.errstate(over="ignore", invalid="ignore"):
-        if op == "sum":
-            if a.dtype.kind in "iu":
-                return np.add.reduce(a, dtype=a.dtype)
-            return a.sum(dtype=np.float64)
-        if op == "prod":
-            if a.dtype.kind in "iu":
-                return np.multiply.reduce(a, dtype=a.dtype)
-            return np.prod(a.astype(np.float64))
-    return a.max() if op == "max" else a.min()
+CODES = {"u8": 0, "u16": 1, "u32": 2, "u64": 3, "i8": 4, "i16": 5, "i32": 6, "i64": 7, "f32": 8, "f64": 9}
+
+
+def oracle_fold(op, dt, a):
+    """The reference's per-PE step (array_reduce.rs:82-88), restated in the C oracle."""
+    from oracle import oracle as o
+    return o.reduce(CODES[dt], NP[dt], op, a)
 
 
 STORAGE = {1: np.uint8, 2: np.int16, 4: np.int32, 8: np.int64}
@@ -61,7 +56,7 @@ def test_reduce_local(world, lam, dt, op):
         else:
             a = lam.UnsafeArray(world.team(), 1, lam.Distribution.Block, dt)
             got = a.sub_array(0, 0).reduce(op).block()      # empty: the reference's None
-        exp = seq_fold(op, x)
+        exp = oracle_fold(op, dt, x)
         if exp is None:
             assert got is None
             continue
@@ -78,6 +73,6 @@ def test_reduce_sub_array_and_atomic(world, lam):
     x = rng.integers(0, 2**63, 100003).astype(np.uint64)
     store(a, x)
     s = a.sub_array(17, 90017)
-    assert s.sum().block() == np.add.reduce(x[17:90017], dtype=np.uint64)
-    assert s.max().block() == x[17:90017].max()
-    assert a.min().block() == x.min()
+    assert s.sum().block() == oracle_fold("sum", "u64", x[17:90017])
+    assert s.max().block() == oracle_fold("max", "u64", x[17:90017])
+    assert a.min().block() == oracle_fold("min", "u64", x)

@@ -207,3 +207,50 @@ def test_compare_exchange_known_answer(orc, dt, npes, dist):
         for p in range(npes):
             st, res, ok = a.op(CAS, np.arange(length, dtype=np.uint64), T(dt, p), current=init)
             assert st == 0 and np.all(ok == 0)
+
+
+@pytest.mark.parametrize("npes", [1, 2, 3, 4])
+@pytest.mark.parametrize("dist", [0, 1], ids=["Block", "Cyclic"])
+@pytest.mark.parametrize("total_len", [100, 7, 1000])
+def test_reduce_known_answer(orc, npes, dist, total_len):
+    """examples/array_examples/dist_array_reduce.rs:36-109: an UnsafeArray<usize> holding
+    0..total_len (put from PE 0), sum() == (total_len / 2) * (0 + 99) for the default 100
+    elements, Block and Cyclic alike; min / max the ends. The oracle's per-PE fold
+    (array_reduce.rs:82-88) and cross-PE tree (:90-107) must give it on every layout."""
+    from oracle import oracle as o
+    a = SimArray(orc, npes, total_len, dist, "u64", "UnsafeArray")
+    g = np.arange(total_len, dtype=np.uint64)
+    for pe in range(npes):                      # place element i at its owner's local offset
+        for i in g:
+            p, off = orc.pe_and_offset(a.L, int(i))
+            if p == pe:
+                a.shards[pe][off] = i
+    sl = a.slices()
+    per = {op: [o.reduce(3, np.uint64, op, s) for s in sl] for op in ("sum", "min", "max", "prod")}
+    assert o.reduce_tree(3, np.uint64, "sum", per["sum"]) == total_len * (total_len - 1) // 2
+    if total_len == 100:
+        assert o.reduce_tree(3, np.uint64, "sum", per["sum"]) == (total_len // 2) * (0 + 99)
+    assert o.reduce_tree(3, np.uint64, "min", per["min"]) == 0
+    assert o.reduce_tree(3, np.uint64, "max", per["max"]) == total_len - 1
+    assert o.reduce_tree(3, np.uint64, "prod", per["prod"]) == 0
+
+
+@pytest.mark.parametrize("dt", ["u8", "i8", "u16", "i32", "u64", "i64", "f32", "f64"])
+def test_reduce_oracle_vs_sequential_fold(orc, dt):
+    """orc_reduce is the left fold of the reference closures: wrapping integers, float
+    rounding in sequence; None for an empty slice."""
+    from oracle import oracle as o
+    rng = np.random.default_rng(3)
+    t = NP[dt]
+    x = (rng.random(2000) * 100 - 50).astype(t) if dt.startswith("f") else \
+        rng.integers(np.iinfo(t).min, np.iinfo(t).max, 2000, dtype=t, endpoint=True)
+    code = {"u8": 0, "u16": 1, "u32": 2, "u64": 3, "i8": 4, "i16": 5, "i32": 6, "i64": 7, "f32": 8, "f64": 9}[dt]
+    with np.errstate(over="ignore"):
+        acc_s, acc_p = x[0], x[0]
+        for v in x[1:]:
+            acc_s = t(acc_s + v)
+            acc_p = t(acc_p * v)
+    assert np.array([o.reduce(code, t, "sum", x)], t).tobytes() == np.array([acc_s], t).tobytes()
+    assert np.array([o.reduce(code, t, "prod", x)], t).tobytes() == np.array([acc_p], t).tobytes()
+    assert o.reduce(code, t, "max", x) == x.max() and o.reduce(code, t, "min", x) == x.min()
+    assert o.reduce(code, t, "sum", x[:0]) is None
