@@ -61,8 +61,11 @@ def test_reduce_local(world, lam, dt, op):
             assert got is None
             continue
         if dt.startswith("f") and op in ("sum", "prod"):
-            tol = (1e-5 if dt == "f32" else 1e-12) * max(1.0, float(np.abs(x).sum()) if op == "sum" else 1.0)
-            assert abs(float(got) - float(exp)) <= tol * max(1, n) ** 0.5 * 10, (n, got, exp)
+            # both the sequential fold and the device's tree fold are within n*eps of the exact
+            # value (times sum|x| for a sum, |result| for a product of values near 1)
+            eps = float(np.finfo(NP[dt]).eps)
+            scale = float(np.abs(x.astype(np.float64)).sum()) if op == "sum" else abs(float(exp))
+            assert abs(float(got) - float(exp)) <= 2 * n * eps * scale + 1e-30, (n, got, exp)
         else:
             assert np.array(got, dtype=NP[dt]).tobytes() == np.array(exp, dtype=NP[dt]).tobytes(), (n, got, exp)
 
