@@ -92,6 +92,10 @@ SIGNATURES = {
                               c_void_p, c_uint64, c_void_p, c_void_p, c_void_p]),
     "lmr_scatter_results": (c_int, [c_void_p, c_void_p, c_uint64, c_uint32, c_void_p, c_void_p,
                                     c_void_p, c_void_p]),
+    "lmr_stage_begin": (c_int, [c_void_p, POINTER(lmr_apply_desc_t)]),
+    "lmr_stage_soa": (c_int, [c_void_p, c_void_p, c_uint32, c_void_p, c_void_p, c_uint64, c_void_p,
+                              c_void_p, c_void_p]),
+    "lmr_stage_finish": (c_int, [c_void_p, c_void_p]),
 }
 
 STAGES = ["direct", "mvsi", "bin_count", "scan", "bin_scatter", "tile_apply", "pack",

@@ -241,6 +241,10 @@ struct PartArgs {
     uint16_t* rbase;              // [rows][C] per-round bucket offsets inside the round region
     uint32_t R;                   // rounds per full block (chunk / kRmRound)
     uint32_t* err;
+    // grouped fine pass (k_fine_scatter): segments [cg_lo, cg_hi) only, bins written
+    // at (final position - *ring_base) so a group's bins reuse the start of the bin buffer
+    uint32_t cg_lo, cg_hi;
+    const uint32_t* ring_base;    // null: 0
 };
 
 // coarse_off[c][g] = start of block g's coarse-c records in the temp buffer
@@ -289,7 +293,6 @@ __global__ __launch_bounds__(1024) void k_coarse_scatter(PartArgs p) {
     __shared__ uint32_t hist[kMaxCoarse], base[kMaxCoarse], cursor[kMaxCoarse], tot;
     __shared__ uint32_t s_idx[kRound];
     __shared__ V s_val[kRound];
-    __shared__ uint8_t s_c[kRound];
     const uint32_t g = blockIdx.x, C = p.C;
     const int cshift = p.tile_shift + kFineShift;
     for (uint32_t c = threadIdx.x; c < C; c += blockDim.x) cursor[c] = p.coarse_off[uint64_t(c) * p.G + g];
@@ -331,18 +334,17 @@ __global__ __launch_bounds__(1024) void k_coarse_scatter(PartArgs p) {
             const uint32_t q = base[m_c[j]] + m_rank[j];
             s_idx[q] = uint32_t(m_raw[j]);
             s_val[q] = m_val[j];
-            s_c[q] = uint8_t(m_c[j]);
             if (p.qpos) p.qpos[k] = cursor[m_c[j]] + m_rank[j];   // coalesced in k
         }
         if (r0 + kRound < hi) load_round(r0 + kRound);     // prefetch the next round
         __syncthreads();
-        const uint32_t total = tot;
-        for (uint32_t q = threadIdx.x; q < total; q += blockDim.x) {
-            const uint32_t c = s_c[q];
-            const uint32_t dst = cursor[c] + q - base[c];
-            p.tmp_idx[dst] = s_idx[q];
-            if (p.val) reinterpret_cast<V*>(p.tmp_val)[dst] = s_val[q];
-        }
+        if (p.val)
+            bucket_writeout(hist, base, cursor, C, [&](uint32_t q, uint32_t dst) {
+                p.tmp_idx[dst] = s_idx[q];
+                reinterpret_cast<V*>(p.tmp_val)[dst] = s_val[q];
+            });
+        else
+            bucket_writeout(hist, base, cursor, C, [&](uint32_t q, uint32_t dst) { p.tmp_idx[dst] = s_idx[q]; });
         __syncthreads();
         for (uint32_t c = threadIdx.x; c < C; c += blockDim.x) cursor[c] += hist[c];
     }
@@ -594,9 +596,8 @@ __global__ __launch_bounds__(1024) void k_fine_scatter(PartArgs p) {
     __shared__ uint32_t hist[kFine], base[kFine], cursor[kFine], tot;
     __shared__ uint16_t s_l[kRound];
     __shared__ V s_val[kRound];
-    __shared__ uint8_t s_f[kRound];
-    const uint32_t nseg = p.C * p.G;
     const uint32_t lmask = (1u << p.tile_shift) - 1u;
+    const uint32_t rb = p.ring_base ? *p.ring_base : 0u;
     uint32_t m_idx[RPT];
     V m_val[RPT];
     auto load_round = [&](uint32_t r0, uint32_t hi) {
@@ -612,18 +613,19 @@ __global__ __launch_bounds__(1024) void k_fine_scatter(PartArgs p) {
     // (coarse_off is monotone in cg = c*G + g): a contiguous run of producers
     // g of one bucket, so each tile's output run keeps growing from one CU (one
     // XCD's L2 merges its partial lines) and work is balanced by records.
-    const uint64_t total_recs = p.coarse_off[nseg];
+    const uint64_t rec_lo = p.coarse_off[p.cg_lo];
+    const uint64_t total_recs = p.coarse_off[p.cg_hi] - rec_lo;
     auto seg_lower_bound = [&](uint64_t target) {
-        uint32_t lo_s = 0, hi_s = nseg;
+        uint32_t lo_s = p.cg_lo, hi_s = p.cg_hi;
         while (lo_s < hi_s) {
             const uint32_t mid = (lo_s + hi_s) >> 1;
             if (uint64_t(p.coarse_off[mid]) < target) lo_s = mid + 1; else hi_s = mid;
         }
         return lo_s;
     };
-    const uint32_t cg_begin = seg_lower_bound(total_recs * blockIdx.x / gridDim.x);
-    const uint32_t cg_end = (blockIdx.x + 1 == gridDim.x) ? nseg
-                                                          : seg_lower_bound(total_recs * (blockIdx.x + 1) / gridDim.x);
+    const uint32_t cg_begin = seg_lower_bound(rec_lo + total_recs * blockIdx.x / gridDim.x);
+    const uint32_t cg_end = (blockIdx.x + 1 == gridDim.x) ? p.cg_hi
+                                                          : seg_lower_bound(rec_lo + total_recs * (blockIdx.x + 1) / gridDim.x);
     uint32_t cg = cg_begin;
     if (cg < cg_end) load_round(p.coarse_off[cg], p.coarse_off[cg + 1]);
     for (; cg < cg_end; cg++) {
@@ -657,7 +659,6 @@ __global__ __launch_bounds__(1024) void k_fine_scatter(PartArgs p) {
                 const uint32_t q = base[m_f[j]] + m_rank[j];
                 s_l[q] = uint16_t(m_idx[j] & lmask);
                 s_val[q] = m_val[j];
-                s_f[q] = uint8_t(m_f[j]);
                 if (p.rpos) p.rpos[r0 + uint32_t(j) * 1024 + threadIdx.x] = cursor[m_f[j]] + m_rank[j];
             }
             if (r0 + kRound < hi) {
@@ -666,13 +667,15 @@ __global__ __launch_bounds__(1024) void k_fine_scatter(PartArgs p) {
                 load_round(p.coarse_off[cg + 1], p.coarse_off[cg + 2]);
             }
             __syncthreads();
-            const uint32_t total = tot;
-            for (uint32_t q = threadIdx.x; q < total; q += blockDim.x) {
-                const uint32_t f = s_f[q];
-                const uint32_t dst = cursor[f] + q - base[f];
-                p.bin_lidx[dst] = s_l[q];
-                if (p.tmp_val) reinterpret_cast<V*>(p.bin_val)[dst] = s_val[q];
-            }
+            uint16_t* bl = p.bin_lidx - rb;
+            V* bv = reinterpret_cast<V*>(p.bin_val) - rb;
+            if (p.tmp_val)
+                bucket_writeout(hist, base, cursor, nf, [&](uint32_t q, uint32_t dst) {
+                    bl[dst] = s_l[q];
+                    bv[dst] = s_val[q];
+                });
+            else
+                bucket_writeout(hist, base, cursor, nf, [&](uint32_t q, uint32_t dst) { bl[dst] = s_l[q]; });
             __syncthreads();
             for (uint32_t f = threadIdx.x; f < nf; f += blockDim.x) cursor[f] += hist[f];
         }
@@ -745,6 +748,17 @@ struct TileArgs {
     void* results;           // binned order: [r] (un-partitioned by k_unpartition)
     uint8_t* ok;             // binned order
     uint32_t* err;
+    // staged apply: an owner item covers tile t of every region r, records
+    // [rts[r * rstride + t], rts[r * rstride + t + 1]); nreg == 0: the item's own [lo, hi)
+    const uint32_t* rts;
+    uint32_t nreg;
+    uint32_t rstride;
+    // grouped apply: the owner kernel serves items [tile_off, tile_off + grid), the delta
+    // kernel items [*delta_lo, *delta_hi); record r's bin lives at r - *ring_base (results at r)
+    uint32_t tile_off;
+    const uint32_t* ring_base;   // null: 0
+    const uint32_t* delta_lo;    // null: 0
+    const uint32_t* delta_hi;    // null: *delta_count
 };
 
 __host__ __device__ constexpr bool op_combines(int op) {
@@ -800,8 +814,15 @@ __global__ __launch_bounds__(1024, 8) void k_tile_owner(TileArgs a) {
     using W = typename word_of<T>::W;
     extern __shared__ __align__(16) uint8_t lds_raw[];
     W* tile = reinterpret_cast<W*>(lds_raw);
-    const TileItem w = a.items[blockIdx.x];
+    const TileItem w = a.items[blockIdx.x + a.tile_off];
     if (w.mode != 0) return;
+    const uint16_t* bin_lidx = a.bin_lidx;
+    const T* bin_val = reinterpret_cast<const T*>(a.bin_val);
+    if (a.ring_base) {
+        const uint32_t rb = *a.ring_base;
+        bin_lidx -= rb;
+        bin_val -= rb;
+    }
     const int op = OPT >= 0 ? OPT : a.op;
     const T cmp = from_bits<T>(U(a.cmp_bits)), eps = from_bits<T>(U(a.eps_bits));
     const T sv = from_bits<T>(U(a.val_bits));
@@ -827,21 +848,28 @@ __global__ __launch_bounds__(1024, 8) void k_tile_owner(TileArgs a) {
     __syncthreads();
     // kOwnUnroll records per thread per round: all loads issued before the LDS atomics
     constexpr int kOwnUnroll = 4;
-    for (uint32_t r0 = w.lo + threadIdx.x; r0 < w.hi; r0 += kOwnUnroll * 1024u) {
+    const uint32_t nrg = a.nreg ? a.nreg : 1u;
+    for (uint32_t rg = 0; rg < nrg; rg++) {
+    uint32_t lo = w.lo, hi = w.hi;
+    if (a.nreg) {
+        lo = a.rts[uint64_t(rg) * a.rstride + w.tile];
+        hi = a.rts[uint64_t(rg) * a.rstride + w.tile + 1];
+    }
+    for (uint32_t r0 = lo + threadIdx.x; r0 < hi; r0 += kOwnUnroll * 1024u) {
         uint32_t l[kOwnUnroll];
         T v[kOwnUnroll];
 #pragma unroll
         for (int k = 0; k < kOwnUnroll; k++) {
             const uint32_t r = r0 + uint32_t(k) * 1024u;
-            if (r < w.hi) {
-                l[k] = a.bin_lidx[r];
-                v[k] = a.scalar ? sv : reinterpret_cast<const T*>(a.bin_val)[r];
+            if (r < hi) {
+                l[k] = bin_lidx[r];
+                v[k] = a.scalar ? sv : bin_val[r];
             }
         }
 #pragma unroll
         for (int k = 0; k < kOwnUnroll; k++) {
             const uint32_t r = r0 + uint32_t(k) * 1024u;
-            if (r < w.hi) {
+            if (r < hi) {
                 uint8_t ok = 0;
                 T old = rmw_lds<T>(tile + l[k], op, a.kind, v[k], cmp, eps, ok, a.err);
                 if (ret != LMR_RET_NONE) {
@@ -850,6 +878,7 @@ __global__ __launch_bounds__(1024, 8) void k_tile_owner(TileArgs a) {
                 }
             }
         }
+    }
     }
     __syncthreads();
     if (!op_is_read(op)) {
@@ -883,12 +912,20 @@ __global__ __launch_bounds__(1024) void k_tile_delta(TileArgs a) {
     const T cmp = from_bits<T>(U(a.cmp_bits)), eps = from_bits<T>(U(a.eps_bits));
     const T sv = from_bits<T>(U(a.val_bits));
     const int ret = a.ret;
-    const uint32_t nitems = *a.delta_count;
+    const uint32_t it_lo = a.delta_lo ? *a.delta_lo : 0u;
+    const uint32_t nitems = a.delta_hi ? *a.delta_hi : *a.delta_count;
+    const uint16_t* bin_lidx = a.bin_lidx;
+    const T* bin_val = reinterpret_cast<const T*>(a.bin_val);
+    if (a.ring_base) {
+        const uint32_t rb = *a.ring_base;
+        bin_lidx -= rb;
+        bin_val -= rb;
+    }
     const W ident = (op == LMR_OP_AND || op == LMR_OP_FETCH_AND) ? W(~U(0)) : W(0);
     const U ident_bits = (op == LMR_OP_AND || op == LMR_OP_FETCH_AND) ? ~U(0) : U(0);
     const int acc = delta_acc_op(op);
     const int gop = delta_global_op(op);
-    for (uint32_t it = blockIdx.x; it < nitems; it += gridDim.x) {
+    for (uint32_t it = it_lo + blockIdx.x; it < nitems; it += gridDim.x) {
         const TileItem w = a.delta[it];
         const uint64_t base = uint64_t(w.tile) << a.tile_shift;
         const uint32_t len = uint32_t(min(uint64_t(1) << a.tile_shift, a.shard_len - base));
@@ -900,8 +937,8 @@ __global__ __launch_bounds__(1024) void k_tile_delta(TileArgs a) {
         for (int k = 0; k < int(kSplit / 1024); k++) {
             const uint32_t r = w.lo + threadIdx.x + uint32_t(k) * 1024u;
             if (r < w.hi) {
-                const uint32_t l = a.bin_lidx[r];
-                const T v = a.scalar ? sv : reinterpret_cast<const T*>(a.bin_val)[r];
+                const uint32_t l = bin_lidx[r];
+                const T v = a.scalar ? sv : bin_val[r];
                 uint8_t ok = 0;
                 pre[k] = rmw_lds<T>(tile + l, acc, a.kind, v, cmp, eps, ok, a.err);
             }
@@ -927,7 +964,7 @@ __global__ __launch_bounds__(1024) void k_tile_delta(TileArgs a) {
             for (int k = 0; k < int(kSplit / 1024); k++) {
                 const uint32_t r = w.lo + threadIdx.x + uint32_t(k) * 1024u;
                 if (r < w.hi) {
-                    const uint32_t l = a.bin_lidx[r];
+                    const uint32_t l = bin_lidx[r];
                     T b;
                     if constexpr (sizeof(T) >= 4) b = tile[l];
                     else b = T(U(tile[l]));
@@ -1055,6 +1092,8 @@ size_t tiled_ws_bytes(uint64_t cap) {
     b += 2 * al((size_t(kMaxTiles) + 1) * 4) + al(size_t(kMaxTiles) / kScanItems * 4 + 256) + al(4);
     b += al((size_t(kMaxTiles) + 2 * (cap / kSplit) + 2) * 16);   // owner items + delta pieces
     b += 2 * al((cap / 4096 + 2) * size_t(kMaxCoarse) * 2);         // round-major rhist / rbase
+    b += al(size_t(kMaxRegions) * (kMaxTiles + 1) * 4);             // staged regions' tile starts
+    b += al(size_t(kStageInfoWords) * 4);                            // staged piece table / totals
     return b;
 }
 
@@ -1081,7 +1120,9 @@ TiledWs carve_tiled_ws(uint8_t* base, uint64_t cap) {
     w.items = p;                                   // [kMaxTiles] owner items, then delta pieces
     p += al((size_t(kMaxTiles) + 2 * (cap / kSplit) + 2) * 16);
     w.rhist = reinterpret_cast<uint16_t*>(p); p += al((cap / 4096 + 2) * size_t(kMaxCoarse) * 2);
-    w.rbase = reinterpret_cast<uint16_t*>(p);
+    w.rbase = reinterpret_cast<uint16_t*>(p); p += al((cap / 4096 + 2) * size_t(kMaxCoarse) * 2);
+    w.rts = reinterpret_cast<uint32_t*>(p); p += al(size_t(kMaxRegions) * (kMaxTiles + 1) * 4);
+    w.sinfo = reinterpret_cast<uint32_t*>(p);
     return w;
 }
 
@@ -1101,22 +1142,40 @@ static int tile_grid_cap() {
     static int v = env_int("LMR_DELTA_BLOCKS", 1024, 1, 1 << 24);
     return v;
 }
-// records per thread per round of the coarse / fine passes (LMR_COARSE_RPT, LMR_FINE_RPT: 4, 6 or 8)
-static int coarse_rpt() {
-    static int v = env_int("LMR_COARSE_RPT", 4, 4, 8);
-    return v;
+// records per thread per round of the coarse / fine passes (LMR_COARSE_RPT,
+// LMR_FINE_RPT: 4, 6, 8, 12 or 16; capped to what fits the LDS). Bigger rounds
+// amortise the per-round barriers and bucket scan and lengthen the output runs.
+// Measured on one box (tools/r1h_cmd.sh): 8-byte values, coarse 1.71 -> 1.43 ms
+// at 12K-record rounds, fine 1.75 -> 1.60 ms at 8K; 4-byte values (C5) are best
+// at 4K-record rounds.
+static int coarse_rpt(int vb) {
+    static int v = env_int("LMR_COARSE_RPT", 0, 0, 16);
+    return v ? v : (vb == 8 ? 12 : 4);
 }
-static int fine_rpt() {
-    static int v = env_int("LMR_FINE_RPT", 4, 4, 8);
-    return v;
+static int fine_rpt(int vb) {
+    static int v = env_int("LMR_FINE_RPT", 0, 0, 16);
+    return v ? v : (vb == 8 ? 8 : 4);
 }
-template <typename F>
+// f(vb, rpt) with rpt the largest supported value <= the request whose round
+// (rpt * 1024 records of Extra + VB bytes in LDS) fits in 150 KiB
+template <int Extra, typename F>
 static void dispatch_vb_rpt(int vb, int rpt, F&& f) {
     using std::integral_constant;
     auto with_vb = [&](auto vbt) {
-        if (rpt >= 8) f(vbt, integral_constant<int, 8>{});
-        else if (rpt >= 6) f(vbt, integral_constant<int, 6>{});
-        else f(vbt, integral_constant<int, 4>{});
+        constexpr int VB = decltype(vbt)::value;
+        constexpr int kMaxR = (150 * 1024) / ((Extra + VB) * 1024);
+        auto call = [&](auto r) {
+            constexpr int R = decltype(r)::value;
+            if constexpr (R <= kMaxR) f(vbt, r);
+            else if constexpr (kMaxR >= 12) f(vbt, integral_constant<int, 12>{});
+            else if constexpr (kMaxR >= 8) f(vbt, integral_constant<int, 8>{});
+            else f(vbt, integral_constant<int, 4>{});
+        };
+        if (rpt >= 16) call(integral_constant<int, 16>{});
+        else if (rpt >= 12) call(integral_constant<int, 12>{});
+        else if (rpt >= 8) call(integral_constant<int, 8>{});
+        else if (rpt >= 6) call(integral_constant<int, 6>{});
+        else call(integral_constant<int, 4>{});
     };
     switch (vb) {
     case 1: with_vb(integral_constant<int, 1>{}); break;
@@ -1133,6 +1192,20 @@ static bool partition_rm_enabled() {      // read per call: tests switch it with
 static int fine_blocks_cap() {
     static int v = env_int("LMR_FINE_BLOCKS", 512, 1, 1 << 20);
     return v;
+}
+
+// records per fine+apply group (LMR_GROUP_RECORDS; 0 = one fine pass, then one tile
+// sweep); read per call: tests switch it within one process
+static int group_records() {
+    return env_int("LMR_GROUP_RECORDS", 0, 0, 1 << 30);
+}
+static void launch_fine(const PartArgs& q, int vb, hipStream_t s) {
+    const uint64_t nseg = uint64_t(q.cg_hi - q.cg_lo);
+    const unsigned fgrid = unsigned(nseg < uint64_t(fine_blocks_cap()) ? nseg : fine_blocks_cap());
+    dispatch_vb_rpt<2>(vb, fine_rpt(vb), [&](auto vbt, auto rpt) {
+        constexpr int VBc = decltype(vbt)::value, R = decltype(rpt)::value;
+        hipLaunchKernelGGL((k_fine_scatter<VBc, R>), dim3(fgrid ? fgrid : 1u), dim3(1024), 0, s, q);
+    });
 }
 
 // One tiled piece: a.n <= workspace capacity, a.n < 2^32.
@@ -1174,6 +1247,8 @@ hipError_t launch_apply_tiled(int dtype, int index_size, const ApplyArgs& a, con
             b.chunk = ch;
         }
     }
+    PartArgs qf{};            // grouped fine pass (launched per group of coarse buckets below)
+    bool grouped = false;
     if (rm) {
         PartArgs q;
         q.idx = a.idx; q.idx_stride = a.idx_stride; q.val = a.val; q.val_stride = a.val_stride;
@@ -1261,19 +1336,20 @@ hipError_t launch_apply_tiled(int dtype, int index_size, const ApplyArgs& a, con
                 constexpr int VBc = decltype(vbt)::value, R = decltype(rpt)::value;
                 hipLaunchKernelGGL((k_coarse_scatter<IW, VBc, R>), dim3(unsigned(G)), dim3(1024), 0, s, q);
             };
-            dispatch_vb_rpt(vb, coarse_rpt(), go);
+            dispatch_vb_rpt<4>(vb, coarse_rpt(vb), go);
             return hipGetLastError();
         });
         if (a.prof) prof_end(a.prof, LMR_STAGE_BIN_SCATTER, s);
         if (e != hipSuccess) return e;
-        ProfScope pf(a.prof, LMR_STAGE_FINE_SCATTER, s);
-        const uint64_t nseg = uint64_t(q.C) * G;
-        const unsigned fgrid = unsigned(nseg < uint64_t(fine_blocks_cap()) ? nseg : fine_blocks_cap());
-        dispatch_vb_rpt(vb, fine_rpt(), [&](auto vbt, auto rpt) {
-            constexpr int VBc = decltype(vbt)::value, R = decltype(rpt)::value;
-            hipLaunchKernelGGL((k_fine_scatter<VBc, R>), dim3(fgrid), dim3(1024), 0, s, q);
-        });
-        e = hipGetLastError();
+        q.cg_lo = 0; q.cg_hi = q.C * uint32_t(G); q.ring_base = nullptr;
+        if (group_records() > 0 && q.C > 1) {
+            qf = q;
+            grouped = true;
+        } else {
+            ProfScope pf(a.prof, LMR_STAGE_FINE_SCATTER, s);
+            launch_fine(q, vb, s);
+            e = hipGetLastError();
+        }
     } else {
     ProfScope ps(a.prof, LMR_STAGE_BIN_SCATTER, s);
     e = dispatch_iw(index_size, [&](auto iw) {
@@ -1315,22 +1391,55 @@ hipError_t launch_apply_tiled(int dtype, int index_size, const ApplyArgs& a, con
     uint8_t* res_bin = w.tmp_val;
     uint8_t* ok_bin = reinterpret_cast<uint8_t*>(w.tmp_idx);
     t.results = res_bin; t.ok = ok_bin; t.err = a.err;
+    t.rts = nullptr; t.nreg = 0; t.rstride = 0;
+    t.tile_off = 0; t.ring_base = nullptr; t.delta_lo = nullptr; t.delta_hi = nullptr;
     const size_t tile_lds = size_t(kTileBytes);
     const bool delta = op_combines(a.op) && a.n > thresh;
     const unsigned dgrid = unsigned(std::min<uint64_t>(2 * ((a.n + kSplit - 1) / kSplit), uint64_t(tile_grid_cap())));
-    e = dispatch_dtype(dtype, [&](auto tag) {
-        using T = decltype(tag);
-        auto go = [&](auto opt) {
-            constexpr int OPT = decltype(opt)::value;
-            hipLaunchKernelGGL((k_tile_owner<T, OPT>), dim3(unsigned(num_tiles)), dim3(1024), tile_lds, s, t);
-            if (delta) hipLaunchKernelGGL((k_tile_delta<T, OPT>), dim3(dgrid), dim3(1024), tile_lds, s, t);
-        };
-        if (a.op == LMR_OP_ADD) go(std::integral_constant<int, LMR_OP_ADD>{});
-        else if (a.op == LMR_OP_FETCH_ADD) go(std::integral_constant<int, LMR_OP_FETCH_ADD>{});
-        else go(std::integral_constant<int, -1>{});
-        return hipGetLastError();
-    });
-    ps.end();
+    auto apply_tiles = [&](unsigned ntiles) {
+        return dispatch_dtype(dtype, [&](auto tag) {
+            using T = decltype(tag);
+            auto go = [&](auto opt) {
+                constexpr int OPT = decltype(opt)::value;
+                hipLaunchKernelGGL((k_tile_owner<T, OPT>), dim3(ntiles), dim3(1024), tile_lds, s, t);
+                if (delta) hipLaunchKernelGGL((k_tile_delta<T, OPT>), dim3(dgrid), dim3(1024), tile_lds, s, t);
+            };
+            if (a.op == LMR_OP_ADD) go(std::integral_constant<int, LMR_OP_ADD>{});
+            else if (a.op == LMR_OP_FETCH_ADD) go(std::integral_constant<int, LMR_OP_FETCH_ADD>{});
+            else go(std::integral_constant<int, -1>{});
+            return hipGetLastError();
+        });
+    };
+    if (!grouped) {
+        e = apply_tiles(unsigned(num_tiles));
+        ps.end();
+    } else {
+        // Fine pass and tile apply per group of coarse buckets: a group's bins are
+        // written at the start of the bin buffer and read back by its tile apply at
+        // once, so that round trip stays in the 256 MiB Infinity Cache instead of HBM
+        // (tools/mallbench: write+read of a <= 256 MB ring at 6.3-6.9 TB/s vs 4.8 TB/s).
+        ps.end();
+        const uint32_t C = qf.C;
+        const uint64_t per_bucket = (a.n + C - 1) / C;
+        uint32_t gb = uint32_t(std::max<uint64_t>(1, uint64_t(group_records()) / std::max<uint64_t>(per_bucket, 1)));
+        if (gb > C) gb = C;
+        for (uint32_t c0 = 0; c0 < C && e == hipSuccess; c0 += gb) {
+            const uint32_t c1 = std::min(C, c0 + gb);
+            const uint32_t t0 = c0 * kFine, t1 = std::min(uint32_t(num_tiles), c1 * kFine);
+            {
+                ProfScope pf(a.prof, LMR_STAGE_FINE_SCATTER, s);
+                PartArgs qg = qf;
+                qg.cg_lo = c0 * qf.G; qg.cg_hi = c1 * qf.G; qg.ring_base = w.tile_start + t0;
+                launch_fine(qg, vb, s);
+            }
+            ProfScope pt(a.prof, LMR_STAGE_TILE_APPLY, s);
+            t.tile_off = t0;
+            t.ring_base = w.tile_start + t0;
+            t.delta_lo = w.tile_items2 + t0;                              // exclusive scan of delta pieces
+            t.delta_hi = (t1 < uint32_t(num_tiles)) ? w.tile_items2 + t1 : w.item_count;
+            e = apply_tiles(t1 - t0);
+        }
+    }
     if (e != hipSuccess || !has_res) return e;
     // un-partition: binned -> (temp ->) input order, each a block-contiguous gather
     ProfScope pu(a.prof, LMR_STAGE_UNPARTITION, s);
@@ -1355,6 +1464,423 @@ hipError_t launch_apply_tiled(int dtype, int index_size, const ApplyArgs& a, con
         gather(w.rpos, nullptr, nullptr, res_bin, reinterpret_cast<uint8_t*>(a.results), ok_src, a.ok);
     }
     return hipGetLastError();
+}
+
+// ============================================================ staged apply
+// The owner side of the multi-PE exchange. A batch reaches its owner PE in
+// chunks (one RCCL all-to-all-v per chunk, engine._distributed), as the
+// reference's op AMs reach it one buffer at a time and are applied on arrival
+// (registered_active_message.rs:443-497 -> impl/src/array_ops.rs:863-1408).
+// Applying every chunk on arrival would sweep the whole shard once per chunk;
+// instead each arriving record stream (a *region*) is partitioned into 64 KiB
+// shard tiles on arrival, inside its own slice of the workspace, and one tile
+// sweep at the end applies every region:
+//   per region : k_ccount (coarse histogram per producer block) -> scan
+//                -> k_coarse_scatter (shared with the one-shot path)
+//                -> k_piece_table -> k_piece_count -> scan -> k_region_starts
+//                -> k_fine_piece                 (region now tile-sorted)
+//   finish     : k_stage_plan_count / _fill -> k_tile_owner over every region's
+//                range of its tile (+ k_tile_delta for hot tiles)
+//                -> k_unpartition x 2 per region (results back to arrival order)
+// The fine level works on fixed pieces of kPiece records of each coarse bucket
+// (not on per-producer-block segments as k_fine_scatter does), so its LDS rounds
+// stay full and its output runs long whatever the region size: a 2^25-record
+// chunk partitions as efficiently as a 2^28-record batch.
+constexpr uint32_t kPiece = 16384;               // records per fine-level piece (4 LDS rounds)
+constexpr int kStagePbase = 0;                   // sinfo words: pbase[kMaxCoarse + 1]
+constexpr int kStageBstart = 160;                //              bstart[kMaxCoarse + 1]
+constexpr int kStageInb = 320;                   //              in-bounds records per region
+static_assert(kStageInb + kMaxRegions <= kStageInfoWords, "staged scratch");
+
+// per-(coarse bucket, producer block) record counts: coarse_off[c * G + g]
+template <int IW>
+__global__ __launch_bounds__(1024) void k_ccount(PartArgs p) {
+    __shared__ uint32_t hist[kMaxCoarse];
+    for (uint32_t c = threadIdx.x; c < p.C; c += blockDim.x) hist[c] = 0;
+    __syncthreads();
+    const uint64_t lo = uint64_t(blockIdx.x) * p.chunk;
+    const uint64_t hi = min(lo + p.chunk, p.n);
+    const int cshift = p.tile_shift + kFineShift;
+    bool oob = false;
+    constexpr int U = 4;
+    for (uint64_t k0 = lo + threadIdx.x; k0 < hi; k0 += U * uint64_t(blockDim.x)) {
+        uint64_t ix[U];
+#pragma unroll
+        for (int j = 0; j < U; j++) {
+            const uint64_t k = k0 + uint64_t(j) * blockDim.x;
+            ix[j] = k < hi ? load_idx<IW>(p.idx, p.idx_stride, k) : ~uint64_t(0);
+        }
+#pragma unroll
+        for (int j = 0; j < U; j++) {
+            const uint64_t k = k0 + uint64_t(j) * blockDim.x;
+            if (k >= hi) continue;
+            if (ix[j] >= p.shard_len) { oob = true; continue; }
+            atomicAdd(&hist[uint32_t(ix[j] >> cshift)], 1u);
+        }
+    }
+    if (oob) raise_err(p.err, LMR_ERRBIT_OOB);
+    __syncthreads();
+    for (uint32_t c = threadIdx.x; c < p.C; c += blockDim.x)
+        p.coarse_off[uint64_t(c) * p.G + blockIdx.x] = hist[c];
+}
+
+struct PieceArgs {
+    const uint32_t* tmp_idx;    // the region's temp records (region-relative slots)
+    const uint8_t* tmp_val;     // null: every record carries scalar_bits
+    uint64_t scalar_bits;
+    int tile_shift;
+    uint32_t num_tiles;
+    uint32_t C;
+    const uint32_t* pbase;      // [C + 1] first piece of bucket c; pbase[C] = pieces
+    const uint32_t* bstart;     // [C + 1] first temp slot of bucket c; bstart[C] = in-bounds records
+    uint32_t* cnt;              // (c, f, p) tile counts at pbase[c]*kFine + f*np_c + p, then their scan
+    uint16_t* bin_lidx;         // workspace bases (binned positions are absolute)
+    uint8_t* bin_val;
+    uint32_t* rpos;             // region temp slot -> binned position (null: nothing returned)
+    uint32_t R;                 // the region's first workspace slot
+};
+
+// bucket sizes -> pieces of kPiece records; one block of 128 threads (C <= 128)
+__global__ __launch_bounds__(128) void k_piece_table(const uint32_t* coarse_off, uint32_t C, uint32_t G,
+                                                     const uint32_t* inb, uint32_t* pbase, uint32_t* bstart) {
+    __shared__ uint32_t np_s[kMaxCoarse], pb_s[kMaxCoarse], tot;
+    const uint32_t c = threadIdx.x;
+    const uint32_t total = *inb;
+    if (c < C) {
+        const uint32_t s = coarse_off[uint64_t(c) * G];
+        const uint32_t e = (c + 1 < C) ? coarse_off[uint64_t(c + 1) * G] : total;
+        bstart[c] = s;
+        np_s[c] = (e - s + kPiece - 1) / kPiece;
+    }
+    __syncthreads();
+    small_excl_scan(np_s, pb_s, C, &tot);
+    __syncthreads();
+    if (c < C) pbase[c] = pb_s[c];
+    if (c == 0) {
+        pbase[C] = tot;
+        bstart[C] = total;
+    }
+}
+
+struct PieceLoc { uint32_t c, p, np, lo, hi; };
+
+// piece pid -> its bucket (the largest c with pbase[c] <= pid) and record range
+__device__ __forceinline__ PieceLoc piece_loc(const PieceArgs& a, uint32_t pid) {
+    uint32_t lo_c = 0, hi_c = a.C;
+    while (hi_c - lo_c > 1) {
+        const uint32_t m = (lo_c + hi_c) >> 1;
+        if (a.pbase[m] <= pid) lo_c = m; else hi_c = m;
+    }
+    PieceLoc L;
+    L.c = lo_c;
+    L.p = pid - a.pbase[lo_c];
+    L.np = a.pbase[lo_c + 1] - a.pbase[lo_c];
+    L.lo = a.bstart[lo_c] + L.p * kPiece;
+    L.hi = min(L.lo + kPiece, a.bstart[lo_c + 1]);
+    return L;
+}
+
+// per-piece tile histogram (one block per piece; grid = upper bound of pieces)
+__global__ __launch_bounds__(1024) void k_piece_count(PieceArgs a) {
+    __shared__ uint32_t hist[kFine];
+    const uint32_t pid = blockIdx.x;
+    if (pid >= a.pbase[a.C]) return;
+    const PieceLoc L = piece_loc(a, pid);
+    const uint32_t t0 = L.c * kFine;
+    if (threadIdx.x < kFine) hist[threadIdx.x] = 0;
+    __syncthreads();
+    constexpr int U = 4;
+    for (uint32_t k0 = L.lo + threadIdx.x; k0 < L.hi; k0 += U * 1024u) {
+        uint32_t ix[U];
+#pragma unroll
+        for (int j = 0; j < U; j++) {
+            const uint32_t k = k0 + uint32_t(j) * 1024u;
+            ix[j] = k < L.hi ? a.tmp_idx[k] : 0u;
+        }
+#pragma unroll
+        for (int j = 0; j < U; j++)
+            if (k0 + uint32_t(j) * 1024u < L.hi) atomicAdd(&hist[(ix[j] >> a.tile_shift) - t0], 1u);
+    }
+    __syncthreads();
+    const uint32_t nf = min(uint32_t(kFine), a.num_tiles - t0);
+    if (threadIdx.x < nf)
+        a.cnt[uint64_t(a.pbase[L.c]) * kFine + uint64_t(threadIdx.x) * L.np + L.p] = hist[threadIdx.x];
+}
+
+// the region's tile starts (absolute binned positions) from the scanned piece counts
+__global__ void k_region_starts(PieceArgs a, uint32_t* ts) {
+    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t > a.num_tiles) return;
+    const uint32_t inb = a.bstart[a.C];
+    if (t == a.num_tiles) {
+        ts[t] = a.R + inb;
+        return;
+    }
+    const uint32_t c = t >> kFineShift, f = t & (kFine - 1);
+    const uint32_t np = a.pbase[c + 1] - a.pbase[c];
+    const uint64_t e = uint64_t(a.pbase[c]) * kFine + uint64_t(f) * np;
+    ts[t] = a.R + (e < uint64_t(a.pbase[a.C]) * kFine ? a.cnt[e] : inb);
+}
+
+// fine level: each piece counting-sorted by tile in LDS rounds, written at its
+// final binned positions (persistent over pieces)
+template <int VB, int RPT>
+__global__ __launch_bounds__(1024) void k_fine_piece(PieceArgs a) {
+    using V = typename idx_t<VB>::I;
+    constexpr uint32_t kRound = RPT * 1024;
+    __shared__ uint32_t hist[kFine], base[kFine], cursor[kFine], tot;
+    __shared__ uint16_t s_l[kRound];
+    __shared__ V s_val[kRound];
+    const uint32_t npieces = a.pbase[a.C];
+    const uint32_t lmask = (1u << a.tile_shift) - 1u;
+    const V sv = V(a.scalar_bits);
+    for (uint32_t pid = blockIdx.x; pid < npieces; pid += gridDim.x) {
+        const PieceLoc L = piece_loc(a, pid);
+        const uint32_t t0 = L.c * kFine;
+        const uint32_t nf = min(uint32_t(kFine), a.num_tiles - t0);
+        const uint32_t* cb = a.cnt + uint64_t(a.pbase[L.c]) * kFine + L.p;
+        for (uint32_t f = threadIdx.x; f < nf; f += blockDim.x) cursor[f] = a.R + cb[uint64_t(f) * L.np];
+        for (uint32_t r0 = L.lo; r0 < L.hi; r0 += kRound) {
+            for (uint32_t f = threadIdx.x; f < nf; f += blockDim.x) hist[f] = 0;
+            uint32_t m_idx[RPT];
+            V m_val[RPT];
+#pragma unroll
+            for (int j = 0; j < RPT; j++) {
+                const uint32_t k = r0 + uint32_t(j) * 1024 + threadIdx.x;
+                const bool in = k < L.hi;
+                m_idx[j] = in ? a.tmp_idx[k] : 0u;
+                m_val[j] = in ? (a.tmp_val ? reinterpret_cast<const V*>(a.tmp_val)[k] : sv) : V(0);
+            }
+            __syncthreads();
+            uint32_t m_rank[RPT], m_f[RPT];
+#pragma unroll
+            for (int j = 0; j < RPT; j++) {
+                m_f[j] = (m_idx[j] >> a.tile_shift) - t0;
+                if (r0 + uint32_t(j) * 1024 + threadIdx.x < L.hi) m_rank[j] = atomicAdd(&hist[m_f[j]], 1u);
+            }
+            __syncthreads();
+            small_excl_scan(hist, base, nf, &tot);
+            __syncthreads();
+#pragma unroll
+            for (int j = 0; j < RPT; j++) {
+                const uint32_t k = r0 + uint32_t(j) * 1024 + threadIdx.x;
+                if (k >= L.hi) continue;
+                const uint32_t q = base[m_f[j]] + m_rank[j];
+                s_l[q] = uint16_t(m_idx[j] & lmask);
+                s_val[q] = m_val[j];
+                if (a.rpos) a.rpos[k] = cursor[m_f[j]] + m_rank[j];
+            }
+            __syncthreads();
+            bucket_writeout(hist, base, cursor, nf, [&](uint32_t q, uint32_t dst) {
+                a.bin_lidx[dst] = s_l[q];
+                reinterpret_cast<V*>(a.bin_val)[dst] = s_val[q];
+            });
+            __syncthreads();
+            for (uint32_t f = threadIdx.x; f < nf; f += blockDim.x) cursor[f] += hist[f];
+        }
+        __syncthreads();
+    }
+}
+
+// work plan over all regions: owner item per touched tile; a hot tile of a
+// combinable op becomes delta pieces of <= kSplit records over each region's range
+__global__ void k_stage_plan_count(const uint32_t* rts, uint32_t nreg, uint32_t stride, uint32_t num_tiles,
+                                   uint32_t thresh, int combinable, uint32_t* tile_items) {
+    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= num_tiles) return;
+    uint32_t tot = 0, pieces = 0;
+    for (uint32_t r = 0; r < nreg; r++) {
+        const uint32_t c = rts[uint64_t(r) * stride + t + 1] - rts[uint64_t(r) * stride + t];
+        tot += c;
+        pieces += (c + kSplit - 1) / kSplit;
+    }
+    tile_items[t] = (tot == 0) ? 0u : ((combinable && tot > thresh && pieces > 1) ? pieces : 1u);
+}
+
+__global__ void k_stage_plan_fill(const uint32_t* rts, uint32_t nreg, uint32_t stride, uint32_t num_tiles,
+                                  const uint32_t* delta_base, const uint32_t* tile_items, TileItem* items,
+                                  TileItem* delta) {
+    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= num_tiles) return;
+    const uint32_t m = tile_items[t];
+    items[t] = TileItem{t, 0u, 0u, m == 1 ? 0u : 2u};
+    if (m <= 1) return;
+    uint32_t j = delta_base[t];
+    for (uint32_t r = 0; r < nreg; r++) {
+        const uint32_t lo = rts[uint64_t(r) * stride + t], hi = rts[uint64_t(r) * stride + t + 1];
+        for (uint32_t l = lo; l < hi; l += kSplit) delta[j++] = TileItem{t, l, min(hi, l + kSplit), 1u};
+    }
+}
+
+hipError_t launch_stage_region(int dtype, int index_size, const ApplyArgs& a, const TiledWs& w,
+                               StageSession& s, hipStream_t st) {
+    if (a.n == 0) return hipSuccess;
+    const int shift = tile_shift_for(dtype);
+    const uint64_t num_tiles = (a.shard_len + (uint64_t(1) << shift) - 1) >> shift;
+    if (num_tiles == 0 || num_tiles > uint64_t(kMaxTiles) || a.n > kStageMaxRegion || s.nreg >= kMaxRegions)
+        return hipErrorInvalidValue;
+    const uint32_t T = uint32_t(num_tiles);
+    const uint32_t C = uint32_t((num_tiles + kFine - 1) / kFine);
+    const int vb = dtype_bytes(dtype);
+    const int r = s.nreg;
+    const uint32_t R = uint32_t(s.staged);
+    const bool has_res = s.a.ret != LMR_RET_NONE;
+    uint64_t G = (a.n + 65535) / 65536;
+    if (G > uint64_t(bin_blocks_cap())) G = bin_blocks_cap();
+    if (G < 1) G = 1;
+    uint32_t* pbase = w.sinfo + kStagePbase;
+    uint32_t* bstart = w.sinfo + kStageBstart;
+    uint32_t* inb = w.sinfo + kStageInb + r;
+    PartArgs q{};
+    q.idx = a.idx; q.idx_stride = a.idx_stride; q.val = a.val; q.val_stride = a.val_stride;
+    q.n = a.n; q.shard_len = a.shard_len; q.chunk = (a.n + G - 1) / G; q.tile_shift = shift;
+    q.num_tiles = T; q.G = uint32_t(G); q.C = C;
+    q.coarse_off = w.coarse_off;
+    q.tmp_idx = w.tmp_idx + R;
+    q.tmp_val = a.val ? w.tmp_val + uint64_t(R) * vb : nullptr;
+    q.qpos = has_res ? w.qpos + R : nullptr;
+    q.err = a.err;
+    hipError_t e;
+    {
+        ProfScope ps(a.prof, LMR_STAGE_BIN_COUNT, st);
+        e = dispatch_iw(index_size, [&](auto iw) {
+            hipLaunchKernelGGL((k_ccount<decltype(iw)::value>), dim3(unsigned(G)), dim3(1024), 0, st, q);
+            return hipGetLastError();
+        });
+    }
+    if (e != hipSuccess) return e;
+    {
+        ProfScope ps(a.prof, LMR_STAGE_SCAN, st);
+        e = scan_exclusive_u32(w.coarse_off, uint64_t(C) * G, w.partials, inb, st);
+    }
+    if (e != hipSuccess) return e;
+    {
+        ProfScope ps(a.prof, LMR_STAGE_BIN_SCATTER, st);
+        e = dispatch_iw(index_size, [&](auto iw) {
+            constexpr int IW = decltype(iw)::value;
+            dispatch_vb_rpt<4>(vb, coarse_rpt(vb), [&](auto vbt, auto rpt) {
+                constexpr int VBc = decltype(vbt)::value, RP = decltype(rpt)::value;
+                hipLaunchKernelGGL((k_coarse_scatter<IW, VBc, RP>), dim3(unsigned(G)), dim3(1024), 0, st, q);
+            });
+            return hipGetLastError();
+        });
+    }
+    if (e != hipSuccess) return e;
+    PieceArgs pa;
+    pa.tmp_idx = q.tmp_idx; pa.tmp_val = q.tmp_val; pa.scalar_bits = a.val_bits;
+    pa.tile_shift = shift; pa.num_tiles = T; pa.C = C; pa.pbase = pbase; pa.bstart = bstart;
+    pa.cnt = w.counts; pa.bin_lidx = w.bin_lidx; pa.bin_val = w.bin_val;
+    pa.rpos = has_res ? w.rpos + R : nullptr; pa.R = R;
+    const uint64_t max_pieces = (a.n + kPiece - 1) / kPiece + C;
+    {
+        ProfScope ps(a.prof, LMR_STAGE_FINE_SCATTER, st);
+        hipLaunchKernelGGL(k_piece_table, dim3(1), dim3(128), 0, st, w.coarse_off, C, uint32_t(G), inb, pbase, bstart);
+        e = hipMemsetAsync(w.counts, 0, size_t(max_pieces) * kFine * 4, st);
+        if (e != hipSuccess) return e;
+        hipLaunchKernelGGL(k_piece_count, dim3(unsigned(max_pieces)), dim3(1024), 0, st, pa);
+        e = scan_exclusive_u32(w.counts, max_pieces * kFine, w.partials, nullptr, st);
+        if (e != hipSuccess) return e;
+        hipLaunchKernelGGL(k_region_starts, dim3((T + 1 + 255) / 256), dim3(256), 0, st, pa,
+                           w.rts + uint64_t(r) * (kMaxTiles + 1));
+        const unsigned fgrid = unsigned(std::min<uint64_t>(max_pieces, uint64_t(fine_blocks_cap())));
+        dispatch_vb_rpt<2>(vb, fine_rpt(vb), [&](auto vbt, auto rpt) {
+            constexpr int VBc = decltype(vbt)::value, RP = decltype(rpt)::value;
+            hipLaunchKernelGGL((k_fine_piece<VBc, RP>), dim3(fgrid), dim3(1024), 0, st, pa);
+        });
+        e = hipGetLastError();
+    }
+    if (e != hipSuccess) return e;
+    s.reg[r] = StageRegion{uint64_t(R), a.n, a.results, a.ok};
+    s.nreg = r + 1;
+    s.staged += a.n;
+    return hipSuccess;
+}
+
+hipError_t launch_stage_finish(const TiledWs& w, StageSession& s, hipStream_t st) {
+    if (s.nreg == 0) return hipSuccess;
+    const ApplyArgs& a = s.a;
+    const int dtype = s.dtype;
+    const int shift = tile_shift_for(dtype);
+    const uint32_t T = uint32_t((a.shard_len + (uint64_t(1) << shift) - 1) >> shift);
+    const int vb = dtype_bytes(dtype);
+    const uint32_t stride = uint32_t(kMaxTiles + 1);
+    const bool has_res = a.ret != LMR_RET_NONE;
+    uint8_t* res_bin = w.tmp_val;                                 // temps are free after the fine passes
+    uint8_t* ok_bin = reinterpret_cast<uint8_t*>(w.tmp_idx);
+    hipError_t e;
+    {
+        ProfScope ps(a.prof, LMR_STAGE_TILE_APPLY, st);
+        const uint64_t avg = (s.staged + T - 1) / T;
+        const uint32_t thresh = uint32_t(std::min<uint64_t>(0xFFFFFFFFull, std::max<uint64_t>(4 * avg, 65536)));
+        const unsigned pg = unsigned((T + 255) / 256);
+        hipLaunchKernelGGL(k_stage_plan_count, dim3(pg), dim3(256), 0, st, w.rts, uint32_t(s.nreg), stride, T,
+                           thresh, op_combines(a.op) ? 1 : 0, w.tile_items);
+        hipLaunchKernelGGL(k_tile_plan_extra, dim3(pg), dim3(256), 0, st, w.tile_items, T, w.tile_items2);
+        e = scan_exclusive_u32(w.tile_items2, T, w.plan_partials, w.item_count, st);
+        if (e != hipSuccess) return e;
+        TileItem* items = reinterpret_cast<TileItem*>(w.items);
+        hipLaunchKernelGGL(k_stage_plan_fill, dim3(pg), dim3(256), 0, st, w.rts, uint32_t(s.nreg), stride, T,
+                           w.tile_items2, w.tile_items, items, items + kMaxTiles);
+        TileArgs t;
+        t.shard = a.shard; t.shard_len = a.shard_len; t.tile_shift = shift;
+        t.kind = a.kind; t.op = a.op; t.ret = a.ret;
+        t.cmp_bits = a.cmp_bits; t.eps_bits = a.eps_bits; t.val_bits = 0;
+        t.scalar = false;                                         // values are materialised in the bins
+        t.items = items; t.delta = items + kMaxTiles; t.delta_count = w.item_count;
+        t.num_tiles = T;
+        t.bin_lidx = w.bin_lidx; t.bin_val = w.bin_val;
+        t.results = res_bin; t.ok = ok_bin; t.err = a.err;
+        t.rts = w.rts; t.nreg = uint32_t(s.nreg); t.rstride = stride;
+        t.tile_off = 0; t.ring_base = nullptr; t.delta_lo = nullptr; t.delta_hi = nullptr;
+        const bool delta = op_combines(a.op) && s.staged > thresh;
+        const unsigned dgrid = unsigned(std::min<uint64_t>(2 * ((s.staged + kSplit - 1) / kSplit) + 2 * uint64_t(s.nreg),
+                                                           uint64_t(tile_grid_cap())));
+        e = dispatch_dtype(dtype, [&](auto tag) {
+            using Ty = decltype(tag);
+            auto go = [&](auto opt) {
+                constexpr int OPT = decltype(opt)::value;
+                hipLaunchKernelGGL((k_tile_owner<Ty, OPT>), dim3(T), dim3(1024), size_t(kTileBytes), st, t);
+                if (delta) hipLaunchKernelGGL((k_tile_delta<Ty, OPT>), dim3(dgrid), dim3(1024), size_t(kTileBytes), st, t);
+            };
+            if (a.op == LMR_OP_ADD) go(std::integral_constant<int, LMR_OP_ADD>{});
+            else if (a.op == LMR_OP_FETCH_ADD) go(std::integral_constant<int, LMR_OP_FETCH_ADD>{});
+            else go(std::integral_constant<int, -1>{});
+            return hipGetLastError();
+        });
+    }
+    if (e == hipSuccess && has_res) {
+        // binned -> temp slot (in-bounds slots of each region) -> arrival order
+        ProfScope pu(a.prof, LMR_STAGE_UNPARTITION, st);
+        uint8_t* tmpres = w.bin_val;                              // bins are free after the tile sweep
+        uint8_t* ok_tmp = (a.ret == LMR_RET_RESULT) ? reinterpret_cast<uint8_t*>(w.bin_lidx) : nullptr;
+        const uint8_t* ok_src = (a.ret == LMR_RET_RESULT) ? ok_bin : nullptr;
+        auto gather = [&](const uint32_t* map, uint64_t n, const uint32_t* n_dev, const uint8_t* src, uint8_t* dst,
+                          const uint8_t* oks, uint8_t* okd) {
+            uint64_t Gu = (n + 65535) / 65536;
+            if (Gu > 1024) Gu = 1024;
+            if (Gu < 1) Gu = 1;
+            const uint64_t chunk = (n + Gu - 1) / Gu;
+            switch (vb) {
+            case 1: hipLaunchKernelGGL((k_unpartition<1>), dim3(unsigned(Gu)), dim3(1024), 0, st, map, n, n_dev, nullptr, chunk, src, dst, oks, okd); break;
+            case 2: hipLaunchKernelGGL((k_unpartition<2>), dim3(unsigned(Gu)), dim3(1024), 0, st, map, n, n_dev, nullptr, chunk, src, dst, oks, okd); break;
+            case 4: hipLaunchKernelGGL((k_unpartition<4>), dim3(unsigned(Gu)), dim3(1024), 0, st, map, n, n_dev, nullptr, chunk, src, dst, oks, okd); break;
+            default: hipLaunchKernelGGL((k_unpartition<8>), dim3(unsigned(Gu)), dim3(1024), 0, st, map, n, n_dev, nullptr, chunk, src, dst, oks, okd); break;
+            }
+        };
+        for (int r = 0; r < s.nreg; r++) {
+            const StageRegion& g = s.reg[r];
+            if (!g.results) continue;
+            gather(w.rpos + g.base, g.n, w.sinfo + kStageInb + r, res_bin, tmpres + g.base * vb, ok_src,
+                   ok_tmp ? ok_tmp + g.base : nullptr);
+            const bool want_ok = ok_tmp && g.ok;
+            gather(w.qpos + g.base, g.n, nullptr, tmpres + g.base * vb, reinterpret_cast<uint8_t*>(g.results),
+                   want_ok ? ok_tmp + g.base : nullptr, want_ok ? g.ok : nullptr);
+        }
+        e = hipGetLastError();
+    }
+    s.nreg = 0;
+    s.staged = 0;
+    return e;
 }
 
 }  // namespace lmr

@@ -38,6 +38,14 @@ void prof_end(Prof* p, int st, hipStream_t s) {
     if (e && p->open_ev[st] && hipEventRecord(e, s) == hipSuccess)
         p->pending.push_back({st, p->open_ev[st], e});
 }
+
+// Staged-apply session of a context (lmr_stage_begin / _soa / _finish).
+struct StageState {
+    bool open = false;
+    lmr_apply_desc_t desc{};
+    StageSession s;
+};
+void stage_state_free(StageState* s) { delete s; }
 }  // namespace lmr
 
 using namespace lmr;
@@ -161,6 +169,45 @@ uint64_t load_scalar_bits(const void* val, int dtype) {
     return b;
 }
 
+// Stage the records of `a` as one or more regions (workspace-sized pieces),
+// applying what is staged first whenever the workspace or the region table is full.
+hipError_t stage_records(lmr_ctx* ctx, StageSession& ss, const ApplyArgs& a, int dtype, int iw, uint64_t split,
+                         hipStream_t s) {
+    TiledWs w = carve_tiled_ws(ctx->ws, ctx->rec_cap);
+    const int eb = dtype_bytes(dtype);
+    uint64_t piece = ctx->rec_cap < kStageMaxRegion ? ctx->rec_cap : kStageMaxRegion;
+    if (split > 1) {
+        const uint64_t per = (a.n + split - 1) / split;
+        if (per < piece) piece = per;
+    }
+    for (uint64_t p0 = 0; p0 < a.n; p0 += piece) {
+        const uint64_t m = a.n - p0 < piece ? a.n - p0 : piece;
+        if (ss.staged + m > ctx->rec_cap || ss.nreg == kMaxRegions) {
+            hipError_t e = launch_stage_finish(w, ss, s);
+            if (e != hipSuccess) return e;
+        }
+        ApplyArgs b = a;
+        b.n = m;
+        b.idx = a.idx + p0 * a.idx_stride;
+        if (a.val) b.val = a.val + p0 * a.val_stride;
+        if (a.results) b.results = reinterpret_cast<uint8_t*>(a.results) + p0 * uint64_t(eb);
+        if (a.ok) b.ok = a.ok + p0;
+        hipError_t e = launch_stage_region(dtype, iw, b, w, ss, s);
+        if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
+}
+
+// LMR_STAGED=1 routes the one-shot tiled path through the staged pipeline
+// (LMR_STAGE_SPLIT=k: k regions per call); read per call, tests switch it.
+uint64_t staged_mode_split() {
+    const char* e = getenv("LMR_STAGED");
+    if (!e || e[0] != '1') return 0;
+    const char* k = getenv("LMR_STAGE_SPLIT");
+    const long v = (k && *k) ? atol(k) : 1;
+    return v < 1 ? 1 : uint64_t(v);
+}
+
 // Run a record stream with the chosen strategy, in workspace-sized pieces.
 lmr_status_t run_apply(lmr_ctx* ctx, const lmr_apply_desc_t* d, ApplyArgs a, int iw,
                        hipStream_t s) {
@@ -175,6 +222,14 @@ lmr_status_t run_apply(lmr_ctx* ctx, const lmr_apply_desc_t* d, ApplyArgs a, int
                 tiled_supported(int(d->dtype), d->shard_len);
     }
     if (!tiled) return hip_status(launch_apply_direct(int(d->dtype), iw, a, s));
+    if (const uint64_t split = staged_mode_split()) {
+        StageSession ss;
+        ss.a = a;
+        ss.dtype = int(d->dtype);
+        hipError_t e = stage_records(ctx, ss, a, int(d->dtype), iw, split, s);
+        if (e == hipSuccess) e = launch_stage_finish(carve_tiled_ws(ctx->ws, ctx->rec_cap), ss, s);
+        return hip_status(e);
+    }
     TiledWs w = carve_tiled_ws(ctx->ws, ctx->rec_cap);
     const uint64_t n = a.n;
     for (uint64_t p0 = 0; p0 < n; p0 += ctx->rec_cap) {
@@ -232,6 +287,7 @@ lmr_status_t lmr_ctx_destroy(lmr_ctx_t* ctx) {
     if (!ctx) return LMR_E_INVALID;
     (void)hipSetDevice(ctx->device);
     host_stage_free(ctx->host);
+    stage_state_free(ctx->stage);
     if (ctx->ws) (void)hipFree(ctx->ws);
     if (ctx->d_err) (void)hipFree(ctx->d_err);
     if (ctx->prof) {
@@ -245,6 +301,7 @@ lmr_status_t lmr_ctx_destroy(lmr_ctx_t* ctx) {
 lmr_status_t lmr_ctx_reserve(lmr_ctx_t* ctx, uint64_t max_records) {
     if (!ctx) return LMR_E_INVALID;
     if (max_records > 0xFFFFFFFFull) max_records = 0xFFFFFFFFull;
+    if (ctx->stage && ctx->stage->s.nreg > 0) return LMR_E_INVALID;   // staged records live in the workspace
     (void)hipSetDevice(ctx->device);
     if (ctx->ws) { (void)hipFree(ctx->ws); ctx->ws = nullptr; ctx->ws_bytes = 0; ctx->rec_cap = 0; }
     if (max_records == 0) return LMR_OK;
@@ -544,6 +601,56 @@ lmr_status_t lmr_apply_soa(lmr_ctx_t* ctx, const lmr_apply_desc_t* desc, const v
     a.val_bits = d_vals ? 0 : load_scalar_bits(val, int(desc->dtype));
     a.n = n;
     return run_apply(ctx, desc, a, int(index_size), reinterpret_cast<hipStream_t>(stream));
+}
+
+// ---------------------------------------------------------------- staged apply
+lmr_status_t lmr_stage_begin(lmr_ctx_t* ctx, const lmr_apply_desc_t* desc) {
+    if (!ctx) return LMR_E_INVALID;
+    lmr_status_t st = check_desc(desc);
+    if (st != LMR_OK) return st;
+    if (!desc->shard) return LMR_E_INVALID;
+    if (!ctx->stage) ctx->stage = new StageState();
+    StageState* S = ctx->stage;
+    if (S->s.nreg > 0) return LMR_E_INVALID;          // the previous session was never finished
+    S->open = true;
+    S->desc = *desc;
+    S->s = StageSession();
+    S->s.a = base_args(ctx, desc, nullptr, nullptr);
+    S->s.a.ret = int(lmr_op_ret_kind(desc->op));     // keep the result maps for every returning op
+    S->s.dtype = int(desc->dtype);
+    return LMR_OK;
+}
+
+lmr_status_t lmr_stage_soa(lmr_ctx_t* ctx, const void* d_indices, uint32_t index_size, const void* d_vals,
+                           const void* val, uint64_t n, void* d_results, uint8_t* d_ok, lmr_stream_t stream) {
+    if (!ctx || !ctx->stage || !ctx->stage->open || !valid_iw(index_size)) return LMR_E_INVALID;
+    if (n == 0) return LMR_OK;
+    if (!d_indices || (!d_vals && !val)) return LMR_E_INVALID;
+    StageState* S = ctx->stage;
+    const lmr_apply_desc_t* d = &S->desc;
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    ApplyArgs a = base_args(ctx, d, d_results, d_ok);
+    a.idx = reinterpret_cast<const uint8_t*>(d_indices);
+    a.idx_stride = index_size;
+    a.val = reinterpret_cast<const uint8_t*>(d_vals);
+    a.val_stride = d_vals ? uint64_t(dtype_bytes(int(d->dtype))) : 0;
+    a.val_bits = d_vals ? 0 : load_scalar_bits(val, int(d->dtype));
+    a.n = n;
+    const bool tiled = ctx->ws && ctx->rec_cap > 0 && d->strategy != LMR_STRATEGY_DIRECT &&
+                       tiled_supported(int(d->dtype), d->shard_len) &&
+                       !(d->strategy == LMR_STRATEGY_AUTO && n < 65536);
+    if (!tiled) return run_apply(ctx, d, a, int(index_size), s);      // small stream: applied now
+    a.ret = S->s.a.ret;
+    return hip_status(stage_records(ctx, S->s, a, int(d->dtype), int(index_size), 1, s));
+}
+
+lmr_status_t lmr_stage_finish(lmr_ctx_t* ctx, lmr_stream_t stream) {
+    if (!ctx || !ctx->stage || !ctx->stage->open) return LMR_E_INVALID;
+    StageState* S = ctx->stage;
+    S->open = false;
+    if (S->s.nreg == 0) return LMR_OK;
+    return hip_status(launch_stage_finish(carve_tiled_ws(ctx->ws, ctx->rec_cap), S->s,
+                                          reinterpret_cast<hipStream_t>(stream)));
 }
 
 // ---------------------------------------------------------------- results

@@ -446,6 +446,25 @@ __device__ __forceinline__ T rmw_lds(typename word_of<T>::W* p, int op, int kind
     else return rmw_widened<T>(p, op, kind, v, cmp, eps, ok, err);
 }
 
+// ---------------------------------------------------------------- LDS-staged write-out
+// Write-out of one bucket-sorted LDS round: bucket c's hist[c] records, staged at
+// LDS [base[c], base[c] + hist[c]), go to global [cursor[c], ...). Waves take
+// whole buckets (several waves share a bucket when there are fewer buckets than
+// waves) and their lanes stream contiguous records, so the bucket / offsets are
+// wave-uniform LDS broadcasts and every store instruction covers one contiguous
+// run: put(lds_pos, global_pos) per record.
+template <typename F>
+__device__ __forceinline__ void bucket_writeout(const uint32_t* hist, const uint32_t* base,
+                                                const uint32_t* cursor, uint32_t nb, F&& put) {
+    const uint32_t nw = blockDim.x >> 6, wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const uint32_t wpb = nb >= nw ? 1u : nw / nb;       // waves per bucket
+    const uint32_t bstep = nw / wpb;
+    for (uint32_t c = wave / wpb; c < nb; c += bstep) {
+        const uint32_t len = hist[c], b = base[c], d = cursor[c];
+        for (uint32_t i = (wave % wpb) * 64 + lane; i < len; i += wpb * 64) put(b + i, d + i);
+    }
+}
+
 // ---------------------------------------------------------------- index load
 template <int IW> struct idx_t;
 template <> struct idx_t<1> { using I = uint8_t; };

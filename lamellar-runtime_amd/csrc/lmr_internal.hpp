@@ -9,6 +9,7 @@
 namespace lmr { struct Prof; }
 
 namespace lmr { struct HostStage; void host_stage_free(HostStage* h); }
+namespace lmr { struct StageState; void stage_state_free(StageState* s); }
 
 struct lmr_ctx {
     int device = 0;
@@ -20,6 +21,7 @@ struct lmr_ctx {
     int num_cus = 256;
     lmr::Prof* prof = nullptr;     // stage timing (lmr_ctx_profile), null when off
     lmr::HostStage* host = nullptr;  // host-buffer ingestion staging (lmr_apply_mvmi_host), lazily made
+    lmr::StageState* stage = nullptr;  // staged-apply session (lmr_stage_*), lazily made
 };
 
 namespace lmr {
@@ -31,6 +33,9 @@ constexpr int kBinBlock = 1024;           // threads per bin/scatter block
 constexpr int kMaxBinBlocks = 1024;       // G: blocks of the bin passes
 constexpr int kScanItems = 4096;          // elements per scan block (1024 threads x 4)
 constexpr int kMaxPackPes = 512;
+constexpr int kMaxRegions = 32;           // staged-apply regions per session
+constexpr int kStageInfoWords = 512;      // staged-apply piece table + per-region totals (u32)
+constexpr uint64_t kStageMaxRegion = uint64_t(1) << 30;   // records per staged region
 
 // ---- stage timing: HIP events around kernel stages (see lmr_ctx_profile) ----
 void prof_begin(Prof* p, int stage, hipStream_t s);
@@ -62,6 +67,8 @@ struct TiledWs {
     uint8_t* items;        // TileItem[kMaxTiles] owner items, then delta pieces
     uint16_t* rhist;       // round-major partition: per-round bucket counts
     uint16_t* rbase;       //                         per-round bucket offsets
+    uint32_t* rts;         // staged apply: [kMaxRegions][kMaxTiles + 1] tile starts of each region
+    uint32_t* sinfo;       // staged apply: piece table (pbase, bstart) + per-region in-bounds totals
 };
 size_t tiled_ws_bytes(uint64_t cap);
 TiledWs carve_tiled_ws(uint8_t* base, uint64_t cap);
@@ -101,6 +108,28 @@ hipError_t launch_apply_mvsi(int dtype, const ApplyArgs& a, uint64_t index, hipS
 hipError_t launch_apply_tiled(int dtype, int index_size, const ApplyArgs& a, const TiledWs& w,
                               hipStream_t s);
 bool tiled_supported(int dtype, uint64_t shard_len);
+
+// Staged (deferred) tiled apply: each record stream ("region") is partitioned
+// into shard tiles on arrival, all regions are applied in one tile sweep.
+struct StageRegion {
+    uint64_t base;       // first workspace slot of the region
+    uint64_t n;          // records (slots) of the region
+    void* results;       // caller's per-record results (arrival order), may be null
+    uint8_t* ok;         // caller's per-record Ok flags, may be null
+};
+struct StageSession {
+    ApplyArgs a;         // op / kind / shard / ret of the session (record fields unused)
+    int dtype = 0;
+    int nreg = 0;
+    uint64_t staged = 0; // workspace slots in use
+    StageRegion reg[kMaxRegions];
+};
+// partition the records of `a` into the next region (caller checks capacity:
+// s.staged + a.n <= workspace capacity, a.n <= kStageMaxRegion, s.nreg < kMaxRegions)
+hipError_t launch_stage_region(int dtype, int index_size, const ApplyArgs& a, const TiledWs& w,
+                               StageSession& s, hipStream_t st);
+// apply every staged region in one tile sweep, results back to each region's caller
+hipError_t launch_stage_finish(const TiledWs& w, StageSession& s, hipStream_t st);
 
 // pack (lmr_pack.hip)
 struct PackArgs {

@@ -213,7 +213,7 @@ __device__ __forceinline__ void stage_scan(const uint32_t* hist, uint32_t* base,
 }
 
 template <int IW, int VB, int RPT, int MODE>
-__global__ __launch_bounds__(1024, (IW == 8 && VB == 8) ? 4 : 8) void k_pack_stage(PackK p) {
+__global__ __launch_bounds__(1024) void k_pack_stage(PackK p) {
     using I = typename idx_t<IW>::I;
     using V = typename idx_t<VB>::I;
     constexpr uint32_t kRound = RPT * 1024;
@@ -221,7 +221,6 @@ __global__ __launch_bounds__(1024, (IW == 8 && VB == 8) ? 4 : 8) void k_pack_sta
     __shared__ I s_off[kRound];
     __shared__ V s_val[kRound];
     __shared__ uint32_t s_pos[kRound];
-    __shared__ uint8_t s_pe[kRound];
     const uint32_t np = p.npes;
     const bool agg = np <= 16;
     for (uint32_t i = threadIdx.x; i < np; i += blockDim.x) cursor[i] = p.counts[uint64_t(i) * p.G + blockIdx.x];
@@ -264,18 +263,14 @@ __global__ __launch_bounds__(1024, (IW == 8 && VB == 8) ? 4 : 8) void k_pack_sta
             s_off[q] = I(m_off[j]);
             s_val[q] = m_v[j];
             if (p.out_pos) s_pos[q] = uint32_t(r0 + uint64_t(j) * 1024 + threadIdx.x);
-            s_pe[q] = uint8_t(m_pe[j]);
         }
         if (r0 + kRound < hi) load_round(r0 + kRound);
         __syncthreads();
-        const uint32_t total = base[kStageMaxPes];
-        for (uint32_t q = threadIdx.x; q < total; q += blockDim.x) {
-            const uint32_t e = s_pe[q];
-            const uint32_t dst = cursor[e] + q - base[e];
+        bucket_writeout(hist, base, cursor, np, [&](uint32_t q, uint32_t dst) {
             reinterpret_cast<I*>(p.out_idx)[dst] = s_off[q];
             if (vals) reinterpret_cast<V*>(p.out_vals)[dst] = s_val[q];
             if (p.out_pos) p.out_pos[dst] = s_pos[q];
-        }
+        });
         __syncthreads();
         for (uint32_t i = threadIdx.x; i < np; i += blockDim.x) cursor[i] += hist[i];
     }
@@ -349,7 +344,9 @@ hipError_t launch_pack(const PackArgs& a, uint32_t* counts, uint32_t* partials, 
             const int vbk = a.vals ? int(a.val_bytes) : 1;
             dispatch_pack_stage(int(a.index_size), vbk, [&](auto iw, auto vb) {
                 by_mode([&](auto m) {
-                    hipLaunchKernelGGL((k_pack_stage<decltype(iw)::value, decltype(vb)::value, 4, decltype(m)::value>),
+                    constexpr int IWc = decltype(iw)::value, VBc = decltype(vb)::value;
+                    constexpr int RP = (IWc + VBc + 4) * 8 <= 150 ? 8 : 4;      // rounds of RP * 1024 records in LDS
+                    hipLaunchKernelGGL((k_pack_stage<IWc, VBc, RP, decltype(m)::value>),
                                        dim3(unsigned(G)), dim3(1024), 0, s, p);
                 });
             });

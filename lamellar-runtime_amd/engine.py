@@ -215,6 +215,12 @@ def _distributed(arr, k, dt, op, ret, i_scalar, idx, v_scalar, vals, n, mvsi, re
     returned values of chunk j travel back (async) after chunk j+1's exchange
     has been issued, then lmr_scatter_results puts them in input order.
 
+    Owner side: every chunk's received records are partitioned into shard tiles
+    on arrival (lmr_stage_soa) and all chunks are applied in one sweep of the
+    shard after the last one (lmr_stage_finish), so the shard is read and
+    written once per batch, not once per chunk. Returned values of every chunk
+    travel back after that sweep.
+
     Collective: every PE issues the same sequence. PEs agree on the chunk count
     through the first header (column 4 = the sender's chunk count); a PE past
     its own last chunk sends empty chunks.
@@ -237,6 +243,11 @@ def _distributed(arr, k, dt, op, ret, i_scalar, idx, v_scalar, vals, n, mvsi, re
     sbits = (vals & 0xFFFFFFFFFFFFFFFF) if (v_scalar and not mvsi) else 0
     shard, slen = arr.local_shard(), arr.num_elems_local()
     empty_u8 = k.empty(0, torch.uint8)
+    # the owner expects about as many records as it sends (uniform streams); more
+    # than the workspace holds only costs an extra shard sweep
+    with st.on("apply"):
+        k.stage_begin(shard, slen, arr.kind, dt, op, cmp_bits, eps_bits,
+                      expect=0 if mvsi else (m + m // 8 + (1 << 16)))
 
     def pack_chunk(j):
         """-> (send_idx, send_vals, pos, counts (device or host), lo, hi)"""
@@ -277,7 +288,7 @@ def _distributed(arr, k, dt, op, ret, i_scalar, idx, v_scalar, vals, n, mvsi, re
 
     nchunks = my_k
     nxt = pack_chunk(0)
-    pending = None
+    pending = []
     j = 0
     while j < nchunks:
         send_idx, send_vals, pos, counts, lo, hi = nxt
@@ -307,9 +318,6 @@ def _distributed(arr, k, dt, op, ret, i_scalar, idx, v_scalar, vals, n, mvsi, re
             r_vals, w_v = team.alltoallv_async(send_vals, val_ss, val_rs, eb)
         # next chunk's pack runs while this chunk is on the wire
         nxt = pack_chunk(j + 1) if j + 1 < nchunks else None
-        if pending is not None:
-            send_back(pending)
-            pending = None
         total = int(sum(recv_counts))
         with st.on("apply"):
             w_i.wait()
@@ -320,18 +328,21 @@ def _distributed(arr, k, dt, op, ret, i_scalar, idx, v_scalar, vals, n, mvsi, re
             _apply_received(k, arr, dt, op, shard, slen, rh, recv_counts, iw, eb, r_idx, r_vals,
                             r_res, r_ok, cmp_bits, eps_bits)
         if returning:
-            pending = (r_res, r_ok, recv_counts, send_counts, pos, lo, hi)
+            pending.append((r_res, r_ok, recv_counts, send_counts, pos, lo, hi))
         j += 1
-    if pending is not None:
-        send_back(pending)
+    with st.on("apply"):
+        k.stage_finish()
+    for p in pending:
+        send_back(p)
     st.join()
 
 
 def _apply_received(k, arr, dt, op, shard, slen, rh, recv_counts, iw, eb, r_idx, r_vals, r_res, r_ok,
                     cmp_bits, eps_bits):
-    """Apply one chunk's received records: consecutive sources with the same
-    value form (array values / the same scalar) go in one call; MVSI sources
-    one by one (their block is applied as one atomic unit)."""
+    """Stage one chunk's received records into the open session: consecutive
+    sources with the same value form (array values / the same scalar) go in one
+    call; MVSI sources are applied at once, one by one (their block is applied
+    as one atomic unit)."""
     npes = len(recv_counts)
     io = vo = ro = 0
     s = 0
@@ -359,11 +370,9 @@ def _apply_received(k, arr, dt, op, shard, slen, rh, recv_counts, iw, eb, r_idx,
         seg_ok = r_ok[ro:ro + cnt] if r_ok is not None else None
         if scalar:
             ubits = int(np.array([bits], dtype=np.int64).view(np.uint64)[0])
-            k.apply_soa(shard, slen, arr.kind, dt, op, seg_idx, iw, None, ubits, cnt, seg_res, seg_ok,
-                        cmp_bits, eps_bits)
+            k.stage_soa(seg_idx, iw, None, ubits, cnt, seg_res, seg_ok)
         else:
-            k.apply_soa(shard, slen, arr.kind, dt, op, seg_idx, iw, r_vals[vo:vo + cnt * eb], 0, cnt,
-                        seg_res, seg_ok, cmp_bits, eps_bits)
+            k.stage_soa(seg_idx, iw, r_vals[vo:vo + cnt * eb], 0, cnt, seg_res, seg_ok)
             vo += cnt * eb
         io += cnt * iw
         ro += cnt

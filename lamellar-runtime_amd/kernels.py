@@ -51,7 +51,7 @@ class DeviceKernels:
     is_device = True
 
     def __init__(self, device: torch.device, strategy: int = Strategy.Auto,
-                 max_ws_records: int = 1 << 28):
+                 max_ws_records: int = 1 << 29):
         if device.type != "cuda" or not torch.cuda.is_available():
             raise LamellarError(LmrStatus.INVALID,
                                 "the batched op path runs on a HIP device; no GPU is visible")
@@ -135,6 +135,29 @@ class DeviceKernels:
                                     None if vals is not None else ctypes.cast(byref(sv), c_void_p),
                                     int(n), _p(results), _p(ok), self.stream())
         check(st, "lmr_apply_soa")
+
+    # ---- staged apply (lmr_stage_*): the owner side of the multi-PE exchange
+    def stage_begin(self, shard, shard_len, kind, dt, op, cmp_bits=0, eps_bits=0, expect=0):
+        """Open a staged session for one op on one shard. `expect`: records the
+        session will likely stage; the workspace grows to hold them now, before
+        anything is staged (lmr_ctx_reserve is refused while records are staged)."""
+        if expect:
+            self._maybe_reserve(int(expect))
+        d = self._desc(shard, shard_len, kind, dt, op, cmp_bits, eps_bits)
+        check(self.lib.lmr_stage_begin(self.ctx, byref(d)), "lmr_stage_begin")
+
+    def stage_soa(self, idx, iw, vals, scalar_bits, n, results=None, ok=None):
+        """Partition n records (lmr_apply_soa's arguments) into the session; their
+        results / Ok flags are valid once stage_finish has run on this stream."""
+        sv = c_uint64(int(scalar_bits) & 0xFFFFFFFFFFFFFFFF)
+        st = self.lib.lmr_stage_soa(self.ctx, _p(idx), int(iw), _p(vals),
+                                    None if vals is not None else ctypes.cast(byref(sv), c_void_p),
+                                    int(n), _p(results), _p(ok), self.stream())
+        check(st, "lmr_stage_soa")
+
+    def stage_finish(self):
+        """Apply every staged record in one sweep of the shard and close the session."""
+        check(self.lib.lmr_stage_finish(self.ctx, self.stream()), "lmr_stage_finish")
 
     def apply_mvmi(self, shard, shard_len, kind, dt, op, idx_vals_bytes, nbytes, iw,
                    results=None, ok=None, cmp_bits=0, eps_bits=0):

@@ -108,6 +108,16 @@ class CpuTestKernels:
                 if o is not None:
                     o[k] = okk
 
+    def stage_begin(self, shard, shard_len, kind, dt, op, cmp_bits=0, eps_bits=0, expect=0):
+        self._stage = (shard, shard_len, kind, dt, op, cmp_bits, eps_bits)
+
+    def stage_soa(self, idx, iw, vals, scalar_bits, n, results=None, ok=None):
+        shard, shard_len, kind, dt, op, cb, eb = self._stage
+        self.apply_soa(shard, shard_len, kind, dt, op, idx, iw, vals, scalar_bits, n, results, ok, cb, eb)
+
+    def stage_finish(self):
+        self._stage = None
+
     def apply_mvsi(self, shard, shard_len, kind, dt, op, vals, n, index, results=None, ok=None,
                    cmp_bits=0, eps_bits=0):
         idx = torch.from_numpy(np.full(n, index, dtype=np.uint64).view(np.uint8))

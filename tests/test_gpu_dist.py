@@ -114,3 +114,59 @@ def test_two_pes_one_gpu_gloo_chunked(orc):
     with tempfile.TemporaryDirectory() as d:
         _run(2, {"LAMELLAR_COMM_BACKEND": "gloo", "LAMELLAR_EXCHANGE_CHUNK": "9000"}, d, 1)
         _check(orc, d, 2, 1)
+
+
+BIG_WORKER = r'''
+import os, sys
+import numpy as np
+sys.path.insert(0, os.environ["LMR_ROOT"])
+from _lamellar_bootstrap import load_package
+lam = load_package()
+world = lam.LamellarWorldBuilder().build()
+me, ws = world.my_pe(), world.num_pes()
+rng = np.random.default_rng(900 + me)
+n_len = (1 << 21) + 9
+arr = lam.AtomicArray(world.team(), n_len, lam.Distribution.Block, "u64")
+gi = rng.integers(0, n_len, 1 << 20).astype(np.uint64)
+gv = rng.integers(0, 2**40, gi.size).astype(np.uint64)
+arr.batch_add(gi, gv).block(); world.barrier()
+after_add = arr.to_numpy()
+# conflict-free fetch_add across PEs: PE p takes the indices = p (mod ws)
+perm = np.random.default_rng(7).permutation(n_len)
+fi = perm[perm % ws == me][:300000].astype(np.uint64)
+olds = arr.batch_fetch_add(fi, gv[:fi.size]).block(); world.barrier()
+np.savez(os.path.join(os.environ["LMR_OUT"], f"pe{me}.npz"), after_add=after_add, gi=gi, gv=gv, fi=fi,
+         olds=olds.cpu().numpy().view(np.uint64), after_fetch=arr.to_numpy())
+world.barrier()
+'''
+
+
+@pytest.mark.parametrize("ws,backend", [(1, "nccl"), (2, "gloo")], ids=["rccl-1rank", "gloo-2pe"])
+def test_staged_exchange_many_chunks(orc, ws, backend):
+    """> 128 tiles per shard, 2^20 records per PE in chunks of 2^18: every chunk's
+    received records are staged as regions (coarse + piece partition) and applied in
+    one sweep; final state and fetch olds against the oracle."""
+    env = dict(os.environ, LMR_ROOT=ROOT, LAMELLAR_COMM_BACKEND=backend, LAMELLAR_EXCHANGE_CHUNK=str(1 << 18),
+               MASTER_ADDR="127.0.0.1", MASTER_PORT=str(29800 + ws + (os.getpid() % 100)))
+    if ws == 1:
+        env["LAMELLAR_FORCE_EXCHANGE"] = "1"
+    with tempfile.TemporaryDirectory() as d:
+        env["LMR_OUT"] = d
+        procs = [subprocess.Popen([sys.executable, "-c", BIG_WORKER],
+                                  env=dict(env, RANK=str(r), WORLD_SIZE=str(ws), LOCAL_RANK=str(r)))
+                 for r in range(ws)]
+        assert [p.wait(timeout=300) for p in procs] == [0] * ws
+        pe = [dict(np.load(os.path.join(d, f"pe{r}.npz"))) for r in range(ws)]
+    n_len = (1 << 21) + 9
+    exp = np.zeros(n_len, dtype=np.uint64)
+    for r in range(ws):
+        np.add.at(exp, pe[r]["gi"].astype(np.int64), pe[r]["gv"])
+    for r in range(ws):
+        assert np.array_equal(pe[r]["after_add"], exp)
+    exp2 = exp.copy()
+    for r in range(ws):
+        fi = pe[r]["fi"].astype(np.int64)
+        assert np.array_equal(pe[r]["olds"], exp[fi])
+        exp2[fi] += pe[r]["gv"][:fi.size]
+    for r in range(ws):
+        assert np.array_equal(pe[r]["after_fetch"], exp2)

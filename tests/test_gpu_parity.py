@@ -101,10 +101,15 @@ def _perm_inputs(dt, op, rng, shard_len, n):
 
 
 @pytest.mark.parametrize("shape", ["soa", "svmi", "aos"])
-@pytest.mark.parametrize("strategy", [1, 2], ids=["direct", "tiled"])
+@pytest.mark.parametrize("strategy", [1, 2, 3], ids=["direct", "tiled", "staged"])
 @pytest.mark.parametrize("dt", DTYPE_NAMES)
-def test_apply_conflict_free_bit_exact(world, orc, lam, dt, strategy, shape):
-    """Every op, every type: one record per element -> bit-exact state and results."""
+def test_apply_conflict_free_bit_exact(world, orc, lam, dt, strategy, shape, monkeypatch):
+    """Every op, every type: one record per element -> bit-exact state and results.
+    staged: the tiled path through the staged pipeline, each call cut into 3 regions."""
+    if strategy == 3:
+        monkeypatch.setenv("LMR_STAGED", "1")
+        monkeypatch.setenv("LMR_STAGE_SPLIT", "3")
+        strategy = 2
     k = world.team().kernels
     k.reserve(1 << 20)
     rng = np.random.default_rng(1234 + CODE[dt])
@@ -372,14 +377,23 @@ def test_device_errors(world, lam, strategy):
         k.strategy = old
 
 
-@pytest.fixture(params=["count", "rm"])
+@pytest.fixture(params=["count", "rm", "staged", "grouped"])
 def partition(request, monkeypatch):
-    """Two-level partition variant: count pass + bucket-major temp ("count") or the
-    round-major temp with the tile counts built in the coarse pass ("rm")."""
+    """Two-level partition variant: count pass + bucket-major temp ("count"), the
+    round-major temp with the tile counts built in the coarse pass ("rm"), or the
+    staged pipeline (coarse pass, then fixed-size pieces counted and sorted by tile)
+    with every call cut into 3 regions applied in one sweep ("staged"), or the count
+    pass with the fine pass and tile apply run per group of coarse buckets ("grouped")."""
+    monkeypatch.delenv("LMR_PARTITION", raising=False)
+    monkeypatch.delenv("LMR_STAGED", raising=False)
+    monkeypatch.delenv("LMR_GROUP_RECORDS", raising=False)
+    if request.param == "grouped":
+        monkeypatch.setenv("LMR_GROUP_RECORDS", "100000")
     if request.param == "rm":
         monkeypatch.setenv("LMR_PARTITION", "rm")
-    else:
-        monkeypatch.delenv("LMR_PARTITION", raising=False)
+    elif request.param == "staged":
+        monkeypatch.setenv("LMR_STAGED", "1")
+        monkeypatch.setenv("LMR_STAGE_SPLIT", "3")
     return request.param
 
 
@@ -490,3 +504,106 @@ def test_two_level_out_of_bounds_fetch(world, orc, lam, partition):
     assert np.array_equal(got, exp)
     res = d_res.cpu().numpy().view(np.uint64)
     assert np.array_equal(res[good], shard0[idx[good].astype(np.int64)])
+
+
+@pytest.mark.parametrize("dt", ["u64", "u32", "u16", "i8", "f64", "f32"])
+def test_staged_session_regions(world, orc, lam, dt):
+    """lmr_stage_*: several record streams of one op staged as regions (array values,
+    a scalar value, out-of-bounds records, one stream below the tiled threshold that is
+    applied at once) and applied in one sweep; final shard, per-stream results in
+    arrival order and the OOB error bit against the oracle (conflict-free: bit-exact)."""
+    k = world.team().kernels
+    k.reserve(1 << 21)
+    rng = np.random.default_rng(606 + CODE[dt])
+    t = NP[dt]
+    shard_len = (1 << 20) + 77
+    dt_obj = lam.dtype_of(dt)
+    eb = np.dtype(t).itemsize
+    for op in (FETCH_ADD, ADD, 18, CAS if not IS_FLOAT[dt] else CAS_EPS):
+        shard0, _, _, cur, eps = _perm_inputs(dt, op, rng, shard_len, 10)
+        perm = rng.permutation(shard_len)
+        sizes = [300000, 70000, 1000, 200000]
+        streams, o = [], 0
+        for j, m in enumerate(sizes):
+            idx = perm[o:o + m].astype(np.uint64)
+            o += m
+            vals = rand_vals(dt, m, rng, op)
+            if op in (CAS, CAS_EPS):
+                vals = rand_vals(dt, m, rng, 18)
+            scalar = (j == 1)
+            if scalar:
+                vals[:] = vals[0]
+            if j == 3:                                     # a few out-of-bounds records
+                idx[rng.random(m) < 0.01] = shard_len + 5
+            streams.append((idx, vals, scalar))
+        # oracle: streams in order (conflict-free across streams)
+        ref = shard0.copy()
+        L = orc.layout_new(shard_len, 1, 0, 0)
+        exp = []
+        for idx, vals, scalar in streams:
+            good = idx < shard_len
+            st, res, okk = orc.batch_op(L, [ref], kind_for(dt), CODE[dt], t, op, idx[good], vals[good], cur, eps)
+            assert st == 0
+            exp.append((good, res, okk))
+        d_shard = to_dev(shard0)
+        rk = ret_kind(op)
+        cb = dt_obj.to_bits(cur) if cur is not None else 0
+        ebits = dt_obj.to_bits(eps) if eps is not None else 0
+        outs = []
+        k.stage_begin(d_shard, shard_len, kind_for(dt), dt_obj, op, cb, ebits)
+        for idx, vals, scalar in streams:
+            m = idx.size
+            d_res = torch.zeros(m * eb, dtype=torch.uint8, device="cuda") if rk else None
+            d_ok = torch.zeros(m, dtype=torch.uint8, device="cuda") if rk == 2 else None
+            if scalar:
+                k.stage_soa(to_dev(idx), 8, None, dt_obj.to_bits(vals[0]), m, d_res, d_ok)
+            else:
+                k.stage_soa(to_dev(idx), 8, to_dev(vals), 0, m, d_res, d_ok)
+            outs.append((d_res, d_ok))
+        k.stage_finish()
+        k.synchronize()
+        assert k.errors(clear=True) == 1, (dt, op)
+        assert bits_equal(from_dev(d_shard, dt, shard_len), ref), (dt, op)
+        for (good, res, okk), (d_res, d_ok), (idx, _, _) in zip(exp, outs, streams):
+            if rk:
+                got = from_dev(d_res, dt, idx.size)[good]
+                assert bits_equal(got, res), (dt, op, "results")
+            if rk == 2:
+                assert np.array_equal(d_ok[:idx.size].cpu().numpy()[good], okk), (dt, op, "ok")
+
+
+def test_staged_session_collisions_many_regions(world, orc, lam):
+    """40 colliding u64 fetch_add streams (more than the 32-region table and the
+    reserved workspace hold: staged records are applied in several sweeps): exact final
+    state; per element the olds are exactly init, init+1, ... (v = 1)."""
+    k = world.team().kernels
+    k.reserve(1 << 21)
+    rng = np.random.default_rng(31)
+    shard_len = (1 << 19) + 3
+    shard0 = rng.integers(0, 2**60, shard_len, dtype=np.uint64)
+    d_shard = to_dev(shard0)
+    dt_obj = lam.dtype_of("u64")
+    k.stage_begin(d_shard, shard_len, 1, dt_obj, FETCH_ADD)
+    idxs, outs = [], []
+    for j in range(40):
+        m = 70000 + 1000 * j
+        idx = rng.integers(0, shard_len, m).astype(np.uint64)
+        d_res = torch.zeros(m * 8, dtype=torch.uint8, device="cuda")
+        k.stage_soa(to_dev(idx), 8, None, 1, m, d_res, None)
+        idxs.append(idx)
+        outs.append(d_res)
+    k.stage_finish()
+    k.synchronize()
+    assert k.errors(clear=True) == 0
+    idx = np.concatenate(idxs)
+    res = np.concatenate([o.cpu().numpy().view(np.uint64) for o in outs])
+    exp = shard0.copy()
+    np.add.at(exp, idx.astype(np.int64), np.uint64(1))
+    assert np.array_equal(d_shard.cpu().numpy().view(np.uint64)[:shard_len], exp)
+    order = np.lexsort((res, idx))
+    si, so = idx[order], res[order]
+    first = np.ones(si.size, dtype=bool)
+    first[1:] = si[1:] != si[:-1]
+    grp_start = np.maximum.accumulate(np.where(first, np.arange(si.size), 0))
+    rank = np.arange(si.size) - grp_start
+    assert np.array_equal(so, shard0[si] + rank.astype(np.uint64))
