@@ -10,11 +10,9 @@ mkdir -p $O
 export TMPDIR=/tmp
 tools/gpu_steps.sh \
   "200|$tag/c2.log|python bench.py --config c2 --steps 20 --warmup 5 --no-cpu-baseline" \
-  "200|$tag/c2_rm.log|LMR_PARTITION=rm python bench.py --config c2 --steps 20 --warmup 5 --no-cpu-baseline" \
   "200|$tag/c3.log|python bench.py --config c3 --steps 20 --warmup 5 --no-cpu-baseline" \
-  "200|$tag/c3_rm.log|LMR_PARTITION=rm python bench.py --config c3 --steps 20 --warmup 5 --no-cpu-baseline" \
   "200|$tag/c5.log|python bench.py --config c5 --steps 20 --warmup 5 --no-cpu-baseline" \
-  "200|$tag/c5_rm.log|LMR_PARTITION=rm python bench.py --config c5 --steps 20 --warmup 5 --no-cpu-baseline" \
+  "200|$tag/c2_direct.log|python bench.py --config c2 --steps 10 --warmup 3 --no-cpu-baseline --strategy direct" \
   "200|$tag/c4_force.log|LAMELLAR_FORCE_EXCHANGE=1 python bench.py --config c4 --steps 10 --warmup 3 --no-cpu-baseline" \
   "300|$tag/e2e.log|python bench.py --config c2 --steps 3 --warmup 1 --no-cpu-baseline --e2e" \
   "300|$tag/prof_c2.log|rocprofv3 --kernel-trace --stats -T --output-format csv -d $O/prof_c2/trace -o run -- python3 bench.py --config c2 --steps 5 --warmup 2 --no-cpu-baseline" \
