@@ -245,6 +245,7 @@ struct PartArgs {
     // at (final position - *ring_base) so a group's bins reuse the start of the bin buffer
     uint32_t cg_lo, cg_hi;
     const uint32_t* ring_base;    // null: 0
+    int match_bits;               // > 0: rank by wave key matching on that many bucket bits
 };
 
 // coarse_off[c][g] = start of block g's coarse-c records in the temp buffer
@@ -318,8 +319,9 @@ __global__ __launch_bounds__(1024) void k_coarse_scatter(PartArgs p) {
 #pragma unroll
         for (int j = 0; j < RPT; j++) {
             m_ok[j] = m_raw[j] < p.shard_len;
-            m_c[j] = uint32_t(m_raw[j] >> cshift);
-            if (m_ok[j]) m_rank[j] = atomicAdd(&hist[m_c[j]], 1u);
+            m_c[j] = m_ok[j] ? uint32_t(m_raw[j] >> cshift) : 0u;
+            if (p.match_bits) m_rank[j] = wave_match_rank(hist, m_c[j], m_ok[j], p.match_bits);
+            else if (m_ok[j]) m_rank[j] = atomicAdd(&hist[m_c[j]], 1u);
         }
         __syncthreads();
         small_excl_scan(hist, base, C, &tot);
@@ -647,8 +649,9 @@ __global__ __launch_bounds__(1024) void k_fine_scatter(PartArgs p) {
 #pragma unroll
             for (int j = 0; j < RPT; j++) {
                 m_ok[j] = r0 + uint32_t(j) * 1024 + threadIdx.x < hi;
-                m_f[j] = (m_idx[j] >> p.tile_shift) - t0;
-                if (m_ok[j]) m_rank[j] = atomicAdd(&hist[m_f[j]], 1u);
+                m_f[j] = m_ok[j] ? (m_idx[j] >> p.tile_shift) - t0 : 0u;
+                if (p.match_bits) m_rank[j] = wave_match_rank(hist, m_f[j], m_ok[j], p.match_bits);
+                else if (m_ok[j]) m_rank[j] = atomicAdd(&hist[m_f[j]], 1u);
             }
             __syncthreads();
             small_excl_scan(hist, base, nf, &tot);
@@ -1194,6 +1197,13 @@ static int fine_blocks_cap() {
     return v;
 }
 
+// LMR_MATCH_RANK=1: rank records in the coarse / fine LDS rounds by wave key
+// matching (one LDS atomic per distinct bucket and wave) instead of one LDS
+// atomic per record; read per call (A/B measurements)
+static bool match_rank() {
+    const char* e = getenv("LMR_MATCH_RANK");
+    return e && e[0] == '1';
+}
 // records per fine+apply group (LMR_GROUP_RECORDS; 0 = one fine pass, then one tile
 // sweep); read per call: tests switch it within one process
 static int group_records() {
@@ -1250,7 +1260,7 @@ hipError_t launch_apply_tiled(int dtype, int index_size, const ApplyArgs& a, con
     PartArgs qf{};            // grouped fine pass (launched per group of coarse buckets below)
     bool grouped = false;
     if (rm) {
-        PartArgs q;
+        PartArgs q{};
         q.idx = a.idx; q.idx_stride = a.idx_stride; q.val = a.val; q.val_stride = a.val_stride;
         q.n = a.n; q.shard_len = a.shard_len; q.chunk = b.chunk; q.tile_shift = shift;
         q.num_tiles = uint32_t(num_tiles); q.G = uint32_t(G);
@@ -1319,7 +1329,7 @@ hipError_t launch_apply_tiled(int dtype, int index_size, const ApplyArgs& a, con
     if (num_tiles > uint64_t(kFine)) {
         // two-level LDS-staged partition: coarse buckets of kFine tiles, then tiles
         if (a.prof) prof_begin(a.prof, LMR_STAGE_BIN_SCATTER, s);
-        PartArgs q;
+        PartArgs q{};
         q.idx = a.idx; q.idx_stride = a.idx_stride; q.val = a.val; q.val_stride = a.val_stride;
         q.n = a.n; q.shard_len = a.shard_len; q.chunk = b.chunk; q.tile_shift = shift;
         q.num_tiles = uint32_t(num_tiles); q.G = uint32_t(G);
@@ -1328,6 +1338,7 @@ hipError_t launch_apply_tiled(int dtype, int index_size, const ApplyArgs& a, con
         q.tmp_idx = w.tmp_idx; q.tmp_val = a.val ? w.tmp_val : nullptr;
         q.qpos = has_res ? w.qpos : nullptr;
         q.bin_lidx = w.bin_lidx; q.bin_val = w.bin_val; q.rpos = b.rpos;
+        q.match_bits = match_rank() ? key_bits(q.C) : 0;
         const uint64_t ncg = uint64_t(q.C) * G + 1;
         hipLaunchKernelGGL(k_coarse_offsets, dim3(unsigned((ncg + 255) / 256)), dim3(256), 0, s, q);
         e = dispatch_iw(index_size, [&](auto iw) {
@@ -1342,6 +1353,7 @@ hipError_t launch_apply_tiled(int dtype, int index_size, const ApplyArgs& a, con
         if (a.prof) prof_end(a.prof, LMR_STAGE_BIN_SCATTER, s);
         if (e != hipSuccess) return e;
         q.cg_lo = 0; q.cg_hi = q.C * uint32_t(G); q.ring_base = nullptr;
+        q.match_bits = match_rank() ? key_bits(kFine) : 0;
         if (group_records() > 0 && q.C > 1) {
             qf = q;
             grouped = true;

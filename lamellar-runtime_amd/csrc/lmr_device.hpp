@@ -446,6 +446,42 @@ __device__ __forceinline__ T rmw_lds(typename word_of<T>::W* p, int op, int kind
     else return rmw_widened<T>(p, op, kind, v, cmp, eps, ok, err);
 }
 
+// ---------------------------------------------------------------- wave key matching
+// Match by key bits: `bits` ballots give every lane the mask of active lanes
+// holding its key (keys < 2^bits); the lowest lane of each group adds the group's
+// size to hist[key] (one LDS atomic instruction for all groups, distinct
+// addresses) and broadcasts the returned base. Constant cost in the number of
+// distinct keys, where wave_agg_rank loops once per key.
+__device__ __forceinline__ uint64_t wave_key_mask(uint32_t key, bool active, int bits) {
+    uint64_t m = __ballot(active);
+    for (int b = 0; b < bits; b++) {
+        const bool on = (key >> b) & 1u;
+        const uint64_t bb = __ballot(on);
+        m &= on ? bb : ~bb;
+    }
+    return m;
+}
+__device__ __forceinline__ uint32_t wave_match_rank(uint32_t* hist, uint32_t key, bool active, int bits) {
+    const int lane = threadIdx.x & 63;
+    const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+    const uint64_t m = wave_key_mask(key, active, bits);
+    const int leader = __ffsll((unsigned long long)m) - 1;
+    uint32_t base = 0;
+    if (active && lane == leader) base = atomicAdd(&hist[key], uint32_t(__popcll(m)));
+    base = __shfl(base, active ? leader : lane, 64);
+    return base + uint32_t(__popcll(m & lt));
+}
+__device__ __forceinline__ void wave_match_count(uint32_t* hist, uint32_t key, bool active, int bits) {
+    const int lane = threadIdx.x & 63;
+    const uint64_t m = wave_key_mask(key, active, bits);
+    if (active && lane == __ffsll((unsigned long long)m) - 1) atomicAdd(&hist[key], uint32_t(__popcll(m)));
+}
+__host__ __device__ inline int key_bits(uint32_t nkeys) {
+    int b = 0;
+    while ((1u << b) < nkeys) b++;
+    return b;
+}
+
 // ---------------------------------------------------------------- LDS-staged write-out
 // Write-out of one bucket-sorted LDS round: bucket c's hist[c] records, staged at
 // LDS [base[c], base[c] + hist[c]), go to global [cursor[c], ...). Waves take

@@ -83,7 +83,7 @@ __global__ __launch_bounds__(1024) void k_pack_count(PackK p) {
     __syncthreads();
     const uint64_t lo = uint64_t(blockIdx.x) * p.chunk;
     const uint64_t hi = min(lo + p.chunk, p.n);
-    const bool agg = p.npes <= 16;
+    const int bits = key_bits(p.npes);
     bool oob = false;
     constexpr int U = 4;
     for (uint64_t b0 = lo; b0 < hi; b0 += U * 1024) {       // block-uniform: ballots need every lane
@@ -101,8 +101,7 @@ __global__ __launch_bounds__(1024) void k_pack_count(PackK p) {
             const bool in = k < hi;
             const bool ok = in && pe_and_offset_mode<MODE>(p.F, g[j], pe, off);
             oob |= in && !ok;
-            if (agg) wave_agg_count(cnt, uint32_t(pe), ok);
-            else if (ok) atomicAdd(&cnt[uint32_t(pe)], 1u);
+            wave_match_count(cnt, ok ? uint32_t(pe) : 0u, ok, bits);
         }
     }
     if (oob) raise_err(p.err, LMR_ERRBIT_OOB);
@@ -222,7 +221,7 @@ __global__ __launch_bounds__(1024) void k_pack_stage(PackK p) {
     __shared__ V s_val[kRound];
     __shared__ uint32_t s_pos[kRound];
     const uint32_t np = p.npes;
-    const bool agg = np <= 16;
+    const int bits = key_bits(np);
     for (uint32_t i = threadIdx.x; i < np; i += blockDim.x) cursor[i] = p.counts[uint64_t(i) * p.G + blockIdx.x];
     const uint64_t lo = uint64_t(blockIdx.x) * p.chunk;
     const uint64_t hi = min(lo + p.chunk, p.n);
@@ -250,8 +249,7 @@ __global__ __launch_bounds__(1024) void k_pack_stage(PackK p) {
             const bool ok = (r0 + uint64_t(j) * 1024 + threadIdx.x < hi) && pe_and_offset_mode<MODE>(p.F, m_g[j], pe, off);
             m_pe[j] = ok ? uint32_t(pe) : 0xFFFFFFFFu;
             m_off[j] = off;
-            if (agg) m_rank[j] = wave_agg_rank(hist, uint32_t(pe), ok);
-            else if (ok) m_rank[j] = atomicAdd(&hist[pe], 1u);
+            m_rank[j] = wave_match_rank(hist, ok ? uint32_t(pe) : 0u, ok, bits);
         }
         __syncthreads();
         stage_scan(hist, base, np);

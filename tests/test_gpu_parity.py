@@ -377,16 +377,20 @@ def test_device_errors(world, lam, strategy):
         k.strategy = old
 
 
-@pytest.fixture(params=["count", "rm", "staged", "grouped"])
+@pytest.fixture(params=["count", "rm", "staged", "grouped", "match"])
 def partition(request, monkeypatch):
     """Two-level partition variant: count pass + bucket-major temp ("count"), the
     round-major temp with the tile counts built in the coarse pass ("rm"), or the
     staged pipeline (coarse pass, then fixed-size pieces counted and sorted by tile)
     with every call cut into 3 regions applied in one sweep ("staged"), or the count
-    pass with the fine pass and tile apply run per group of coarse buckets ("grouped")."""
+    pass with the fine pass and tile apply run per group of coarse buckets ("grouped"), or the
+    count pass with records ranked by wave key matching in the LDS rounds ("match")."""
     monkeypatch.delenv("LMR_PARTITION", raising=False)
     monkeypatch.delenv("LMR_STAGED", raising=False)
     monkeypatch.delenv("LMR_GROUP_RECORDS", raising=False)
+    monkeypatch.delenv("LMR_MATCH_RANK", raising=False)
+    if request.param == "match":
+        monkeypatch.setenv("LMR_MATCH_RANK", "1")
     if request.param == "grouped":
         monkeypatch.setenv("LMR_GROUP_RECORDS", "100000")
     if request.param == "rm":
