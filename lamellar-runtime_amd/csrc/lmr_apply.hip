@@ -629,18 +629,31 @@ __global__ __launch_bounds__(1024) void k_fine_scatter(PartArgs p) {
     const uint32_t cg_end = (blockIdx.x + 1 == gridDim.x) ? p.cg_hi
                                                           : seg_lower_bound(rec_lo + total_recs * (blockIdx.x + 1) / gridDim.x);
     uint32_t cg = cg_begin;
-    if (cg < cg_end) load_round(p.coarse_off[cg], p.coarse_off[cg + 1]);
+    // segment cg's tile cursors (threads f < 128 hold tile f's), prefetched with the
+    // segment's first round so the strided fine_off loads are off the critical path
+    uint32_t pf_cur = 0;
+    auto load_cursor = [&](uint32_t cgn) {
+        const uint32_t cn = cgn / p.G, gn = cgn % p.G, tn = cn * kFine;
+        if (threadIdx.x < min(uint32_t(kFine), p.num_tiles - tn))
+            pf_cur = p.fine_off[uint64_t(tn + threadIdx.x) * p.G + gn];
+    };
+    if (cg < cg_end) {
+        load_round(p.coarse_off[cg], p.coarse_off[cg + 1]);
+        load_cursor(cg);
+    }
     for (; cg < cg_end; cg++) {
-        const uint32_t c = cg / p.G, g = cg % p.G;
+        const uint32_t c = cg / p.G;
         const uint32_t t0 = c * kFine;
         const uint32_t nf = min(uint32_t(kFine), p.num_tiles - t0);
         const uint32_t lo = p.coarse_off[cg], hi = p.coarse_off[cg + 1];
         if (lo == hi) {   // empty segment: its (all-invalid) prefetch is replaced by the next one's
-            if (cg + 1 < cg_end) load_round(p.coarse_off[cg + 1], p.coarse_off[cg + 2]);
+            if (cg + 1 < cg_end) {
+                load_round(p.coarse_off[cg + 1], p.coarse_off[cg + 2]);
+                load_cursor(cg + 1);
+            }
             continue;
         }
-        for (uint32_t f = threadIdx.x; f < nf; f += blockDim.x)
-            cursor[f] = p.fine_off[uint64_t(t0 + f) * p.G + g];
+        if (threadIdx.x < nf) cursor[threadIdx.x] = pf_cur;
         for (uint32_t r0 = lo; r0 < hi; r0 += kRound) {
             for (uint32_t f = threadIdx.x; f < nf; f += blockDim.x) hist[f] = 0;
             __syncthreads();
@@ -668,6 +681,7 @@ __global__ __launch_bounds__(1024) void k_fine_scatter(PartArgs p) {
                 load_round(r0 + kRound, hi);
             } else if (cg + 1 < cg_end) {
                 load_round(p.coarse_off[cg + 1], p.coarse_off[cg + 2]);
+                load_cursor(cg + 1);
             }
             __syncthreads();
             uint16_t* bl = p.bin_lidx - rb;
