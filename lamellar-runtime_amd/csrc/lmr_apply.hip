@@ -1660,23 +1660,41 @@ __global__ __launch_bounds__(1024) void k_fine_piece(PieceArgs a) {
     const uint32_t npieces = a.pbase[a.C];
     const uint32_t lmask = (1u << a.tile_shift) - 1u;
     const V sv = V(a.scalar_bits);
-    for (uint32_t pid = blockIdx.x; pid < npieces; pid += gridDim.x) {
-        const PieceLoc L = piece_loc(a, pid);
+    // the next round's records and the next piece's tile cursors are loaded into
+    // registers while the current round is ranked and written out
+    uint32_t m_idx[RPT];
+    V m_val[RPT];
+    uint32_t pf_cur = 0;
+    auto load_round = [&](uint32_t r0, uint32_t hi) {
+#pragma unroll
+        for (int j = 0; j < RPT; j++) {
+            const uint32_t k = r0 + uint32_t(j) * 1024 + threadIdx.x;
+            const bool in = k < hi;
+            m_idx[j] = in ? a.tmp_idx[k] : 0u;
+            m_val[j] = in ? (a.tmp_val ? reinterpret_cast<const V*>(a.tmp_val)[k] : sv) : V(0);
+        }
+    };
+    auto load_piece = [&](const PieceLoc& L) {
+        load_round(L.lo, L.hi);
+        const uint32_t nf = min(uint32_t(kFine), a.num_tiles - L.c * kFine);
+        if (threadIdx.x < nf)
+            pf_cur = a.R + a.cnt[uint64_t(a.pbase[L.c]) * kFine + uint64_t(threadIdx.x) * L.np + L.p];
+    };
+    uint32_t pid = blockIdx.x;
+    PieceLoc L{};
+    if (pid < npieces) {
+        L = piece_loc(a, pid);
+        load_piece(L);
+    }
+    for (; pid < npieces; pid += gridDim.x) {
         const uint32_t t0 = L.c * kFine;
         const uint32_t nf = min(uint32_t(kFine), a.num_tiles - t0);
-        const uint32_t* cb = a.cnt + uint64_t(a.pbase[L.c]) * kFine + L.p;
-        for (uint32_t f = threadIdx.x; f < nf; f += blockDim.x) cursor[f] = a.R + cb[uint64_t(f) * L.np];
+        if (threadIdx.x < nf) cursor[threadIdx.x] = pf_cur;
+        const uint32_t nxt = pid + gridDim.x;
+        PieceLoc LN{};
+        if (nxt < npieces) LN = piece_loc(a, nxt);
         for (uint32_t r0 = L.lo; r0 < L.hi; r0 += kRound) {
             for (uint32_t f = threadIdx.x; f < nf; f += blockDim.x) hist[f] = 0;
-            uint32_t m_idx[RPT];
-            V m_val[RPT];
-#pragma unroll
-            for (int j = 0; j < RPT; j++) {
-                const uint32_t k = r0 + uint32_t(j) * 1024 + threadIdx.x;
-                const bool in = k < L.hi;
-                m_idx[j] = in ? a.tmp_idx[k] : 0u;
-                m_val[j] = in ? (a.tmp_val ? reinterpret_cast<const V*>(a.tmp_val)[k] : sv) : V(0);
-            }
             __syncthreads();
             uint32_t m_rank[RPT], m_f[RPT];
 #pragma unroll
@@ -1696,6 +1714,8 @@ __global__ __launch_bounds__(1024) void k_fine_piece(PieceArgs a) {
                 s_val[q] = m_val[j];
                 if (a.rpos) a.rpos[k] = cursor[m_f[j]] + m_rank[j];
             }
+            if (r0 + kRound < L.hi) load_round(r0 + kRound, L.hi);
+            else if (nxt < npieces) load_piece(LN);
             __syncthreads();
             bucket_writeout(hist, base, cursor, nf, [&](uint32_t q, uint32_t dst) {
                 a.bin_lidx[dst] = s_l[q];
@@ -1705,6 +1725,7 @@ __global__ __launch_bounds__(1024) void k_fine_piece(PieceArgs a) {
             for (uint32_t f = threadIdx.x; f < nf; f += blockDim.x) cursor[f] += hist[f];
         }
         __syncthreads();
+        L = LN;
     }
 }
 

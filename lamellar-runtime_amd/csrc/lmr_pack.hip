@@ -192,23 +192,36 @@ __global__ __launch_bounds__(1024) void k_pack_scatter(PackK p) {
 // apply's coarse pass. Not stable within a PE: no caller depends on the order of
 // records inside one destination's buffer (the apply is a parallel, per-element
 // atomic application, as the reference's concurrent AMs are).
-constexpr uint32_t kStageMaxPes = 128;
+constexpr uint32_t kStageMaxPes = 512;
 
+// exclusive scan of hist[0..m) (m <= kStageMaxPes <= blockDim.x) into base[], total
+// into base[kStageMaxPes]; every thread of the block takes part
 __device__ __forceinline__ void stage_scan(const uint32_t* hist, uint32_t* base, uint32_t m) {
-    if (threadIdx.x < 64) {
-        const uint32_t l = threadIdx.x;
-        uint32_t a = (2 * l < m) ? hist[2 * l] : 0u, b = (2 * l + 1 < m) ? hist[2 * l + 1] : 0u;
-        uint32_t x = a + b, inc = x;
+    __shared__ uint32_t wsum[16];
+    const uint32_t t = threadIdx.x, lane = t & 63, w = t >> 6;
+    const uint32_t x = t < m ? hist[t] : 0u;
+    uint32_t inc = x;
 #pragma unroll
-        for (int d = 1; d < 64; d <<= 1) {
-            uint32_t y = __shfl_up(inc, d, 64);
-            if (int(l) >= d) inc += y;
-        }
-        uint32_t ex = inc - x;
-        if (2 * l < m) base[2 * l] = ex;
-        if (2 * l + 1 < m) base[2 * l + 1] = ex + a;
-        if (l == 63) base[kStageMaxPes] = inc;
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t y = __shfl_up(inc, d, 64);
+        if (int(lane) >= d) inc += y;
     }
+    if (lane == 63) wsum[w] = inc;
+    __syncthreads();
+    if (w == 0) {
+        const uint32_t nw = blockDim.x >> 6;
+        const uint32_t v = lane < nw ? wsum[lane] : 0u;
+        uint32_t vi = v;
+#pragma unroll
+        for (int d = 1; d < 16; d <<= 1) {
+            const uint32_t y = __shfl_up(vi, d, 64);
+            if (int(lane) >= d) vi += y;
+        }
+        if (lane < nw) wsum[lane] = vi - v;
+        if (lane == nw - 1) base[kStageMaxPes] = vi;
+    }
+    __syncthreads();
+    if (t < m) base[t] = inc - x + wsum[w];
 }
 
 template <int IW, int VB, int RPT, int MODE>

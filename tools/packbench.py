@@ -30,11 +30,13 @@ def main():
     dt = lam.dtype_of("u64")
     g = torch.Generator(device="cuda")
     g.manual_seed(5)
-    for npes in (1, 2, 8):
+    # npes = 512 over 2^29 elements: the key count of a pack by (destination PE, coarse
+    # bucket) for 8 PEs x 64 coarse buckets of 2^20 u64 elements each
+    for npes, elems in ((1, 1 << 26), (2, 2 << 26), (8, 8 << 26), (64, 8 << 26), (512, 8 << 26)):
         L = _capi.lmr_layout_t()
-        _capi.lib().lmr_layout_new(ctypes.byref(L), npes << 26, npes, 0, 0)
+        _capi.lib().lmr_layout_new(ctypes.byref(L), elems, npes, 0, 0)
         iw = _capi.lib().lmr_index_size(ctypes.byref(L))
-        gidx = torch.randint(0, npes << 26, (n,), dtype=torch.int64, device="cuda", generator=g)
+        gidx = torch.randint(0, elems, (n,), dtype=torch.int64, device="cuda", generator=g)
         vals = torch.randint(0, 1 << 62, (n,), dtype=torch.int64, device="cuda", generator=g)
         for want_pos in (False, True):
             for _ in range(2):

@@ -1,4 +1,3 @@
-# pack microbenchmark + its rocprofv3 kernel trace (GPU box, repo root)
-mkdir -p gpurun_out/pack && export TMPDIR=/tmp && tools/gpu_steps.sh \
-  "200|pack/packbench.log|python tools/packbench.py" \
-  "300|pack/prof.log|rocprofv3 --kernel-trace --stats -T --output-format csv -d gpurun_out/pack/prof -o run -- python3 tools/packbench.py --reps 3"
+# pack tests + microbenchmark (GPU box, repo root)
+mkdir -p gpurun_out/pack && export TMPDIR=/tmp && timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py -m gpu -x -q --timeout 200 --timeout-method thread -k "pack" > gpurun_out/pack/tests.log 2>&1; echo "pytest rc=$?"; tail -2 gpurun_out/pack/tests.log; tools/gpu_steps.sh \
+  "200|pack/packbench.log|python tools/packbench.py"
