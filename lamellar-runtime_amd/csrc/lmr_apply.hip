@@ -1232,6 +1232,17 @@ static void launch_fine(const PartArgs& q, int vb, hipStream_t s) {
     });
 }
 
+bool piece_partition_pays(int dtype, uint64_t shard_len, uint64_t n) {
+    if (partition_rm_enabled()) return false;
+    const int shift = tile_shift_for(dtype);
+    const uint64_t num_tiles = (shard_len + (uint64_t(1) << shift) - 1) >> shift;
+    if (num_tiles <= uint64_t(kFine) || num_tiles > uint64_t(kMaxTiles) || n == 0) return false;
+    uint64_t G = (n + 65535) / 65536;
+    if (G > uint64_t(bin_blocks_cap())) G = bin_blocks_cap();
+    const uint64_t C = (num_tiles + kFine - 1) / kFine;
+    return n / (G * C) < 8192;
+}
+
 // One tiled piece: a.n <= workspace capacity, a.n < 2^32.
 hipError_t launch_apply_tiled(int dtype, int index_size, const ApplyArgs& a, const TiledWs& w,
                               hipStream_t s) {

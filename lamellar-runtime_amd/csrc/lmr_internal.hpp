@@ -108,6 +108,9 @@ hipError_t launch_apply_mvsi(int dtype, const ApplyArgs& a, uint64_t index, hipS
 hipError_t launch_apply_tiled(int dtype, int index_size, const ApplyArgs& a, const TiledWs& w,
                               hipStream_t s);
 bool tiled_supported(int dtype, uint64_t shard_len);
+// true when the two-level partition's per-(bucket, producer block) segments of an
+// n-record piece would be short (< 8192 records) and fixed-size pieces pay
+bool piece_partition_pays(int dtype, uint64_t shard_len, uint64_t n);
 
 // Staged (deferred) tiled apply: each record stream ("region") is partitioned
 // into shard tiles on arrival, all regions are applied in one tile sweep.

@@ -386,7 +386,7 @@ def partition(request, monkeypatch):
     pass with the fine pass and tile apply run per group of coarse buckets ("grouped"), or the
     count pass with records ranked by wave key matching in the LDS rounds ("match")."""
     monkeypatch.delenv("LMR_PARTITION", raising=False)
-    monkeypatch.delenv("LMR_STAGED", raising=False)
+    monkeypatch.setenv("LMR_STAGED", "0")          # the segment-based fine pass unless "staged"
     monkeypatch.delenv("LMR_GROUP_RECORDS", raising=False)
     monkeypatch.delenv("LMR_MATCH_RANK", raising=False)
     if request.param == "match":
