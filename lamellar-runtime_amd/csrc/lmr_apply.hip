@@ -287,10 +287,10 @@ __device__ __forceinline__ void small_excl_scan(const uint32_t* hist, uint32_t* 
 // into registers right after the current round is staged in LDS, so they are
 // in flight while the staged round is written out.
 // RPT records per thread per round (kRound = RPT * 1024 records staged in LDS).
-template <int IW, int VB, int RPT>
-__global__ __launch_bounds__(1024) void k_coarse_scatter(PartArgs p) {
+template <int IW, int VB, int RPT, int NT>
+__global__ __launch_bounds__(NT) void k_coarse_scatter(PartArgs p) {
     using V = typename idx_t<VB>::I;
-    constexpr uint32_t kRound = RPT * 1024;
+    constexpr uint32_t kRound = RPT * NT;
     __shared__ uint32_t hist[kMaxCoarse], base[kMaxCoarse], cursor[kMaxCoarse], tot;
     __shared__ uint32_t s_idx[kRound];
     __shared__ V s_val[kRound];
@@ -304,7 +304,7 @@ __global__ __launch_bounds__(1024) void k_coarse_scatter(PartArgs p) {
     auto load_round = [&](uint64_t r0) {
 #pragma unroll
         for (int j = 0; j < RPT; j++) {
-            const uint64_t k = r0 + uint64_t(j) * 1024 + threadIdx.x;
+            const uint64_t k = r0 + uint64_t(j) * NT + threadIdx.x;
             const bool in = k < hi;
             m_raw[j] = in ? load_idx<IW>(p.idx, p.idx_stride, k) : ~uint64_t(0);
             m_val[j] = (in && p.val) ? *reinterpret_cast<const V*>(p.val + k * p.val_stride) : V(0);
@@ -328,7 +328,7 @@ __global__ __launch_bounds__(1024) void k_coarse_scatter(PartArgs p) {
         __syncthreads();
 #pragma unroll
         for (int j = 0; j < RPT; j++) {
-            const uint64_t k = r0 + uint64_t(j) * 1024 + threadIdx.x;
+            const uint64_t k = r0 + uint64_t(j) * NT + threadIdx.x;
             if (!m_ok[j]) {
                 if (p.qpos && k < hi) p.qpos[k] = 0xFFFFFFFFu;
                 continue;
@@ -591,10 +591,10 @@ __global__ __launch_bounds__(1024, 8) void k_fine_rm(PartArgs p) {
 // Persistent over (coarse bucket c, producer block g) segments, a contiguous
 // record-balanced range of them per block; the first round of the next segment
 // is prefetched while the current segment's last round is written out.
-template <int VB, int RPT>
-__global__ __launch_bounds__(1024) void k_fine_scatter(PartArgs p) {
+template <int VB, int RPT, int NT>
+__global__ __launch_bounds__(NT) void k_fine_scatter(PartArgs p) {
     using V = typename idx_t<VB>::I;
-    constexpr uint32_t kRound = RPT * 1024;
+    constexpr uint32_t kRound = RPT * NT;
     __shared__ uint32_t hist[kFine], base[kFine], cursor[kFine], tot;
     __shared__ uint16_t s_l[kRound];
     __shared__ V s_val[kRound];
@@ -605,7 +605,7 @@ __global__ __launch_bounds__(1024) void k_fine_scatter(PartArgs p) {
     auto load_round = [&](uint32_t r0, uint32_t hi) {
 #pragma unroll
         for (int j = 0; j < RPT; j++) {
-            const uint32_t k = r0 + uint32_t(j) * 1024 + threadIdx.x;
+            const uint32_t k = r0 + uint32_t(j) * NT + threadIdx.x;
             const bool in = k < hi;
             m_idx[j] = in ? p.tmp_idx[k] : 0xFFFFFFFFu;
             m_val[j] = (in && p.tmp_val) ? reinterpret_cast<const V*>(p.tmp_val)[k] : V(0);
@@ -661,7 +661,7 @@ __global__ __launch_bounds__(1024) void k_fine_scatter(PartArgs p) {
             bool m_ok[RPT];
 #pragma unroll
             for (int j = 0; j < RPT; j++) {
-                m_ok[j] = r0 + uint32_t(j) * 1024 + threadIdx.x < hi;
+                m_ok[j] = r0 + uint32_t(j) * NT + threadIdx.x < hi;
                 m_f[j] = m_ok[j] ? (m_idx[j] >> p.tile_shift) - t0 : 0u;
                 if (p.match_bits) m_rank[j] = wave_match_rank(hist, m_f[j], m_ok[j], p.match_bits);
                 else if (m_ok[j]) m_rank[j] = atomicAdd(&hist[m_f[j]], 1u);
@@ -675,7 +675,7 @@ __global__ __launch_bounds__(1024) void k_fine_scatter(PartArgs p) {
                 const uint32_t q = base[m_f[j]] + m_rank[j];
                 s_l[q] = uint16_t(m_idx[j] & lmask);
                 s_val[q] = m_val[j];
-                if (p.rpos) p.rpos[r0 + uint32_t(j) * 1024 + threadIdx.x] = cursor[m_f[j]] + m_rank[j];
+                if (p.rpos) p.rpos[r0 + uint32_t(j) * NT + threadIdx.x] = cursor[m_f[j]] + m_rank[j];
             }
             if (r0 + kRound < hi) {
                 load_round(r0 + kRound, hi);
@@ -1175,12 +1175,13 @@ static int fine_rpt(int vb) {
 }
 // f(vb, rpt) with rpt the largest supported value <= the request whose round
 // (rpt * 1024 records of Extra + VB bytes in LDS) fits in 150 KiB
-template <int Extra, typename F>
+template <int Extra, int NT = 1024, typename F>
 static void dispatch_vb_rpt(int vb, int rpt, F&& f) {
     using std::integral_constant;
     auto with_vb = [&](auto vbt) {
         constexpr int VB = decltype(vbt)::value;
-        constexpr int kMaxR = (150 * 1024) / ((Extra + VB) * 1024);
+        // 1024-thread blocks may take 150 KiB (one per CU); 512-thread blocks 75 KiB (two per CU)
+        constexpr int kMaxR = (NT == 1024 ? 150 * 1024 : 75 * 1024) / ((Extra + VB) * NT);
         auto call = [&](auto r) {
             constexpr int R = decltype(r)::value;
             if constexpr (R <= kMaxR) f(vbt, r);
@@ -1211,6 +1212,12 @@ static int fine_blocks_cap() {
     return v;
 }
 
+// threads per block of the coarse / fine passes (LMR_PART_NT: 1024 = one block per CU
+// with the largest rounds, 512 = two blocks per CU, each with half the LDS)
+static int part_nt() {
+    static int v = env_int("LMR_PART_NT", 1024, 512, 1024);
+    return v >= 1024 ? 1024 : 512;
+}
 // LMR_MATCH_RANK=1: rank records in the coarse / fine LDS rounds by wave key
 // matching (one LDS atomic per distinct bucket and wave) instead of one LDS
 // atomic per record; read per call (A/B measurements)
@@ -1226,10 +1233,16 @@ static int group_records() {
 static void launch_fine(const PartArgs& q, int vb, hipStream_t s) {
     const uint64_t nseg = uint64_t(q.cg_hi - q.cg_lo);
     const unsigned fgrid = unsigned(nseg < uint64_t(fine_blocks_cap()) ? nseg : fine_blocks_cap());
-    dispatch_vb_rpt<2>(vb, fine_rpt(vb), [&](auto vbt, auto rpt) {
-        constexpr int VBc = decltype(vbt)::value, R = decltype(rpt)::value;
-        hipLaunchKernelGGL((k_fine_scatter<VBc, R>), dim3(fgrid ? fgrid : 1u), dim3(1024), 0, s, q);
-    });
+    if (part_nt() == 512)
+        dispatch_vb_rpt<2, 512>(vb, fine_rpt(vb), [&](auto vbt, auto rpt) {
+            constexpr int VBc = decltype(vbt)::value, R = decltype(rpt)::value;
+            hipLaunchKernelGGL((k_fine_scatter<VBc, R, 512>), dim3(fgrid ? fgrid : 1u), dim3(512), 0, s, q);
+        });
+    else
+        dispatch_vb_rpt<2>(vb, fine_rpt(vb), [&](auto vbt, auto rpt) {
+            constexpr int VBc = decltype(vbt)::value, R = decltype(rpt)::value;
+            hipLaunchKernelGGL((k_fine_scatter<VBc, R, 1024>), dim3(fgrid ? fgrid : 1u), dim3(1024), 0, s, q);
+        });
 }
 
 bool piece_partition_pays(int dtype, uint64_t shard_len, uint64_t n) {
@@ -1368,11 +1381,16 @@ hipError_t launch_apply_tiled(int dtype, int index_size, const ApplyArgs& a, con
         hipLaunchKernelGGL(k_coarse_offsets, dim3(unsigned((ncg + 255) / 256)), dim3(256), 0, s, q);
         e = dispatch_iw(index_size, [&](auto iw) {
             constexpr int IW = decltype(iw)::value;
-            auto go = [&](auto vbt, auto rpt) {
-                constexpr int VBc = decltype(vbt)::value, R = decltype(rpt)::value;
-                hipLaunchKernelGGL((k_coarse_scatter<IW, VBc, R>), dim3(unsigned(G)), dim3(1024), 0, s, q);
-            };
-            dispatch_vb_rpt<4>(vb, coarse_rpt(vb), go);
+            if (part_nt() == 512)
+                dispatch_vb_rpt<4, 512>(vb, coarse_rpt(vb), [&](auto vbt, auto rpt) {
+                    constexpr int VBc = decltype(vbt)::value, R = decltype(rpt)::value;
+                    hipLaunchKernelGGL((k_coarse_scatter<IW, VBc, R, 512>), dim3(unsigned(G)), dim3(512), 0, s, q);
+                });
+            else
+                dispatch_vb_rpt<4>(vb, coarse_rpt(vb), [&](auto vbt, auto rpt) {
+                    constexpr int VBc = decltype(vbt)::value, R = decltype(rpt)::value;
+                    hipLaunchKernelGGL((k_coarse_scatter<IW, VBc, R, 1024>), dim3(unsigned(G)), dim3(1024), 0, s, q);
+                });
             return hipGetLastError();
         });
         if (a.prof) prof_end(a.prof, LMR_STAGE_BIN_SCATTER, s);
@@ -1818,7 +1836,7 @@ hipError_t launch_stage_region(int dtype, int index_size, const ApplyArgs& a, co
             constexpr int IW = decltype(iw)::value;
             dispatch_vb_rpt<4>(vb, coarse_rpt(vb), [&](auto vbt, auto rpt) {
                 constexpr int VBc = decltype(vbt)::value, RP = decltype(rpt)::value;
-                hipLaunchKernelGGL((k_coarse_scatter<IW, VBc, RP>), dim3(unsigned(G)), dim3(1024), 0, st, q);
+                hipLaunchKernelGGL((k_coarse_scatter<IW, VBc, RP, 1024>), dim3(unsigned(G)), dim3(1024), 0, st, q);
             });
             return hipGetLastError();
         });
