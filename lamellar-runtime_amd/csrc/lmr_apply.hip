@@ -246,6 +246,14 @@ struct PartArgs {
     uint32_t cg_lo, cg_hi;
     const uint32_t* ring_base;    // null: 0
     int match_bits;               // > 0: rank by wave key matching on that many bucket bits
+    // slot maps (two-level count path, returning ops): instead of qpos / rpos positions the
+    // coarse pass stores each record's LDS slot in its round (qslot[k]) and logs every
+    // round's bucket cursors and counts (clog), the fine pass likewise (rslot[temp], flog);
+    // k_uncoarse / k_unfine rebuild each round in LDS from contiguous runs (see there)
+    uint16_t* qslot;
+    uint32_t* clog;
+    uint16_t* rslot;
+    uint32_t* flog;
 };
 
 // coarse_off[c][g] = start of block g's coarse-c records in the temp buffer
@@ -331,12 +339,21 @@ __global__ __launch_bounds__(NT) void k_coarse_scatter(PartArgs p) {
             const uint64_t k = r0 + uint64_t(j) * NT + threadIdx.x;
             if (!m_ok[j]) {
                 if (p.qpos && k < hi) p.qpos[k] = 0xFFFFFFFFu;
+                if (p.qslot && k < hi) p.qslot[k] = 0xFFFFu;
                 continue;
             }
             const uint32_t q = base[m_c[j]] + m_rank[j];
             s_idx[q] = uint32_t(m_raw[j]);
             s_val[q] = m_val[j];
             if (p.qpos) p.qpos[k] = cursor[m_c[j]] + m_rank[j];   // coalesced in k
+            if (p.qslot) p.qslot[k] = uint16_t(q);
+        }
+        if (p.clog) {                                          // this round's runs, for k_uncoarse
+            uint32_t* lg = p.clog + (uint64_t(r0 / kRound) + g) * 2 * C;
+            for (uint32_t c = threadIdx.x; c < C; c += blockDim.x) {
+                lg[c] = cursor[c];
+                lg[C + c] = hist[c];
+            }
         }
         if (r0 + kRound < hi) load_round(r0 + kRound);     // prefetch the next round
         __syncthreads();
@@ -676,6 +693,14 @@ __global__ __launch_bounds__(NT) void k_fine_scatter(PartArgs p) {
                 s_l[q] = uint16_t(m_idx[j] & lmask);
                 s_val[q] = m_val[j];
                 if (p.rpos) p.rpos[r0 + uint32_t(j) * NT + threadIdx.x] = cursor[m_f[j]] + m_rank[j];
+                if (p.rslot) p.rslot[r0 + uint32_t(j) * NT + threadIdx.x] = uint16_t(q);
+            }
+            if (p.flog) {                                      // this round's runs, for k_unfine
+                uint32_t* lg = p.flog + (uint64_t(lo / kRound) + cg + (r0 - lo) / kRound) * 2 * kFine;
+                for (uint32_t f = threadIdx.x; f < nf; f += blockDim.x) {
+                    lg[f] = cursor[f];
+                    lg[kFine + f] = hist[f];
+                }
             }
             if (r0 + kRound < hi) {
                 load_round(r0 + kRound, hi);
@@ -1026,6 +1051,101 @@ __global__ __launch_bounds__(1024) void k_unpartition(const uint32_t* __restrict
     }
 }
 
+// ---- slot-map un-partition (two-level count path) -----------------------------
+// Round by round the forward passes know where every record went: a round's
+// records were staged in LDS sorted by bucket (record -> LDS slot) and each
+// bucket's run was written contiguously at the round's logged cursor. The
+// inverse reloads those runs (contiguous reads) into the same LDS layout and
+// returns each record's value by its slot, written in the round's own order
+// (coalesced). k_unpartition gathered 8 bytes per record from scattered lines
+// instead: on C3, 2.27 GB fetched per launch for 0.8 GB of algorithmic reads.
+struct UnArgs {
+    const uint8_t* src;      // values in the forward pass's output order
+    uint8_t* dst;            // values in its input order
+    const uint8_t* ok_src;   // Ok flags (Result ops), or null
+    uint8_t* ok_dst;
+    const uint16_t* slot;    // per input-order record: its LDS slot (0xFFFF: dropped record)
+    const uint32_t* log;     // per round: cursor[stride], count[stride]
+    uint32_t kround;         // records per forward round
+    uint32_t stride;         // log entries per half (C coarse buckets / kFine tiles)
+    uint64_t n, chunk;       // k_uncoarse: block g's chunk [g*chunk, min(+chunk, n))
+    const uint32_t* coarse_off;   // k_unfine: the forward fine pass's segments
+    uint32_t cg_lo, cg_hi, G, num_tiles;
+};
+
+template <int VB>
+__device__ __forceinline__ void un_round(const UnArgs& u, const uint32_t* lg, uint32_t nb, uint64_t r0,
+                                         uint32_t len, typename idx_t<VB>::I* lv, uint8_t* lok,
+                                         uint32_t* base, uint32_t* tot) {
+    using V = typename idx_t<VB>::I;
+    const uint32_t* cur = lg;
+    const uint32_t* cnt = lg + u.stride;
+    small_excl_scan(cnt, base, nb, tot);
+    __syncthreads();
+    const V* src = reinterpret_cast<const V*>(u.src);
+    if (u.ok_src)
+        bucket_writeout(cnt, base, cur, nb, [&](uint32_t q, uint32_t g) {
+            lv[q] = src[g];
+            lok[q] = u.ok_src[g];
+        });
+    else
+        bucket_writeout(cnt, base, cur, nb, [&](uint32_t q, uint32_t g) { lv[q] = src[g]; });
+    __syncthreads();
+    V* dst = reinterpret_cast<V*>(u.dst);
+    for (uint32_t i = threadIdx.x; i < len; i += blockDim.x) {
+        const uint32_t sl = u.slot[r0 + i];
+        if (sl == 0xFFFFu) continue;
+        dst[r0 + i] = lv[sl];
+        if (u.ok_src) u.ok_dst[r0 + i] = lok[sl];
+    }
+    __syncthreads();
+}
+
+// temp order -> input order: block g replays the coarse rounds of its chunk
+template <int VB, int KR>
+__global__ __launch_bounds__(1024) void k_uncoarse(UnArgs u) {
+    __shared__ typename idx_t<VB>::I lv[KR];
+    __shared__ uint8_t lok[KR];
+    __shared__ uint32_t base[kMaxCoarse], tot;
+    const uint32_t g = blockIdx.x;
+    const uint64_t lo = uint64_t(g) * u.chunk;
+    const uint64_t hi = min(lo + u.chunk, u.n);
+    for (uint64_t r0 = lo; r0 < hi; r0 += u.kround) {
+        const uint32_t* lg = u.log + (r0 / u.kround + g) * 2 * u.stride;
+        un_round<VB>(u, lg, u.stride, r0, uint32_t(min(uint64_t(u.kround), hi - r0)), lv, lok, base, &tot);
+    }
+}
+
+// binned order -> temp order: the fine pass's segments, rounds replayed per segment
+template <int VB, int KR>
+__global__ __launch_bounds__(1024) void k_unfine(UnArgs u) {
+    __shared__ typename idx_t<VB>::I lv[KR];
+    __shared__ uint8_t lok[KR];
+    __shared__ uint32_t base[kFine], tot;
+    const uint64_t rec_lo = u.coarse_off[u.cg_lo];
+    const uint64_t total_recs = u.coarse_off[u.cg_hi] - rec_lo;
+    auto seg_lower_bound = [&](uint64_t target) {
+        uint32_t lo_s = u.cg_lo, hi_s = u.cg_hi;
+        while (lo_s < hi_s) {
+            const uint32_t mid = (lo_s + hi_s) >> 1;
+            if (uint64_t(u.coarse_off[mid]) < target) lo_s = mid + 1; else hi_s = mid;
+        }
+        return lo_s;
+    };
+    const uint32_t cg_begin = seg_lower_bound(rec_lo + total_recs * blockIdx.x / gridDim.x);
+    const uint32_t cg_end = (blockIdx.x + 1 == gridDim.x) ? u.cg_hi
+                                                          : seg_lower_bound(rec_lo + total_recs * (blockIdx.x + 1) / gridDim.x);
+    for (uint32_t cg = cg_begin; cg < cg_end; cg++) {
+        const uint32_t lo = u.coarse_off[cg], hi = u.coarse_off[cg + 1];
+        const uint32_t t0 = (cg / u.G) * kFine;
+        const uint32_t nf = min(uint32_t(kFine), u.num_tiles - t0);
+        for (uint32_t r0 = lo; r0 < hi; r0 += u.kround) {
+            const uint32_t* lg = u.log + (uint64_t(lo / u.kround) + cg + (r0 - lo) / u.kround) * 2 * kFine;
+            un_round<VB>(u, lg, nf, r0, min(u.kround, hi - r0), lv, lok, base, &tot);
+        }
+    }
+}
+
 // ------------------------------------------------------------------ dispatch
 template <typename F>
 static hipError_t dispatch_dtype(int dtype, F&& f) {
@@ -1097,6 +1217,12 @@ bool tiled_supported(int dtype, uint64_t shard_len) {
     return tiles >= 1 && tiles <= uint64_t(kMaxTiles);
 }
 
+// round logs: both passes log 2 x (C or 128) u32 per LDS round of >= 4096 records;
+// the fine pass has at most one extra round per (bucket, block) segment
+static size_t rlog_words(uint64_t cap) {
+    return (size_t(cap / 2048) + 2 * size_t(kMaxBinBlocks) * 64 + 4096) * 2 * kFine;
+}
+
 size_t tiled_ws_bytes(uint64_t cap) {
     size_t b = 0;
     auto al = [](size_t x) { return (x + 255) & ~size_t(255); };
@@ -1111,6 +1237,7 @@ size_t tiled_ws_bytes(uint64_t cap) {
     b += 2 * al((cap / 4096 + 2) * size_t(kMaxCoarse) * 2);         // round-major rhist / rbase
     b += al(size_t(kMaxRegions) * (kMaxTiles + 1) * 4);             // staged regions' tile starts
     b += al(size_t(kStageInfoWords) * 4);                            // staged piece table / totals
+    b += al(rlog_words(cap) * 4);                                    // round logs (slot-map un-partition)
     return b;
 }
 
@@ -1139,7 +1266,9 @@ TiledWs carve_tiled_ws(uint8_t* base, uint64_t cap) {
     w.rhist = reinterpret_cast<uint16_t*>(p); p += al((cap / 4096 + 2) * size_t(kMaxCoarse) * 2);
     w.rbase = reinterpret_cast<uint16_t*>(p); p += al((cap / 4096 + 2) * size_t(kMaxCoarse) * 2);
     w.rts = reinterpret_cast<uint32_t*>(p); p += al(size_t(kMaxRegions) * (kMaxTiles + 1) * 4);
-    w.sinfo = reinterpret_cast<uint32_t*>(p);
+    w.sinfo = reinterpret_cast<uint32_t*>(p); p += al(size_t(kStageInfoWords) * 4);
+    w.rlog = reinterpret_cast<uint32_t*>(p);
+    w.rlog_words = rlog_words(cap);
     return w;
 }
 
@@ -1201,6 +1330,22 @@ static void dispatch_vb_rpt(int vb, int rpt, F&& f) {
     case 4: with_vb(integral_constant<int, 4>{}); break;
     default: with_vb(integral_constant<int, 8>{}); break;
     }
+}
+// the rpt dispatch_vb_rpt<Extra> (1024 threads) picks for a request (same rule)
+static int eff_rpt(int extra, int vb, int rpt) {
+    const int maxr = (150 * 1024) / ((extra + vb) * 1024);
+    int r = rpt >= 16 ? 16 : rpt >= 12 ? 12 : rpt >= 8 ? 8 : rpt >= 6 ? 6 : 4;
+    if (r > maxr) r = maxr >= 12 ? 12 : (maxr >= 8 ? 8 : 4);
+    return r;
+}
+// LMR_SLOT_UNPARTITION=1: returned values go back through the slot maps and round
+// logs (k_unfine / k_uncoarse: contiguous reads, no fetch amplification) instead of
+// the position maps and k_unpartition's scattered gathers. Off: measured slower
+// (C3 un-partition 0.92 -> 1.43 ms): with one 1024-thread block per CU each replayed
+// round waits on three dependent global round trips. Read per call (tests).
+static bool slot_unpartition() {
+    const char* e = getenv("LMR_SLOT_UNPARTITION");
+    return e && e[0] == '1';
 }
 // LMR_PARTITION=rm selects the round-major two-level partition (no count pass)
 static bool partition_rm_enabled() {      // read per call: tests switch it within one process
@@ -1297,6 +1442,8 @@ hipError_t launch_apply_tiled(int dtype, int index_size, const ApplyArgs& a, con
     }
     PartArgs qf{};            // grouped fine pass (launched per group of coarse buckets below)
     bool grouped = false;
+    bool slot_maps = false;   // returning ops: slot maps + round logs (k_unfine / k_uncoarse)
+    size_t clog_words = 0;
     if (rm) {
         PartArgs q{};
         q.idx = a.idx; q.idx_stride = a.idx_stride; q.val = a.val; q.val_stride = a.val_stride;
@@ -1377,6 +1524,17 @@ hipError_t launch_apply_tiled(int dtype, int index_size, const ApplyArgs& a, con
         q.qpos = has_res ? w.qpos : nullptr;
         q.bin_lidx = w.bin_lidx; q.bin_val = w.bin_val; q.rpos = b.rpos;
         q.match_bits = match_rank() ? key_bits(q.C) : 0;
+        if (has_res && slot_unpartition() && part_nt() == 1024) {
+            const uint64_t kr_c = uint64_t(eff_rpt(4, vb, coarse_rpt(vb))) * 1024;
+            const uint64_t kr_f = uint64_t(eff_rpt(2, vb, fine_rpt(vb))) * 1024;
+            clog_words = size_t(a.n / kr_c + G + 2) * 2 * q.C;
+            const size_t flog_words = size_t(a.n / kr_f + uint64_t(q.C) * G + 2) * 2 * kFine;
+            if (clog_words + flog_words <= w.rlog_words) {
+                slot_maps = true;
+                q.qpos = nullptr; q.qslot = reinterpret_cast<uint16_t*>(w.qpos); q.clog = w.rlog;
+                q.rpos = nullptr; q.rslot = reinterpret_cast<uint16_t*>(w.rpos); q.flog = w.rlog + clog_words;
+            }
+        }
         const uint64_t ncg = uint64_t(q.C) * G + 1;
         hipLaunchKernelGGL(k_coarse_offsets, dim3(unsigned((ncg + 255) / 256)), dim3(256), 0, s, q);
         e = dispatch_iw(index_size, [&](auto iw) {
@@ -1508,7 +1666,31 @@ hipError_t launch_apply_tiled(int dtype, int index_size, const ApplyArgs& a, con
         default: hipLaunchKernelGGL((k_unpartition<8>), dim3(unsigned(G)), dim3(1024), 0, s, map, a.n, n_dev, bound_dev, b.chunk, src, dst, oks, okd); break;
         }
     };
-    if (num_tiles > uint64_t(kFine)) {
+    if (num_tiles > uint64_t(kFine) && slot_maps) {
+        uint8_t* ok_tmp = ok_src ? reinterpret_cast<uint8_t*>(w.bin_lidx) : nullptr;
+        const uint32_t C = uint32_t((num_tiles + kFine - 1) / kFine);
+        UnArgs u{};
+        u.coarse_off = w.coarse_off; u.cg_lo = 0; u.cg_hi = C * uint32_t(G); u.G = uint32_t(G);
+        u.num_tiles = uint32_t(num_tiles); u.n = a.n; u.chunk = b.chunk;
+        // binned -> temp order, replaying the fine rounds
+        u.src = res_bin; u.dst = w.bin_val; u.ok_src = ok_src; u.ok_dst = ok_tmp;
+        u.slot = reinterpret_cast<const uint16_t*>(w.rpos); u.log = w.rlog + clog_words; u.stride = kFine;
+        const uint64_t nseg = uint64_t(C) * G;
+        const unsigned fgrid = unsigned(nseg < uint64_t(fine_blocks_cap()) ? nseg : fine_blocks_cap());
+        dispatch_vb_rpt<2>(vb, fine_rpt(vb), [&](auto vbt, auto rpt) {
+            constexpr int VBc = decltype(vbt)::value, KR = decltype(rpt)::value * 1024;
+            u.kround = KR;
+            hipLaunchKernelGGL((k_unfine<VBc, KR>), dim3(fgrid ? fgrid : 1u), dim3(1024), 0, s, u);
+        });
+        // temp -> input order, replaying the coarse rounds
+        u.src = w.bin_val; u.dst = reinterpret_cast<uint8_t*>(a.results); u.ok_src = ok_tmp; u.ok_dst = a.ok;
+        u.slot = reinterpret_cast<const uint16_t*>(w.qpos); u.log = w.rlog; u.stride = C;
+        dispatch_vb_rpt<4>(vb, coarse_rpt(vb), [&](auto vbt, auto rpt) {
+            constexpr int VBc = decltype(vbt)::value, KR = decltype(rpt)::value * 1024;
+            u.kround = KR;
+            hipLaunchKernelGGL((k_uncoarse<VBc, KR>), dim3(unsigned(G)), dim3(1024), 0, s, u);
+        });
+    } else if (num_tiles > uint64_t(kFine)) {
         uint8_t* ok_tmp = ok_src ? reinterpret_cast<uint8_t*>(w.bin_lidx) : nullptr;
         if (rm)   // temp slots are input positions (holes where records were out of bounds)
             gather(w.rpos, nullptr, w.total, res_bin, w.bin_val, ok_src, ok_tmp);

@@ -69,6 +69,8 @@ struct TiledWs {
     uint16_t* rbase;       //                         per-round bucket offsets
     uint32_t* rts;         // staged apply: [kMaxRegions][kMaxTiles + 1] tile starts of each region
     uint32_t* sinfo;       // staged apply: piece table (pbase, bstart) + per-region in-bounds totals
+    uint32_t* rlog;        // per-round bucket cursors / counts of the partition passes (returning ops)
+    size_t rlog_words;
 };
 size_t tiled_ws_bytes(uint64_t cap);
 TiledWs carve_tiled_ws(uint8_t* base, uint64_t cap);

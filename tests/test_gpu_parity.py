@@ -377,18 +377,22 @@ def test_device_errors(world, lam, strategy):
         k.strategy = old
 
 
-@pytest.fixture(params=["count", "rm", "staged", "grouped", "match"])
+@pytest.fixture(params=["count", "rm", "staged", "grouped", "match", "slotmap"])
 def partition(request, monkeypatch):
     """Two-level partition variant: count pass + bucket-major temp ("count"), the
     round-major temp with the tile counts built in the coarse pass ("rm"), or the
     staged pipeline (coarse pass, then fixed-size pieces counted and sorted by tile)
     with every call cut into 3 regions applied in one sweep ("staged"), or the count
     pass with the fine pass and tile apply run per group of coarse buckets ("grouped"), or the
-    count pass with records ranked by wave key matching in the LDS rounds ("match")."""
+    count pass with records ranked by wave key matching in the LDS rounds ("match"), or the count
+    pass with returned values brought back by slot maps and round logs ("slotmap")."""
     monkeypatch.delenv("LMR_PARTITION", raising=False)
     monkeypatch.setenv("LMR_STAGED", "0")          # the segment-based fine pass unless "staged"
     monkeypatch.delenv("LMR_GROUP_RECORDS", raising=False)
     monkeypatch.delenv("LMR_MATCH_RANK", raising=False)
+    monkeypatch.delenv("LMR_SLOT_UNPARTITION", raising=False)
+    if request.param == "slotmap":
+        monkeypatch.setenv("LMR_SLOT_UNPARTITION", "1")
     if request.param == "match":
         monkeypatch.setenv("LMR_MATCH_RANK", "1")
     if request.param == "grouped":
