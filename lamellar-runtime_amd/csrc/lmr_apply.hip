@@ -1057,8 +1057,8 @@ __global__ __launch_bounds__(1024) void k_unpartition(const uint32_t* __restrict
 // bucket's run was written contiguously at the round's logged cursor. The
 // inverse reloads those runs (contiguous reads) into the same LDS layout and
 // returns each record's value by its slot, written in the round's own order
-// (coalesced). k_unpartition gathered 8 bytes per record from scattered lines
-// instead: on C3, 2.27 GB fetched per launch for 0.8 GB of algorithmic reads.
+// (coalesced). k_unpartition gathers 8 bytes per record from scattered lines
+// instead (C3: FETCH_SIZE 1.14 GB per launch for 0.8 GB of algorithmic reads).
 struct UnArgs {
     const uint8_t* src;      // values in the forward pass's output order
     uint8_t* dst;            // values in its input order
