@@ -1280,9 +1280,14 @@ static int env_int(const char* name, int dflt, int lo, int hi) {
     int x = atoi(v);
     return x < lo ? lo : (x > hi ? hi : x);
 }
-static int bin_blocks_cap() {
-    static int v = env_int("LMR_BIN_BLOCKS", 512, 1, kMaxBinBlocks);
-    return v;
+static int coarse_rpt(int vb);
+// Coarse-pass blocks G (also the count pass's): one per CU when a coarse block
+// takes more than half the LDS (rounds of >= 8K records), two otherwise. G = 256
+// vs 512 on one box (tools/sweep_c2.sh): C2 4.40 -> 4.33 ms, C3 2.72 -> 2.47 ms
+// (larger producer chunks also keep the un-partition gathers local).
+static int bin_blocks_cap(int vb) {
+    static int v = env_int("LMR_BIN_BLOCKS", 0, 0, kMaxBinBlocks);
+    return v ? v : (coarse_rpt(vb) >= 8 ? 256 : 512);
 }
 static int tile_grid_cap() {
     static int v = env_int("LMR_DELTA_BLOCKS", 1024, 1, 1 << 24);
@@ -1395,8 +1400,9 @@ bool piece_partition_pays(int dtype, uint64_t shard_len, uint64_t n) {
     const int shift = tile_shift_for(dtype);
     const uint64_t num_tiles = (shard_len + (uint64_t(1) << shift) - 1) >> shift;
     if (num_tiles <= uint64_t(kFine) || num_tiles > uint64_t(kMaxTiles) || n == 0) return false;
+    const int vb = dtype_bytes(dtype);
     uint64_t G = (n + 65535) / 65536;
-    if (G > uint64_t(bin_blocks_cap())) G = bin_blocks_cap();
+    if (G > uint64_t(bin_blocks_cap(vb))) G = bin_blocks_cap(vb);
     const uint64_t C = (num_tiles + kFine - 1) / kFine;
     return n / (G * C) < 8192;
 }
@@ -1411,7 +1417,7 @@ hipError_t launch_apply_tiled(int dtype, int index_size, const ApplyArgs& a, con
     const int vb = dtype_bytes(dtype);
     // G blocks: >= 64K records each, at most kMaxBinBlocks
     uint64_t G = (a.n + 65535) / 65536;
-    if (G > uint64_t(bin_blocks_cap())) G = bin_blocks_cap();
+    if (G > uint64_t(bin_blocks_cap(vb))) G = bin_blocks_cap(vb);
     if (G < 1) G = 1;
     BinArgs b;
     b.idx = a.idx; b.idx_stride = a.idx_stride;
@@ -1984,7 +1990,7 @@ hipError_t launch_stage_region(int dtype, int index_size, const ApplyArgs& a, co
     const uint32_t R = uint32_t(s.staged);
     const bool has_res = s.a.ret != LMR_RET_NONE;
     uint64_t G = (a.n + 65535) / 65536;
-    if (G > uint64_t(bin_blocks_cap())) G = bin_blocks_cap();
+    if (G > uint64_t(bin_blocks_cap(vb))) G = bin_blocks_cap(vb);
     if (G < 1) G = 1;
     uint32_t* pbase = w.sinfo + kStagePbase;
     uint32_t* bstart = w.sinfo + kStageBstart;
