@@ -46,8 +46,8 @@ METRIC = "batched array ops applied/sec (device-resident), 1/2/4/8 MI355X"
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
-    p.add_argument("--steps", type=int, default=10)
-    p.add_argument("--warmup", type=int, default=3)
+    p.add_argument("--steps", type=int, default=20)
+    p.add_argument("--warmup", type=int, default=10)
     p.add_argument("--config", default=None, choices=[None, "c2", "c3", "c4", "c5"])
     p.add_argument("--records-log2", type=int, default=None)
     p.add_argument("--elems-log2", type=int, default=None)
