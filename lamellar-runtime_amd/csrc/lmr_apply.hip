@@ -654,19 +654,25 @@ __global__ __launch_bounds__(NT) void k_fine_scatter(PartArgs p) {
         if (threadIdx.x < min(uint32_t(kFine), p.num_tiles - tn))
             pf_cur = p.fine_off[uint64_t(tn + threadIdx.x) * p.G + gn];
     };
+    // Consecutive segments (c, g..g') of one bucket are one stream: tile t's records
+    // of producers g..g' own the contiguous range [fine_off[t][g], fine_off[t][g'+1])
+    // and their order inside it is free, so rounds run across segment boundaries
+    // (no partial round per segment, one cursor load per bucket and block).
+    auto range_end = [&](uint32_t c0) { return min(cg_end, (c0 / p.G + 1) * p.G); };
     if (cg < cg_end) {
-        load_round(p.coarse_off[cg], p.coarse_off[cg + 1]);
+        load_round(p.coarse_off[cg], p.coarse_off[range_end(cg)]);
         load_cursor(cg);
     }
-    for (; cg < cg_end; cg++) {
+    for (uint32_t ce; cg < cg_end; cg = ce) {
+        ce = range_end(cg);
         const uint32_t c = cg / p.G;
         const uint32_t t0 = c * kFine;
         const uint32_t nf = min(uint32_t(kFine), p.num_tiles - t0);
-        const uint32_t lo = p.coarse_off[cg], hi = p.coarse_off[cg + 1];
-        if (lo == hi) {   // empty segment: its (all-invalid) prefetch is replaced by the next one's
-            if (cg + 1 < cg_end) {
-                load_round(p.coarse_off[cg + 1], p.coarse_off[cg + 2]);
-                load_cursor(cg + 1);
+        const uint32_t lo = p.coarse_off[cg], hi = p.coarse_off[ce];
+        if (lo == hi) {   // empty range: its (all-invalid) prefetch is replaced by the next one's
+            if (ce < cg_end) {
+                load_round(p.coarse_off[ce], p.coarse_off[range_end(ce)]);
+                load_cursor(ce);
             }
             continue;
         }
@@ -704,9 +710,9 @@ __global__ __launch_bounds__(NT) void k_fine_scatter(PartArgs p) {
             }
             if (r0 + kRound < hi) {
                 load_round(r0 + kRound, hi);
-            } else if (cg + 1 < cg_end) {
-                load_round(p.coarse_off[cg + 1], p.coarse_off[cg + 2]);
-                load_cursor(cg + 1);
+            } else if (ce < cg_end) {
+                load_round(p.coarse_off[ce], p.coarse_off[range_end(ce)]);
+                load_cursor(ce);
             }
             __syncthreads();
             uint16_t* bl = p.bin_lidx - rb;
@@ -1135,8 +1141,9 @@ __global__ __launch_bounds__(1024) void k_unfine(UnArgs u) {
     const uint32_t cg_begin = seg_lower_bound(rec_lo + total_recs * blockIdx.x / gridDim.x);
     const uint32_t cg_end = (blockIdx.x + 1 == gridDim.x) ? u.cg_hi
                                                           : seg_lower_bound(rec_lo + total_recs * (blockIdx.x + 1) / gridDim.x);
-    for (uint32_t cg = cg_begin; cg < cg_end; cg++) {
-        const uint32_t lo = u.coarse_off[cg], hi = u.coarse_off[cg + 1];
+    for (uint32_t cg = cg_begin, ce; cg < cg_end; cg = ce) {     // merged as in k_fine_scatter
+        ce = min(cg_end, (cg / u.G + 1) * u.G);
+        const uint32_t lo = u.coarse_off[cg], hi = u.coarse_off[ce];
         const uint32_t t0 = (cg / u.G) * kFine;
         const uint32_t nf = min(uint32_t(kFine), u.num_tiles - t0);
         for (uint32_t r0 = lo; r0 < hi; r0 += u.kround) {
