@@ -1305,12 +1305,19 @@ static int tile_grid_cap() {
 // amortise the per-round barriers and bucket scan and lengthen the output runs.
 // Measured on one box (tools/r1h_cmd.sh): 8-byte values, coarse 1.71 -> 1.43 ms
 // at 12K-record rounds, fine 1.75 -> 1.60 ms at 8K; 4-byte values (C5) are best
-// at 4K-record rounds.
+// at 4K-record rounds. Once a fine block streams its consecutive segments as one
+// range (no partial round per segment), 12K fine rounds pay too (same box, C2:
+// fine 1.59 -> 1.51 ms); the piece-based fine pass (kPiece = 16K records) stays
+// at 8K rounds (C4 rehearsal: 12K = 1.5 rounds per piece, fine 2.52 -> 2.89 ms).
 static int coarse_rpt(int vb) {
     static int v = env_int("LMR_COARSE_RPT", 0, 0, 16);
     return v ? v : (vb == 8 ? 12 : 4);
 }
 static int fine_rpt(int vb) {
+    static int v = env_int("LMR_FINE_RPT", 0, 0, 16);
+    return v ? v : (vb == 8 ? 12 : 4);
+}
+static int piece_fine_rpt(int vb) {
     static int v = env_int("LMR_FINE_RPT", 0, 0, 16);
     return v ? v : (vb == 8 ? 8 : 4);
 }
@@ -1736,7 +1743,10 @@ hipError_t launch_apply_tiled(int dtype, int index_size, const ApplyArgs& a, con
 // (not on per-producer-block segments as k_fine_scatter does), so its LDS rounds
 // stay full and its output runs long whatever the region size: a 2^25-record
 // chunk partitions as efficiently as a 2^28-record batch.
-constexpr uint32_t kPiece = 16384;               // records per fine-level piece (4 LDS rounds)
+#ifndef LMR_PIECE_RECORDS
+#define LMR_PIECE_RECORDS 16384                  // (variant builds for measurements: -DLMR_PIECE_RECORDS=...)
+#endif
+constexpr uint32_t kPiece = LMR_PIECE_RECORDS;   // records per fine-level piece (2 LDS rounds of 8K)
 constexpr int kStagePbase = 0;                   // sinfo words: pbase[kMaxCoarse + 1]
 constexpr int kStageBstart = 160;                //              bstart[kMaxCoarse + 1]
 constexpr int kStageInb = 320;                   //              in-bounds records per region
@@ -1814,20 +1824,25 @@ __global__ __launch_bounds__(128) void k_piece_table(const uint32_t* coarse_off,
 
 struct PieceLoc { uint32_t c, p, np, lo, hi; };
 
-// piece pid -> its bucket (the largest c with pbase[c] <= pid) and record range
-__device__ __forceinline__ PieceLoc piece_loc(const PieceArgs& a, uint32_t pid) {
-    uint32_t lo_c = 0, hi_c = a.C;
+// piece pid -> its bucket (the largest c with pbase[c] <= pid) and record range;
+// pbase / bstart are the piece table in global memory or a block's LDS copy of it
+__device__ __forceinline__ PieceLoc piece_loc(const uint32_t* pbase, const uint32_t* bstart, uint32_t C,
+                                              uint32_t pid) {
+    uint32_t lo_c = 0, hi_c = C;
     while (hi_c - lo_c > 1) {
         const uint32_t m = (lo_c + hi_c) >> 1;
-        if (a.pbase[m] <= pid) lo_c = m; else hi_c = m;
+        if (pbase[m] <= pid) lo_c = m; else hi_c = m;
     }
     PieceLoc L;
     L.c = lo_c;
-    L.p = pid - a.pbase[lo_c];
-    L.np = a.pbase[lo_c + 1] - a.pbase[lo_c];
-    L.lo = a.bstart[lo_c] + L.p * kPiece;
-    L.hi = min(L.lo + kPiece, a.bstart[lo_c + 1]);
+    L.p = pid - pbase[lo_c];
+    L.np = pbase[lo_c + 1] - pbase[lo_c];
+    L.lo = bstart[lo_c] + L.p * kPiece;
+    L.hi = min(L.lo + kPiece, bstart[lo_c + 1]);
     return L;
+}
+__device__ __forceinline__ PieceLoc piece_loc(const PieceArgs& a, uint32_t pid) {
+    return piece_loc(a.pbase, a.bstart, a.C, pid);
 }
 
 // per-piece tile histogram (one block per piece; grid = upper bound of pieces)
@@ -1879,9 +1894,15 @@ __global__ __launch_bounds__(1024) void k_fine_piece(PieceArgs a) {
     using V = typename idx_t<VB>::I;
     constexpr uint32_t kRound = RPT * 1024;
     __shared__ uint32_t hist[kFine], base[kFine], cursor[kFine], tot;
+    __shared__ uint32_t s_pb[kMaxCoarse + 1], s_bs[kMaxCoarse + 1];   // the piece table, for piece_loc
     __shared__ uint16_t s_l[kRound];
     __shared__ V s_val[kRound];
-    const uint32_t npieces = a.pbase[a.C];
+    for (uint32_t c = threadIdx.x; c <= a.C; c += blockDim.x) {
+        s_pb[c] = a.pbase[c];
+        s_bs[c] = a.bstart[c];
+    }
+    __syncthreads();
+    const uint32_t npieces = s_pb[a.C];
     const uint32_t lmask = (1u << a.tile_shift) - 1u;
     const V sv = V(a.scalar_bits);
     // the next round's records and the next piece's tile cursors are loaded into
@@ -1902,12 +1923,12 @@ __global__ __launch_bounds__(1024) void k_fine_piece(PieceArgs a) {
         load_round(L.lo, L.hi);
         const uint32_t nf = min(uint32_t(kFine), a.num_tiles - L.c * kFine);
         if (threadIdx.x < nf)
-            pf_cur = a.R + a.cnt[uint64_t(a.pbase[L.c]) * kFine + uint64_t(threadIdx.x) * L.np + L.p];
+            pf_cur = a.R + a.cnt[uint64_t(s_pb[L.c]) * kFine + uint64_t(threadIdx.x) * L.np + L.p];
     };
     uint32_t pid = blockIdx.x;
     PieceLoc L{};
     if (pid < npieces) {
-        L = piece_loc(a, pid);
+        L = piece_loc(s_pb, s_bs, a.C, pid);
         load_piece(L);
     }
     for (; pid < npieces; pid += gridDim.x) {
@@ -1916,7 +1937,7 @@ __global__ __launch_bounds__(1024) void k_fine_piece(PieceArgs a) {
         if (threadIdx.x < nf) cursor[threadIdx.x] = pf_cur;
         const uint32_t nxt = pid + gridDim.x;
         PieceLoc LN{};
-        if (nxt < npieces) LN = piece_loc(a, nxt);
+        if (nxt < npieces) LN = piece_loc(s_pb, s_bs, a.C, nxt);
         for (uint32_t r0 = L.lo; r0 < L.hi; r0 += kRound) {
             for (uint32_t f = threadIdx.x; f < nf; f += blockDim.x) hist[f] = 0;
             __syncthreads();
@@ -2054,7 +2075,7 @@ hipError_t launch_stage_region(int dtype, int index_size, const ApplyArgs& a, co
         hipLaunchKernelGGL(k_region_starts, dim3((T + 1 + 255) / 256), dim3(256), 0, st, pa,
                            w.rts + uint64_t(r) * (kMaxTiles + 1));
         const unsigned fgrid = unsigned(std::min<uint64_t>(max_pieces, uint64_t(fine_blocks_cap())));
-        dispatch_vb_rpt<2>(vb, fine_rpt(vb), [&](auto vbt, auto rpt) {
+        dispatch_vb_rpt<2>(vb, piece_fine_rpt(vb), [&](auto vbt, auto rpt) {
             constexpr int VBc = decltype(vbt)::value, RP = decltype(rpt)::value;
             hipLaunchKernelGGL((k_fine_piece<VBc, RP>), dim3(fgrid), dim3(1024), 0, st, pa);
         });
