@@ -138,10 +138,12 @@ struct BinArgs {
     uint8_t* bin_val;
     uint32_t* rpos;        // [n] record k -> binned position (~0 = out of bounds); null when nothing is returned
     uint32_t* err;
+    const uint32_t* only_if;  // non-null: the kernel runs only when *only_if != 0
 };
 
 template <int IW>
 __global__ __launch_bounds__(kBinBlock) void k_bin_count(BinArgs b) {
+    if (b.only_if && *b.only_if == 0) return;
     extern __shared__ uint32_t hist[];
     for (uint32_t t = threadIdx.x; t < b.num_tiles; t += blockDim.x) hist[t] = 0;
     __syncthreads();
@@ -194,7 +196,8 @@ __global__ __launch_bounds__(kBinBlock) void k_bin_scatter(BinArgs b) {
 }
 
 __global__ void k_tile_starts(const uint32_t* counts, uint32_t num_tiles, uint32_t G,
-                              const uint32_t* total, uint32_t* tile_start) {
+                              const uint32_t* total, uint32_t* tile_start, const uint32_t* only_if) {
+    if (only_if && *only_if == 0) return;
     uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
     if (t < num_tiles) tile_start[t] = counts[uint64_t(t) * G];
     if (t == num_tiles) tile_start[t] = *total;
@@ -254,11 +257,19 @@ struct PartArgs {
     uint32_t* clog;
     uint16_t* rslot;
     uint32_t* flog;
+    // count-free partition (k_coarse_free / k_fine_free) and its counted fallback
+    const uint32_t* only_if;      // non-null: the kernel runs only when *only_if != 0
+    uint32_t* ff_flag;            // set when a coarse bucket overflows its region
+    uint32_t* ff_fill;            // [C] records reserved in each coarse bucket's region
+    uint32_t* ff_tfill;           // [num_tiles] records reserved in each tile
+    uint32_t capc;                // records per coarse bucket region
+    uint64_t tmp_cap;             // temp arrays' capacity (records)
 };
 
 // coarse_off[c][g] = start of block g's coarse-c records in the temp buffer
 //                  = tile_start[c*kFine] + sum_{t in c} (fine_off[t][g] - tile_start[t])
 __global__ void k_coarse_offsets(PartArgs p) {
+    if (p.only_if && *p.only_if == 0) return;
     const uint64_t i = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
     const uint64_t cg = uint64_t(p.C) * p.G;
     if (i < cg) {
@@ -297,6 +308,7 @@ __device__ __forceinline__ void small_excl_scan(const uint32_t* hist, uint32_t* 
 // RPT records per thread per round (kRound = RPT * 1024 records staged in LDS).
 template <int IW, int VB, int RPT, int NT>
 __global__ __launch_bounds__(NT) void k_coarse_scatter(PartArgs p) {
+    if (p.only_if && *p.only_if == 0) return;
     using V = typename idx_t<VB>::I;
     constexpr uint32_t kRound = RPT * NT;
     __shared__ uint32_t hist[kMaxCoarse], base[kMaxCoarse], cursor[kMaxCoarse], tot;
@@ -610,6 +622,7 @@ __global__ __launch_bounds__(1024, 8) void k_fine_rm(PartArgs p) {
 // is prefetched while the current segment's last round is written out.
 template <int VB, int RPT, int NT>
 __global__ __launch_bounds__(NT) void k_fine_scatter(PartArgs p) {
+    if (p.only_if && *p.only_if == 0) return;
     using V = typename idx_t<VB>::I;
     constexpr uint32_t kRound = RPT * NT;
     __shared__ uint32_t hist[kFine], base[kFine], cursor[kFine], tot;
@@ -728,6 +741,226 @@ __global__ __launch_bounds__(NT) void k_fine_scatter(PartArgs p) {
             for (uint32_t f = threadIdx.x; f < nf; f += blockDim.x) cursor[f] += hist[f];
         }
         __syncthreads();
+    }
+}
+
+// ---- count-free two-level partition (order-insensitive ops) -----------------
+// For ops whose result does not depend on the order records are applied in
+// (wrapping integer add / sub / mul / and / or / xor) with nothing returned, the
+// records of one tile need not keep their input order, and the count pass (a
+// full read of the indices, 8 B/op at 1 PE) is dropped:
+//   k_coarse_free : as k_coarse_scatter, but each round reserves its bucket runs
+//                   with one atomicAdd per bucket on that bucket's fill counter,
+//                   inside a fixed region of capc records per bucket; on the way
+//                   it counts the records of every tile in LDS (one row per block)
+//   k_free_tile_totals + scan : exact tile starts from those rows
+//   k_fine_free   : as k_fine_scatter over record-balanced ranges of the bucket
+//                   regions; each round reserves its tile runs with one atomicAdd
+//                   per tile on that tile's fill counter
+// A bucket that outgrows its region (a batch concentrated on a few 8 MB stretches
+// of the shard) sets ff_flag: the fine pass then does nothing and the counted
+// pipeline, launched behind it with only_if = ff_flag, partitions the batch again
+// from its input. Its kernels return at once when the flag is clear.
+template <int IW, int VB, int RPT>
+__global__ __launch_bounds__(1024) void k_coarse_free(PartArgs p) {
+    using V = typename idx_t<VB>::I;
+    constexpr uint32_t kRound = RPT * 1024;
+    extern __shared__ uint32_t th[];                   // [num_tiles] this block's tile counts
+    __shared__ uint32_t hist[kMaxCoarse], base[kMaxCoarse], cursor[kMaxCoarse], tot;
+    __shared__ uint32_t s_idx[kRound];
+    __shared__ V s_val[kRound];
+    const uint32_t g = blockIdx.x, C = p.C;
+    const int cshift = p.tile_shift + kFineShift;
+    for (uint32_t t = threadIdx.x; t < p.num_tiles; t += blockDim.x) th[t] = 0;
+    const uint64_t lo = uint64_t(g) * p.chunk;
+    const uint64_t hi = min(lo + p.chunk, p.n);
+    uint64_t m_raw[RPT];
+    V m_val[RPT];
+    bool oob = false;
+    auto load_round = [&](uint64_t r0) {
+#pragma unroll
+        for (int j = 0; j < RPT; j++) {
+            const uint64_t k = r0 + uint64_t(j) * 1024 + threadIdx.x;
+            const bool in = k < hi;
+            m_raw[j] = in ? load_idx<IW>(p.idx, p.idx_stride, k) : ~uint64_t(0);
+            m_val[j] = (in && p.val) ? *reinterpret_cast<const V*>(p.val + k * p.val_stride) : V(0);
+        }
+    };
+    load_round(lo);
+    for (uint64_t r0 = lo; r0 < hi; r0 += kRound) {
+        for (uint32_t c = threadIdx.x; c < C; c += blockDim.x) hist[c] = 0;
+        __syncthreads();
+        uint32_t m_rank[RPT], m_c[RPT];
+        bool m_ok[RPT];
+#pragma unroll
+        for (int j = 0; j < RPT; j++) {
+            const uint64_t k = r0 + uint64_t(j) * 1024 + threadIdx.x;
+            m_ok[j] = m_raw[j] < p.shard_len;
+            if (!m_ok[j] && k < hi) oob = true;
+            m_c[j] = m_ok[j] ? uint32_t(m_raw[j] >> cshift) : 0u;
+            if (m_ok[j]) {
+                m_rank[j] = atomicAdd(&hist[m_c[j]], 1u);
+                atomicAdd(&th[uint32_t(m_raw[j] >> p.tile_shift)], 1u);
+            }
+        }
+        __syncthreads();
+        small_excl_scan(hist, base, C, &tot);
+        __syncthreads();
+        // reserve this round's run in every bucket region; the returned fill is
+        // consumed after the LDS staging below, which hides the atomic's latency
+        uint32_t rsv = 0, cnt = 0;
+        if (threadIdx.x < C) {
+            cnt = hist[threadIdx.x];
+            if (cnt) rsv = atomicAdd(&p.ff_fill[threadIdx.x], cnt);
+        }
+#pragma unroll
+        for (int j = 0; j < RPT; j++) {
+            if (!m_ok[j]) continue;
+            const uint32_t q = base[m_c[j]] + m_rank[j];
+            s_idx[q] = uint32_t(m_raw[j]);
+            s_val[q] = m_val[j];
+        }
+        if (threadIdx.x < C) {
+            if (cnt && rsv + cnt > p.capc) atomicOr(p.ff_flag, 1u);
+            cursor[threadIdx.x] = threadIdx.x * p.capc + rsv;
+        }
+        if (r0 + kRound < hi) load_round(r0 + kRound);     // prefetch the next round
+        __syncthreads();
+        // an overflowing bucket spills into the next region (the partition is then
+        // discarded); nothing is written past the temp arrays
+        const uint64_t lim = p.tmp_cap;
+        if (p.val)
+            bucket_writeout(hist, base, cursor, C, [&](uint32_t q, uint32_t dst) {
+                if (dst < lim) {
+                    p.tmp_idx[dst] = s_idx[q];
+                    reinterpret_cast<V*>(p.tmp_val)[dst] = s_val[q];
+                }
+            });
+        else
+            bucket_writeout(hist, base, cursor, C, [&](uint32_t q, uint32_t dst) {
+                if (dst < lim) p.tmp_idx[dst] = s_idx[q];
+            });
+        __syncthreads();
+    }
+    if (oob) raise_err(p.err, LMR_ERRBIT_OOB);
+    __syncthreads();
+    for (uint32_t t = threadIdx.x; t < p.num_tiles; t += blockDim.x)
+        p.counts[uint64_t(g) * p.num_tiles + t] = th[t];   // row g (coalesced)
+}
+
+// tile_start[t] = sum over blocks of the coarse pass's row counts (scanned after).
+// One block per 64 tiles: wave w sums rows w, w + 16, ... (256 B per row read),
+// then the 16 partial sums are added in LDS.
+__global__ __launch_bounds__(1024) void k_free_tile_totals(const uint32_t* rows, uint32_t num_tiles, uint32_t G,
+                                                           uint32_t* out) {
+    __shared__ uint32_t part[16][64];
+    const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const uint32_t t = blockIdx.x * 64 + lane;
+    uint32_t s = 0;
+    if (t < num_tiles)
+        for (uint32_t g = w; g < G; g += 16) s += rows[uint64_t(g) * num_tiles + t];
+    part[w][lane] = s;
+    __syncthreads();
+    if (w == 0 && t < num_tiles) {
+        uint32_t tot = 0;
+#pragma unroll
+        for (int i = 0; i < 16; i++) tot += part[i][lane];
+        out[t] = tot;
+    }
+}
+
+template <int VB, int RPT>
+__global__ __launch_bounds__(1024) void k_fine_free(PartArgs p) {
+    if (*p.ff_flag) return;                            // overflow: the counted pipeline takes over
+    using V = typename idx_t<VB>::I;
+    constexpr uint32_t kRound = RPT * 1024;
+    __shared__ uint32_t hist[kFine], base[kFine], cursor[kFine], tot;
+    __shared__ uint32_t s_fill[kMaxCoarse], s_vs[kMaxCoarse], s_total;
+    __shared__ uint16_t s_l[kRound];
+    __shared__ V s_val[kRound];
+    const uint32_t C = p.C;
+    const uint32_t lmask = (1u << p.tile_shift) - 1u;
+    for (uint32_t c = threadIdx.x; c < C; c += blockDim.x) s_fill[c] = p.ff_fill[c];
+    __syncthreads();
+    small_excl_scan(s_fill, s_vs, C, &s_total);        // bucket c = virtual records [s_vs[c], s_vs[c] + s_fill[c])
+    __syncthreads();
+    const uint64_t total = s_total;
+    const uint32_t v_lo = uint32_t(total * blockIdx.x / gridDim.x);
+    const uint32_t v_hi = uint32_t(total * (blockIdx.x + 1) / gridDim.x);
+    uint32_t c = 0;
+    while (c + 1 < C && s_vs[c + 1] <= v_lo) c++;
+    uint32_t m_idx[RPT];
+    V m_val[RPT];
+    auto load_round = [&](uint32_t r0, uint32_t hi) {
+#pragma unroll
+        for (int j = 0; j < RPT; j++) {
+            const uint32_t k = r0 + uint32_t(j) * 1024 + threadIdx.x;
+            const bool in = k < hi;
+            m_idx[j] = in ? p.tmp_idx[k] : 0xFFFFFFFFu;
+            m_val[j] = (in && p.tmp_val) ? reinterpret_cast<const V*>(p.tmp_val)[k] : V(0);
+        }
+    };
+    // bucket c's slice of [v_lo, v_hi) as physical temp slots
+    auto seg = [&](uint32_t cc, uint32_t& lo, uint32_t& hi) {
+        const uint32_t a = max(v_lo, s_vs[cc]), b = min(v_hi, s_vs[cc] + s_fill[cc]);
+        lo = cc * p.capc + (a - s_vs[cc]);
+        hi = lo + (b > a ? b - a : 0u);
+    };
+    // invariant: the current bucket's first round is loaded (prefetched) on entry
+    uint32_t lo, hi;
+    seg(c, lo, hi);
+    if (lo < hi) load_round(lo, hi);
+    for (; c < C && s_vs[c] < v_hi; c++) {
+        uint32_t nlo = 0, nhi = 0;
+        if (c + 1 < C && s_vs[c + 1] < v_hi) seg(c + 1, nlo, nhi);
+        if (lo == hi) {
+            if (nlo < nhi) load_round(nlo, nhi);
+            lo = nlo; hi = nhi;
+            continue;
+        }
+        const uint32_t t0 = c * kFine;
+        const uint32_t nf = min(uint32_t(kFine), p.num_tiles - t0);
+        const uint32_t ts = threadIdx.x < nf ? p.tile_start[t0 + threadIdx.x] : 0u;
+        for (uint32_t r0 = lo; r0 < hi; r0 += kRound) {
+            for (uint32_t f = threadIdx.x; f < nf; f += blockDim.x) hist[f] = 0;
+            __syncthreads();
+            // (tile, validity) are recomputed from m_idx where needed: with 12-record
+            // rounds the kernel sits at the 128-VGPR limit of a 1024-thread block
+            uint32_t m_rank[RPT];
+#pragma unroll
+            for (int j = 0; j < RPT; j++)
+                if (r0 + uint32_t(j) * 1024 + threadIdx.x < hi)
+                    m_rank[j] = atomicAdd(&hist[(m_idx[j] >> p.tile_shift) - t0], 1u);
+            __syncthreads();
+            small_excl_scan(hist, base, nf, &tot);
+            __syncthreads();
+            uint32_t rsv = 0, cnt = 0;
+            if (threadIdx.x < nf) {
+                cnt = hist[threadIdx.x];
+                if (cnt) rsv = atomicAdd(&p.ff_tfill[t0 + threadIdx.x], cnt);
+            }
+#pragma unroll
+            for (int j = 0; j < RPT; j++) {
+                if (r0 + uint32_t(j) * 1024 + threadIdx.x >= hi) continue;
+                const uint32_t q = base[(m_idx[j] >> p.tile_shift) - t0] + m_rank[j];
+                s_l[q] = uint16_t(m_idx[j] & lmask);
+                s_val[q] = m_val[j];
+            }
+            if (threadIdx.x < nf) cursor[threadIdx.x] = ts + rsv;
+            if (r0 + kRound < hi) load_round(r0 + kRound, hi);
+            else if (nlo < nhi) load_round(nlo, nhi);
+            __syncthreads();
+            V* bv = reinterpret_cast<V*>(p.bin_val);
+            if (p.tmp_val)
+                bucket_writeout(hist, base, cursor, nf, [&](uint32_t q, uint32_t dst) {
+                    p.bin_lidx[dst] = s_l[q];
+                    bv[dst] = s_val[q];
+                });
+            else
+                bucket_writeout(hist, base, cursor, nf, [&](uint32_t q, uint32_t dst) { p.bin_lidx[dst] = s_l[q]; });
+            __syncthreads();
+        }
+        lo = nlo; hi = nhi;
     }
 }
 
@@ -1230,6 +1463,12 @@ static size_t rlog_words(uint64_t cap) {
     return (size_t(cap / 2048) + 2 * size_t(kMaxBinBlocks) * 64 + 4096) * 2 * kFine;
 }
 
+// temp arrays: 25 % (+ 8192 records per coarse bucket) above the piece capacity, the
+// headroom the count-free partition's fixed per-bucket regions need (3 B per record)
+static uint64_t tmp_cap_for(uint64_t cap) {
+    return cap + cap / 4 + uint64_t(kMaxCoarse) * 8192;
+}
+
 size_t tiled_ws_bytes(uint64_t cap) {
     size_t b = 0;
     auto al = [](size_t x) { return (x + 255) & ~size_t(255); };
@@ -1238,7 +1477,7 @@ size_t tiled_ws_bytes(uint64_t cap) {
     b += al((size_t(kMaxTiles) + 1) * 4);                                   // tile_start
     b += al(cap * 2) + al(cap * 8) + al(cap * 4) + al(4);
     b += al((size_t(kMaxCoarse) * kMaxBinBlocks + 1) * 4);
-    b += al(cap * 4) + al(cap * 8) + al(cap * 4);
+    b += al(tmp_cap_for(cap) * 4) + al(tmp_cap_for(cap) * 8) + al(cap * 4);
     b += 2 * al((size_t(kMaxTiles) + 1) * 4) + al(size_t(kMaxTiles) / kScanItems * 4 + 256) + al(4);
     b += al((size_t(kMaxTiles) + 2 * (cap / kSplit) + 2) * 16);   // owner items + delta pieces
     b += 2 * al((cap / 4096 + 2) * size_t(kMaxCoarse) * 2);         // round-major rhist / rbase
@@ -1261,8 +1500,8 @@ TiledWs carve_tiled_ws(uint8_t* base, uint64_t cap) {
     w.rpos = reinterpret_cast<uint32_t*>(p); p += al(cap * 4);
     w.total = reinterpret_cast<uint32_t*>(p); p += al(4);
     w.coarse_off = reinterpret_cast<uint32_t*>(p); p += al((size_t(kMaxCoarse) * kMaxBinBlocks + 1) * 4);
-    w.tmp_idx = reinterpret_cast<uint32_t*>(p); p += al(cap * 4);
-    w.tmp_val = p; p += al(cap * 8);
+    w.tmp_idx = reinterpret_cast<uint32_t*>(p); p += al(tmp_cap_for(cap) * 4);
+    w.tmp_val = p; p += al(tmp_cap_for(cap) * 8);
     w.qpos = reinterpret_cast<uint32_t*>(p); p += al(cap * 4);
     w.tile_items = reinterpret_cast<uint32_t*>(p); p += al((size_t(kMaxTiles) + 1) * 4);
     w.tile_items2 = reinterpret_cast<uint32_t*>(p); p += al((size_t(kMaxTiles) + 1) * 4);
@@ -1276,6 +1515,8 @@ TiledWs carve_tiled_ws(uint8_t* base, uint64_t cap) {
     w.sinfo = reinterpret_cast<uint32_t*>(p); p += al(size_t(kStageInfoWords) * 4);
     w.rlog = reinterpret_cast<uint32_t*>(p);
     w.rlog_words = rlog_words(cap);
+    w.cap = cap;
+    w.tmp_cap = tmp_cap_for(cap);
     return w;
 }
 
@@ -1301,7 +1542,7 @@ static int tile_grid_cap() {
     return v;
 }
 // records per thread per round of the coarse / fine passes (LMR_COARSE_RPT,
-// LMR_FINE_RPT: 4, 6, 8, 12 or 16; capped to what fits the LDS). Bigger rounds
+// LMR_FINE_RPT: 4, 6, 8, 10, 12 or 16; capped to what fits the LDS). Bigger rounds
 // amortise the per-round barriers and bucket scan and lengthen the output runs.
 // Measured on one box (tools/r1h_cmd.sh): 8-byte values, coarse 1.71 -> 1.43 ms
 // at 12K-record rounds, fine 1.75 -> 1.60 ms at 8K; 4-byte values (C5) are best
@@ -1339,6 +1580,7 @@ static void dispatch_vb_rpt(int vb, int rpt, F&& f) {
         };
         if (rpt >= 16) call(integral_constant<int, 16>{});
         else if (rpt >= 12) call(integral_constant<int, 12>{});
+        else if (rpt >= 10) call(integral_constant<int, 10>{});
         else if (rpt >= 8) call(integral_constant<int, 8>{});
         else if (rpt >= 6) call(integral_constant<int, 6>{});
         else call(integral_constant<int, 4>{});
@@ -1353,7 +1595,7 @@ static void dispatch_vb_rpt(int vb, int rpt, F&& f) {
 // the rpt dispatch_vb_rpt<Extra> (1024 threads) picks for a request (same rule)
 static int eff_rpt(int extra, int vb, int rpt) {
     const int maxr = (150 * 1024) / ((extra + vb) * 1024);
-    int r = rpt >= 16 ? 16 : rpt >= 12 ? 12 : rpt >= 8 ? 8 : rpt >= 6 ? 6 : 4;
+    int r = rpt >= 16 ? 16 : rpt >= 12 ? 12 : rpt >= 10 ? 10 : rpt >= 8 ? 8 : rpt >= 6 ? 6 : 4;
     if (r > maxr) r = maxr >= 12 ? 12 : (maxr >= 8 ? 8 : 4);
     return r;
 }
@@ -1409,6 +1651,38 @@ static void launch_fine(const PartArgs& q, int vb, hipStream_t s) {
         });
 }
 
+// Count-free partition (k_coarse_free / k_fine_free): order-insensitive ops with
+// nothing returned, two-level shards, and >= 25 % headroom per coarse bucket region
+// in the temp arrays (always, for pieces within the workspace capacity). Returns its coarse round (records per thread), 0 when not
+// used. LMR_FREE=0 disables it (read per call: tests switch it in one process).
+static int free_partition_rpt(int dtype, int op, int ret, uint64_t n, uint64_t num_tiles, uint64_t tmp_cap) {
+    const char* e = getenv("LMR_FREE");
+    if (e && e[0] == '0') return 0;
+    if (ret != LMR_RET_NONE || dtype > LMR_I64) return 0;
+    if (op != LMR_OP_ADD && op != LMR_OP_SUB && op != LMR_OP_MUL && op != LMR_OP_AND &&
+        op != LMR_OP_OR && op != LMR_OP_XOR)
+        return 0;
+    if (num_tiles <= uint64_t(kFine) || num_tiles > uint64_t(kMaxTiles)) return 0;
+    if (partition_rm_enabled() || group_records() > 0 || match_rank() || part_nt() != 1024) return 0;
+    const uint64_t C = (num_tiles + kFine - 1) / kFine;
+    const uint64_t capc = tmp_cap / C;
+    if (n / C + n / (4 * C) + 8192 > capc) return 0;
+    const int vb = dtype_bytes(dtype);
+    // the largest round that fits next to the LDS tile counts (static + dynamic LDS
+    // <= 160 KiB); 8-byte values: 10K-record rounds at 8192 tiles (12K with the
+    // counted pass). 4-byte values take 8K rounds here (C5: coarse 0.80 -> 0.72 ms)
+    const int cap_r = std::max(coarse_rpt(vb), 8);
+    for (int r : {12, 10, 8, 4})
+        if (r <= cap_r && size_t(4 + vb) * r * 1024 + num_tiles * 4 + 2048 <= size_t(158) * 1024) return r;
+    return 0;
+}
+
+bool free_partition_applies(int dtype, int op, int ret, uint64_t shard_len, uint64_t n, uint64_t cap) {
+    const int shift = tile_shift_for(dtype);
+    const uint64_t num_tiles = (shard_len + (uint64_t(1) << shift) - 1) >> shift;
+    return free_partition_rpt(dtype, op, ret, n, num_tiles, tmp_cap_for(cap)) > 0;
+}
+
 bool piece_partition_pays(int dtype, uint64_t shard_len, uint64_t n) {
     if (partition_rm_enabled()) return false;
     const int shift = tile_shift_for(dtype);
@@ -1433,7 +1707,7 @@ hipError_t launch_apply_tiled(int dtype, int index_size, const ApplyArgs& a, con
     uint64_t G = (a.n + 65535) / 65536;
     if (G > uint64_t(bin_blocks_cap(vb))) G = bin_blocks_cap(vb);
     if (G < 1) G = 1;
-    BinArgs b;
+    BinArgs b{};
     b.idx = a.idx; b.idx_stride = a.idx_stride;
     b.val = a.val; b.val_stride = a.val_stride;
     b.n = a.n; b.shard_len = a.shard_len;
@@ -1500,7 +1774,7 @@ hipError_t launch_apply_tiled(int dtype, int index_size, const ApplyArgs& a, con
         e = scan_exclusive_u32(w.counts, num_tiles * G, w.partials, w.total, s);
         if (e != hipSuccess) return e;
         hipLaunchKernelGGL(k_tile_starts, dim3(unsigned((num_tiles + 1 + 255) / 256)), dim3(256), 0, s,
-                           w.counts, uint32_t(num_tiles), uint32_t(G), w.total, w.tile_start);
+                           w.counts, uint32_t(num_tiles), uint32_t(G), w.total, w.tile_start, nullptr);
         }
         {
         ProfScope pf(a.prof, LMR_STAGE_FINE_SCATTER, s);
@@ -1515,8 +1789,66 @@ hipError_t launch_apply_tiled(int dtype, int index_size, const ApplyArgs& a, con
         e = hipGetLastError();
         }
     } else {
+    // count-free partition first; the counted one below then runs only if it overflowed
+    const uint32_t* guard = nullptr;
+    const int frpt = free_partition_rpt(dtype, a.op, a.ret, a.n, num_tiles, w.tmp_cap);
+    if (frpt > 0) {
+        const uint32_t T = uint32_t(num_tiles);
+        uint32_t* ff_flag = w.rlog;
+        // one coarse block per CU once a round takes most of the LDS
+        uint64_t Gf = (a.n + 65535) / 65536;
+        Gf = std::max<uint64_t>(1, std::min<uint64_t>(Gf, frpt >= 8 ? 256 : 512));
+        PartArgs q{};
+        q.idx = a.idx; q.idx_stride = a.idx_stride; q.val = a.val; q.val_stride = a.val_stride;
+        q.n = a.n; q.shard_len = a.shard_len; q.chunk = (a.n + Gf - 1) / Gf; q.tile_shift = shift;
+        q.num_tiles = T; q.G = uint32_t(Gf); q.C = (T + kFine - 1) / kFine;
+        q.tile_start = w.tile_start; q.counts = w.counts;
+        q.tmp_idx = w.tmp_idx; q.tmp_val = a.val ? w.tmp_val : nullptr;
+        q.bin_lidx = w.bin_lidx; q.bin_val = w.bin_val;
+        q.err = a.err;
+        q.ff_flag = ff_flag; q.ff_fill = w.rlog + 64; q.ff_tfill = w.rlog + 64 + kMaxCoarse;
+        q.capc = uint32_t(w.tmp_cap / q.C); q.tmp_cap = w.tmp_cap;
+        e = hipMemsetAsync(w.rlog, 0, (64 + kMaxCoarse + size_t(T)) * 4, s);
+        if (e != hipSuccess) return e;
+        {
+            ProfScope ps(a.prof, LMR_STAGE_BIN_SCATTER, s);
+            e = dispatch_iw(index_size, [&](auto iw) {
+                constexpr int IW = decltype(iw)::value;
+                dispatch_vb_rpt<4>(vb, frpt, [&](auto vbt, auto rpt) {
+                    constexpr int VBc = decltype(vbt)::value, R = decltype(rpt)::value;
+                    hipLaunchKernelGGL((k_coarse_free<IW, VBc, R>), dim3(unsigned(Gf)), dim3(1024), size_t(T) * 4, s, q);
+                });
+                return hipGetLastError();
+            });
+        }
+        if (e != hipSuccess) return e;
+        {
+            ProfScope ps(a.prof, LMR_STAGE_SCAN, s);
+            hipLaunchKernelGGL(k_free_tile_totals, dim3((T + 63) / 64), dim3(1024), 0, s, w.counts, T, uint32_t(Gf),
+                               w.tile_start);
+            e = scan_exclusive_u32(w.tile_start, T, w.partials, w.tile_start + T, s);
+        }
+        if (e != hipSuccess) return e;
+        {
+            ProfScope ps(a.prof, LMR_STAGE_FINE_SCATTER, s);
+            const unsigned fgrid = unsigned(fine_blocks_cap());
+            dispatch_vb_rpt<2>(vb, fine_rpt(vb), [&](auto vbt, auto rpt) {
+                constexpr int VBc = decltype(vbt)::value, R = decltype(rpt)::value;
+                hipLaunchKernelGGL((k_fine_free<VBc, R>), dim3(fgrid), dim3(1024), 0, s, q);
+            });
+            e = hipGetLastError();
+        }
+        if (e != hipSuccess) return e;
+        guard = ff_flag;
+    }
+    b.only_if = guard;
+    // behind the count-free partition the counted kernels return at once (unless it
+    // overflowed): their time is booked as one scan-stage entry, so the per-launch
+    // stage times stay those of the kernels that did the work
+    Prof* cprof = guard ? nullptr : a.prof;
+    ProfScope gscope(guard ? a.prof : nullptr, LMR_STAGE_SCAN, s);
     {
-    ProfScope ps(a.prof, LMR_STAGE_BIN_COUNT, s);
+    ProfScope ps(cprof, LMR_STAGE_BIN_COUNT, s);
     e = dispatch_iw(index_size, [&](auto iw) {
         hipLaunchKernelGGL((k_bin_count<decltype(iw)::value>), dim3(unsigned(G)), dim3(kBinBlock),
                            hist_lds, s, b);
@@ -1525,15 +1857,15 @@ hipError_t launch_apply_tiled(int dtype, int index_size, const ApplyArgs& a, con
     }
     if (e != hipSuccess) return e;
     {
-    ProfScope ps(a.prof, LMR_STAGE_SCAN, s);
-    e = scan_exclusive_u32(w.counts, num_tiles * G, w.partials, w.total, s);
+    ProfScope ps(cprof, LMR_STAGE_SCAN, s);
+    e = scan_exclusive_u32(w.counts, num_tiles * G, w.partials, w.total, s, guard);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(k_tile_starts, dim3(unsigned((num_tiles + 1 + 255) / 256)), dim3(256), 0, s,
-                       w.counts, uint32_t(num_tiles), uint32_t(G), w.total, w.tile_start);
+                       w.counts, uint32_t(num_tiles), uint32_t(G), w.total, w.tile_start, guard);
     }
     if (num_tiles > uint64_t(kFine)) {
         // two-level LDS-staged partition: coarse buckets of kFine tiles, then tiles
-        if (a.prof) prof_begin(a.prof, LMR_STAGE_BIN_SCATTER, s);
+        if (cprof) prof_begin(cprof, LMR_STAGE_BIN_SCATTER, s);
         PartArgs q{};
         q.idx = a.idx; q.idx_stride = a.idx_stride; q.val = a.val; q.val_stride = a.val_stride;
         q.n = a.n; q.shard_len = a.shard_len; q.chunk = b.chunk; q.tile_shift = shift;
@@ -1544,6 +1876,7 @@ hipError_t launch_apply_tiled(int dtype, int index_size, const ApplyArgs& a, con
         q.qpos = has_res ? w.qpos : nullptr;
         q.bin_lidx = w.bin_lidx; q.bin_val = w.bin_val; q.rpos = b.rpos;
         q.match_bits = match_rank() ? key_bits(q.C) : 0;
+        q.only_if = guard;
         if (has_res && slot_unpartition() && part_nt() == 1024) {
             const uint64_t kr_c = uint64_t(eff_rpt(4, vb, coarse_rpt(vb))) * 1024;
             const uint64_t kr_f = uint64_t(eff_rpt(2, vb, fine_rpt(vb))) * 1024;
@@ -1571,7 +1904,7 @@ hipError_t launch_apply_tiled(int dtype, int index_size, const ApplyArgs& a, con
                 });
             return hipGetLastError();
         });
-        if (a.prof) prof_end(a.prof, LMR_STAGE_BIN_SCATTER, s);
+        if (cprof) prof_end(cprof, LMR_STAGE_BIN_SCATTER, s);
         if (e != hipSuccess) return e;
         q.cg_lo = 0; q.cg_hi = q.C * uint32_t(G); q.ring_base = nullptr;
         q.match_bits = match_rank() ? key_bits(kFine) : 0;
@@ -1579,12 +1912,12 @@ hipError_t launch_apply_tiled(int dtype, int index_size, const ApplyArgs& a, con
             qf = q;
             grouped = true;
         } else {
-            ProfScope pf(a.prof, LMR_STAGE_FINE_SCATTER, s);
+            ProfScope pf(cprof, LMR_STAGE_FINE_SCATTER, s);
             launch_fine(q, vb, s);
             e = hipGetLastError();
         }
     } else {
-    ProfScope ps(a.prof, LMR_STAGE_BIN_SCATTER, s);
+    ProfScope ps(cprof, LMR_STAGE_BIN_SCATTER, s);
     e = dispatch_iw(index_size, [&](auto iw) {
         constexpr int IW = decltype(iw)::value;
         switch (vb) {
@@ -1596,6 +1929,7 @@ hipError_t launch_apply_tiled(int dtype, int index_size, const ApplyArgs& a, con
         return hipGetLastError();
     });
     }
+    gscope.end();
     }   // count-based partition
     if (e != hipSuccess) return e;
     ProfScope ps(a.prof, LMR_STAGE_TILE_APPLY, s);

@@ -202,11 +202,14 @@ hipError_t stage_records(lmr_ctx* ctx, StageSession& ss, const ApplyArgs& a, int
 // (LMR_STAGE_SPLIT=k: k regions per call); read per call, tests switch it.
 // Unset: automatic -- the piece-based (staged) partition when the segment-based
 // fine pass would see short segments (piece_partition_pays), e.g. C5's 27 M-record
-// u32 batches: fine 1.25 -> 0.83 ms; LMR_STAGED=0 keeps the segment-based path.
-uint64_t staged_mode_split(int dtype, uint64_t shard_len, uint64_t n) {
+// u32 batches: fine 1.25 -> 0.83 ms, unless the count-free partition applies (it has
+// no segments); LMR_STAGED=0 keeps the one-shot path.
+uint64_t staged_mode_split(int dtype, int op, int ret, uint64_t shard_len, uint64_t n, uint64_t cap) {
     const char* e = getenv("LMR_STAGED");
     if (e && e[0] == '0') return 0;
-    if (!e || e[0] != '1') return piece_partition_pays(dtype, shard_len, n) ? 1 : 0;
+    if (!e || e[0] != '1')
+        return (piece_partition_pays(dtype, shard_len, n) && !free_partition_applies(dtype, op, ret, shard_len, n, cap))
+                   ? 1 : 0;
     const char* k = getenv("LMR_STAGE_SPLIT");
     const long v = (k && *k) ? atol(k) : 1;
     return v < 1 ? 1 : uint64_t(v);
@@ -226,8 +229,8 @@ lmr_status_t run_apply(lmr_ctx* ctx, const lmr_apply_desc_t* d, ApplyArgs a, int
                 tiled_supported(int(d->dtype), d->shard_len);
     }
     if (!tiled) return hip_status(launch_apply_direct(int(d->dtype), iw, a, s));
-    if (const uint64_t split = staged_mode_split(int(d->dtype), d->shard_len,
-                                                 a.n < ctx->rec_cap ? a.n : ctx->rec_cap)) {
+    if (const uint64_t split = staged_mode_split(int(d->dtype), a.op, a.ret, d->shard_len,
+                                                 a.n < ctx->rec_cap ? a.n : ctx->rec_cap, ctx->rec_cap)) {
         StageSession ss;
         ss.a = a;
         ss.dtype = int(d->dtype);

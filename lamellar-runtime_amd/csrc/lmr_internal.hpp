@@ -69,16 +69,20 @@ struct TiledWs {
     uint16_t* rbase;       //                         per-round bucket offsets
     uint32_t* rts;         // staged apply: [kMaxRegions][kMaxTiles + 1] tile starts of each region
     uint32_t* sinfo;       // staged apply: piece table (pbase, bstart) + per-region in-bounds totals
-    uint32_t* rlog;        // per-round bucket cursors / counts of the partition passes (returning ops)
+    uint32_t* rlog;        // per-round bucket cursors / counts of the partition passes (returning ops);
+                           // the count-free partition's flag and fill counters otherwise
     size_t rlog_words;
+    uint64_t cap;          // records of one tiled piece (bin arrays, position maps)
+    uint64_t tmp_cap;      // records the temp arrays (tmp_idx / tmp_val) hold, > cap
 };
 size_t tiled_ws_bytes(uint64_t cap);
 TiledWs carve_tiled_ws(uint8_t* base, uint64_t cap);
 
 // exclusive scan of d[0..m) in place; *d_total = sum (may be null). partials
-// must hold ceil(m / kScanItems) entries.
+// must hold ceil(m / kScanItems) entries. only_if non-null: the launches do
+// nothing unless *only_if != 0 when they run (device-side condition).
 hipError_t scan_exclusive_u32(uint32_t* d, uint64_t m, uint32_t* partials, uint32_t* d_total,
-                              hipStream_t s);
+                              hipStream_t s, const uint32_t* only_if = nullptr);
 
 struct ApplyArgs {
     void* shard;
@@ -113,6 +117,9 @@ bool tiled_supported(int dtype, uint64_t shard_len);
 // true when the two-level partition's per-(bucket, producer block) segments of an
 // n-record piece would be short (< 8192 records) and fixed-size pieces pay
 bool piece_partition_pays(int dtype, uint64_t shard_len, uint64_t n);
+// true when a one-shot tiled piece of n records (workspace capacity cap) takes the
+// count-free partition: order-insensitive integer op, nothing returned
+bool free_partition_applies(int dtype, int op, int ret, uint64_t shard_len, uint64_t n, uint64_t cap);
 
 // Staged (deferred) tiled apply: each record stream ("region") is partitioned
 // into shard tiles on arrival, all regions are applied in one tile sweep.

@@ -36,7 +36,8 @@ __device__ __forceinline__ uint32_t block_excl_scan(uint32_t x, uint32_t* total)
 }
 
 __global__ __launch_bounds__(1024) void k_scan_reduce(const uint32_t* __restrict__ d, uint64_t m,
-                                                      uint32_t* __restrict__ partials) {
+                                                      uint32_t* __restrict__ partials, const uint32_t* only_if) {
+    if (only_if && *only_if == 0) return;
     const uint64_t base = uint64_t(blockIdx.x) * kScanItems + uint64_t(threadIdx.x) * 4;
     uint32_t s = 0;
 #pragma unroll
@@ -49,7 +50,9 @@ __global__ __launch_bounds__(1024) void k_scan_reduce(const uint32_t* __restrict
 
 // single block: exclusive scan of the partials in place, grand total to *d_total
 __global__ __launch_bounds__(1024) void k_scan_partials(uint32_t* __restrict__ partials,
-                                                        uint64_t nb, uint32_t* __restrict__ d_total) {
+                                                        uint64_t nb, uint32_t* __restrict__ d_total,
+                                                        const uint32_t* only_if) {
+    if (only_if && *only_if == 0) return;
     __shared__ uint32_t tot;
     uint32_t carry = 0;
     for (uint64_t b0 = 0; b0 < nb; b0 += 1024) {
@@ -64,7 +67,8 @@ __global__ __launch_bounds__(1024) void k_scan_partials(uint32_t* __restrict__ p
 }
 
 __global__ __launch_bounds__(1024) void k_scan_apply(uint32_t* __restrict__ d, uint64_t m,
-                                                     const uint32_t* __restrict__ partials) {
+                                                     const uint32_t* __restrict__ partials, const uint32_t* only_if) {
+    if (only_if && *only_if == 0) return;
     const uint64_t base = uint64_t(blockIdx.x) * kScanItems + uint64_t(threadIdx.x) * 4;
     uint32_t v[4];
     uint32_t s = 0;
@@ -83,15 +87,15 @@ __global__ __launch_bounds__(1024) void k_scan_apply(uint32_t* __restrict__ d, u
 }
 
 hipError_t scan_exclusive_u32(uint32_t* d, uint64_t m, uint32_t* partials, uint32_t* d_total,
-                              hipStream_t s) {
+                              hipStream_t s, const uint32_t* only_if) {
     if (m == 0) {
         if (d_total) return hipMemsetAsync(d_total, 0, sizeof(uint32_t), s);
         return hipSuccess;
     }
     uint64_t nb = (m + kScanItems - 1) / kScanItems;
-    hipLaunchKernelGGL(k_scan_reduce, dim3(unsigned(nb)), dim3(1024), 0, s, d, m, partials);
-    hipLaunchKernelGGL(k_scan_partials, dim3(1), dim3(1024), 0, s, partials, nb, d_total);
-    hipLaunchKernelGGL(k_scan_apply, dim3(unsigned(nb)), dim3(1024), 0, s, d, m, partials);
+    hipLaunchKernelGGL(k_scan_reduce, dim3(unsigned(nb)), dim3(1024), 0, s, d, m, partials, only_if);
+    hipLaunchKernelGGL(k_scan_partials, dim3(1), dim3(1024), 0, s, partials, nb, d_total, only_if);
+    hipLaunchKernelGGL(k_scan_apply, dim3(unsigned(nb)), dim3(1024), 0, s, d, m, partials, only_if);
     return hipGetLastError();
 }
 

@@ -377,7 +377,7 @@ def test_device_errors(world, lam, strategy):
         k.strategy = old
 
 
-@pytest.fixture(params=["count", "rm", "staged", "grouped", "match", "slotmap"])
+@pytest.fixture(params=["count", "free", "rm", "staged", "grouped", "match", "slotmap"])
 def partition(request, monkeypatch):
     """Two-level partition variant: count pass + bucket-major temp ("count"), the
     round-major temp with the tile counts built in the coarse pass ("rm"), or the
@@ -385,7 +385,10 @@ def partition(request, monkeypatch):
     with every call cut into 3 regions applied in one sweep ("staged"), or the count
     pass with the fine pass and tile apply run per group of coarse buckets ("grouped"), or the
     count pass with records ranked by wave key matching in the LDS rounds ("match"), or the count
-    pass with returned values brought back by slot maps and round logs ("slotmap")."""
+    pass with returned values brought back by slot maps and round logs ("slotmap"), or the
+    default selection, where order-insensitive integer ops that return nothing take the
+    count-free partition ("free"; "count" switches it off)."""
+    monkeypatch.setenv("LMR_FREE", "0" if request.param == "count" else "1")
     monkeypatch.delenv("LMR_PARTITION", raising=False)
     monkeypatch.setenv("LMR_STAGED", "0")          # the segment-based fine pass unless "staged"
     monkeypatch.delenv("LMR_GROUP_RECORDS", raising=False)
@@ -512,6 +515,78 @@ def test_two_level_out_of_bounds_fetch(world, orc, lam, partition):
     assert np.array_equal(got, exp)
     res = d_res.cpu().numpy().view(np.uint64)
     assert np.array_equal(res[good], shard0[idx[good].astype(np.int64)])
+
+
+FREE_OPS = [ADD, SUB, MUL, AND, OR, XOR]
+
+
+@pytest.mark.parametrize("shape", ["soa", "svmi", "aos"])
+@pytest.mark.parametrize("dt", ["u64", "i64", "u32", "i32", "u16", "u8", "i8"])
+def test_free_partition_collisions_bit_exact(world, orc, lam, dt, shape, monkeypatch):
+    """Count-free partition (order-insensitive integer ops, nothing returned): colliding
+    records in any order give the oracle's state bit for bit, for array values, one
+    scalar value and AoS records, next to the counted partition on the same inputs."""
+    k = world.team().kernels
+    k.reserve(1 << 22)
+    rng = np.random.default_rng(99 + CODE[dt])
+    shard_len = (1 << 22) + 777 if NP[dt](0).itemsize >= 4 else (1 << 23) + 777
+    n = 1 << 21
+    for op in FREE_OPS:
+        shard0 = rand_elems(dt, shard_len, rng, op)
+        idx = rng.integers(0, shard_len, n).astype(np.uint64)
+        vals = rand_vals(dt, n, rng, op)
+        if shape == "svmi":
+            vals[:] = vals[0]
+        for free in ("1", "0"):
+            monkeypatch.setenv("LMR_FREE", free)
+            c = Case(k, orc, lam, dt, op, shard0, idx, vals, shape, 2)
+            assert c.err == 0 and c.st_o == 0, (dt, op, free)
+            assert bits_equal(c.got, c.ref), (dt, op, shape, free)
+
+
+@pytest.mark.parametrize("dt", ["u64", "u16"])
+def test_free_partition_bucket_overflow_falls_back(world, orc, lam, dt, monkeypatch):
+    """Records concentrated on one coarse bucket (128 tiles) overflow its region in the
+    count-free partition; the counted pipeline queued behind it takes over on the
+    device, and the state is still the oracle's. Also a batch split over two buckets and
+    one with 1 % out-of-bounds records (error bit raised, the rest applied)."""
+    monkeypatch.setenv("LMR_FREE", "1")
+    k = world.team().kernels
+    k.reserve(1 << 22)
+    rng = np.random.default_rng(5)
+    t = NP[dt]
+    tile = 8192 if t(0).itemsize == 8 else 16384
+    shard_len = 640 * tile + 3                     # 641 tiles: 6 coarse buckets
+    n = 1 << 21
+    shard0 = rand_elems(dt, shard_len, rng, ADD)
+    cases = [rng.integers(0, 128 * tile, n),                                   # all in bucket 0
+             np.where(rng.random(n) < 0.5, rng.integers(0, 50, n),
+                      rng.integers(5 * 128 * tile, shard_len, n)),              # buckets 0 and 5
+             rng.integers(0, shard_len, n)]                                     # uniform
+    for j, idx in enumerate(cases):
+        idx = idx.astype(np.uint64)
+        vals = rand_vals(dt, n, rng, ADD)
+        c = Case(k, orc, lam, dt, ADD, shard0, idx, vals, "soa", 2)
+        assert c.err == 0 and c.st_o == 0, j
+        assert bits_equal(c.got, c.ref), (dt, j)
+    # out-of-bounds records
+    idx = rng.integers(0, shard_len, n).astype(np.uint64)
+    bad = rng.random(n) < 0.01
+    idx[bad] = shard_len + rng.integers(0, 99, int(bad.sum())).astype(np.uint64)
+    vals = rand_vals(dt, n, rng, ADD)
+    d_shard = to_dev(shard0)
+    old = k.strategy
+    k.strategy = 2
+    try:
+        k.apply_soa(d_shard, shard_len, 1, lam.dtype_of(dt), ADD, to_dev(idx), 8, to_dev(vals), 0, n, None, None)
+        k.synchronize()
+        assert k.errors(clear=True) & 1
+    finally:
+        k.strategy = old
+    exp = shard0.copy()
+    good = ~bad
+    np.add.at(exp, idx[good].astype(np.int64), vals[good])
+    assert bits_equal(from_dev(d_shard, dt, shard_len), exp)
 
 
 @pytest.mark.parametrize("dt", ["u64", "u32", "u16", "i8", "f64", "f32"])
