@@ -264,6 +264,12 @@ struct PartArgs {
     uint32_t* ff_tfill;           // [num_tiles] records reserved in each tile
     uint32_t capc;                // records per coarse bucket region
     uint64_t tmp_cap;             // temp arrays' capacity (records)
+    int spill;                    // 1: records beyond a full bucket region are applied to the shard
+                                  //    at once (device atomics) instead of setting ff_flag
+    int accumulate;               // 1: add this launch's tile counts to the rows (staged regions)
+    void* shard;                  // spill target
+    int op;
+    uint64_t val_bits;            // the scalar value when val is null (spilled records)
 };
 
 // coarse_off[c][g] = start of block g's coarse-c records in the temp buffer
@@ -783,7 +789,7 @@ __global__ __launch_bounds__(1024) void k_coarse_free(PartArgs p) {
             const uint64_t k = r0 + uint64_t(j) * 1024 + threadIdx.x;
             const bool in = k < hi;
             m_raw[j] = in ? load_idx<IW>(p.idx, p.idx_stride, k) : ~uint64_t(0);
-            m_val[j] = (in && p.val) ? *reinterpret_cast<const V*>(p.val + k * p.val_stride) : V(0);
+            m_val[j] = !in ? V(0) : p.val ? *reinterpret_cast<const V*>(p.val + k * p.val_stride) : V(p.val_bits);
         }
     };
     load_round(lo);
@@ -821,31 +827,38 @@ __global__ __launch_bounds__(1024) void k_coarse_free(PartArgs p) {
             s_val[q] = m_val[j];
         }
         if (threadIdx.x < C) {
-            if (cnt && rsv + cnt > p.capc) atomicOr(p.ff_flag, 1u);
-            cursor[threadIdx.x] = threadIdx.x * p.capc + rsv;
+            if (cnt && rsv + cnt > p.capc && !p.spill) atomicOr(p.ff_flag, 1u);
+            cursor[threadIdx.x] = rsv;                     // bucket-relative
         }
         if (r0 + kRound < hi) load_round(r0 + kRound);     // prefetch the next round
         __syncthreads();
-        // an overflowing bucket spills into the next region (the partition is then
-        // discarded); nothing is written past the temp arrays
-        const uint64_t lim = p.tmp_cap;
-        if (p.val)
-            bucket_writeout(hist, base, cursor, C, [&](uint32_t q, uint32_t dst) {
-                if (dst < lim) {
-                    p.tmp_idx[dst] = s_idx[q];
-                    reinterpret_cast<V*>(p.tmp_val)[dst] = s_val[q];
+        // Records past the end of their bucket's region: spill mode applies them to
+        // the shard with device atomics (the op is order-insensitive), flag mode drops
+        // them (the partition is discarded and the counted pipeline redoes it).
+        const uint32_t nw = blockDim.x >> 6, wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+        const uint32_t wpb = C >= nw ? 1u : nw / C, bstep = nw / wpb;
+        for (uint32_t c = wave / wpb; c < C; c += bstep) {
+            const uint32_t len = hist[c], b = base[c], d = cursor[c];
+            const uint64_t reg = uint64_t(c) * p.capc;
+            for (uint32_t i = (wave % wpb) * 64 + lane; i < len; i += wpb * 64) {
+                const uint32_t q = b + i;
+                if (d + i < p.capc) {
+                    p.tmp_idx[reg + d + i] = s_idx[q];
+                    if (p.tmp_val) reinterpret_cast<V*>(p.tmp_val)[reg + d + i] = s_val[q];
+                } else if (p.spill) {                       // not binned: out of the tile counts
+                    atomicSub(&th[s_idx[q] >> p.tile_shift], 1u);
+                    uint8_t ok;
+                    rmw_global<V>(reinterpret_cast<V*>(p.shard) + s_idx[q], p.op, LMR_KIND_NATIVE_ATOMIC, s_val[q],
+                                  V(0), V(0), ok, p.err);
                 }
-            });
-        else
-            bucket_writeout(hist, base, cursor, C, [&](uint32_t q, uint32_t dst) {
-                if (dst < lim) p.tmp_idx[dst] = s_idx[q];
-            });
+            }
+        }
         __syncthreads();
     }
     if (oob) raise_err(p.err, LMR_ERRBIT_OOB);
     __syncthreads();
-    for (uint32_t t = threadIdx.x; t < p.num_tiles; t += blockDim.x)
-        p.counts[uint64_t(g) * p.num_tiles + t] = th[t];   // row g (coalesced)
+    uint32_t* row = p.counts + uint64_t(g) * p.num_tiles;   // row g (coalesced)
+    for (uint32_t t = threadIdx.x; t < p.num_tiles; t += blockDim.x) row[t] = p.accumulate ? row[t] + th[t] : th[t];
 }
 
 // tile_start[t] = sum over blocks of the coarse pass's row counts (scanned after).
@@ -880,7 +893,7 @@ __global__ __launch_bounds__(1024) void k_fine_free(PartArgs p) {
     __shared__ V s_val[kRound];
     const uint32_t C = p.C;
     const uint32_t lmask = (1u << p.tile_shift) - 1u;
-    for (uint32_t c = threadIdx.x; c < C; c += blockDim.x) s_fill[c] = p.ff_fill[c];
+    for (uint32_t c = threadIdx.x; c < C; c += blockDim.x) s_fill[c] = min(p.ff_fill[c], p.capc);  // spilled: clipped
     __syncthreads();
     small_excl_scan(s_fill, s_vs, C, &s_total);        // bucket c = virtual records [s_vs[c], s_vs[c] + s_fill[c])
     __syncthreads();
@@ -2338,9 +2351,137 @@ __global__ void k_stage_plan_fill(const uint32_t* rts, uint32_t nreg, uint32_t s
     }
 }
 
+// ---- count-free staged regions (order-insensitive integer ops, nothing returned)
+// Every region's records go through k_coarse_free into the same per-bucket regions
+// of the temp arrays (fill counters and per-block tile-count rows accumulate over the
+// session); records that find their bucket region full are applied to the shard at
+// once with device atomics (spill). The finish runs the tile totals, one k_fine_free
+// over all buckets and one tile sweep: no per-region counting and no piece tables.
+constexpr uint32_t kStageFreeBlocks = 256;
+
+bool stage_free_applies(int dtype, int op, int ret, uint64_t shard_len, uint64_t cap) {
+    return free_partition_applies(dtype, op, ret, shard_len, 0, cap);
+}
+
+static PartArgs stage_free_args(int dtype, const ApplyArgs& a, const TiledWs& w) {
+    const int shift = tile_shift_for(dtype);
+    const uint32_t T = uint32_t((a.shard_len + (uint64_t(1) << shift) - 1) >> shift);
+    PartArgs q{};
+    q.shard_len = a.shard_len; q.tile_shift = shift; q.num_tiles = T;
+    q.G = kStageFreeBlocks; q.C = (T + kFine - 1) / kFine;
+    q.tile_start = w.tile_start; q.counts = w.counts;
+    q.tmp_idx = w.tmp_idx; q.tmp_val = w.tmp_val;          // values always materialised
+    q.bin_lidx = w.bin_lidx; q.bin_val = w.bin_val;
+    q.err = a.err;
+    q.ff_flag = w.rlog; q.ff_fill = w.rlog + 64; q.ff_tfill = w.rlog + 64 + kMaxCoarse;
+    q.capc = uint32_t(w.tmp_cap / q.C); q.tmp_cap = w.tmp_cap;
+    q.spill = 1; q.accumulate = 1; q.shard = a.shard; q.op = a.op;
+    return q;
+}
+
+static hipError_t stage_region_free(int dtype, int index_size, const ApplyArgs& a, const TiledWs& w,
+                                    StageSession& s, hipStream_t st) {
+    PartArgs q = stage_free_args(dtype, a, w);
+    const int vb = dtype_bytes(dtype);
+    const int frpt = free_partition_rpt(dtype, a.op, a.ret, 0, q.num_tiles, w.tmp_cap);
+    if (frpt == 0 || s.nreg >= kMaxRegions) return hipErrorInvalidValue;
+    hipError_t e;
+    if (!s.free_armed) {                                    // fill counters, flag, tile-count rows
+        e = hipMemsetAsync(w.rlog, 0, (64 + kMaxCoarse + size_t(q.num_tiles)) * 4, st);
+        if (e == hipSuccess) e = hipMemsetAsync(w.counts, 0, size_t(q.G) * q.num_tiles * 4, st);
+        if (e != hipSuccess) return e;
+        s.free_armed = true;
+    }
+    q.idx = a.idx; q.idx_stride = a.idx_stride; q.val = a.val; q.val_stride = a.val_stride;
+    q.val_bits = a.val_bits; q.n = a.n; q.chunk = (a.n + q.G - 1) / q.G;
+    {
+        ProfScope ps(a.prof, LMR_STAGE_BIN_SCATTER, st);
+        e = dispatch_iw(index_size, [&](auto iw) {
+            constexpr int IW = decltype(iw)::value;
+            dispatch_vb_rpt<4>(vb, frpt, [&](auto vbt, auto rpt) {
+                constexpr int VBc = decltype(vbt)::value, R = decltype(rpt)::value;
+                hipLaunchKernelGGL((k_coarse_free<IW, VBc, R>), dim3(q.G), dim3(1024), size_t(q.num_tiles) * 4, st, q);
+            });
+            return hipGetLastError();
+        });
+    }
+    if (e != hipSuccess) return e;
+    s.reg[s.nreg] = StageRegion{0, a.n, nullptr, nullptr};
+    s.nreg += 1;
+    s.staged += a.n;
+    return hipSuccess;
+}
+
+static hipError_t stage_finish_free(const TiledWs& w, StageSession& s, hipStream_t st) {
+    const ApplyArgs& a = s.a;
+    const int dtype = s.dtype, vb = dtype_bytes(dtype);
+    PartArgs q = stage_free_args(dtype, a, w);
+    const uint32_t T = q.num_tiles;
+    hipError_t e;
+    {
+        ProfScope ps(a.prof, LMR_STAGE_SCAN, st);
+        hipLaunchKernelGGL(k_free_tile_totals, dim3((T + 63) / 64), dim3(1024), 0, st, w.counts, T, q.G, w.tile_start);
+        e = scan_exclusive_u32(w.tile_start, T, w.partials, w.tile_start + T, st);
+    }
+    if (e != hipSuccess) return e;
+    {
+        ProfScope ps(a.prof, LMR_STAGE_FINE_SCATTER, st);
+        dispatch_vb_rpt<2>(vb, fine_rpt(vb), [&](auto vbt, auto rpt) {
+            constexpr int VBc = decltype(vbt)::value, R = decltype(rpt)::value;
+            hipLaunchKernelGGL((k_fine_free<VBc, R>), dim3(unsigned(fine_blocks_cap())), dim3(1024), 0, st, q);
+        });
+        e = hipGetLastError();
+    }
+    if (e != hipSuccess) return e;
+    {
+        ProfScope ps(a.prof, LMR_STAGE_TILE_APPLY, st);
+        const uint64_t n = s.staged;
+        const uint64_t avg = (n + T - 1) / T;
+        const uint32_t thresh = uint32_t(std::min<uint64_t>(0xFFFFFFFFull, std::max<uint64_t>(4 * avg, 65536)));
+        const unsigned pg = (T + 255) / 256;
+        hipLaunchKernelGGL(k_tile_plan_count, dim3(pg), dim3(256), 0, st, w.tile_start, T, thresh,
+                           op_combines(a.op) ? 1 : 0, w.tile_items);
+        hipLaunchKernelGGL(k_tile_plan_extra, dim3(pg), dim3(256), 0, st, w.tile_items, T, w.tile_items2);
+        e = scan_exclusive_u32(w.tile_items2, T, w.plan_partials, w.item_count, st);
+        if (e != hipSuccess) return e;
+        TileItem* items = reinterpret_cast<TileItem*>(w.items);
+        hipLaunchKernelGGL(k_tile_plan_fill, dim3(pg), dim3(256), 0, st, w.tile_start, T, w.tile_items2,
+                           w.tile_items, items, items + kMaxTiles);
+        TileArgs t;
+        t.shard = a.shard; t.shard_len = a.shard_len; t.tile_shift = q.tile_shift;
+        t.kind = a.kind; t.op = a.op; t.ret = LMR_RET_NONE;
+        t.cmp_bits = 0; t.eps_bits = 0; t.val_bits = 0;
+        t.scalar = false;                                         // values are materialised in the bins
+        t.items = items; t.delta = items + kMaxTiles; t.delta_count = w.item_count;
+        t.num_tiles = T;
+        t.bin_lidx = w.bin_lidx; t.bin_val = w.bin_val;
+        t.results = nullptr; t.ok = nullptr; t.err = a.err;
+        t.rts = nullptr; t.nreg = 0; t.rstride = 0;
+        t.tile_off = 0; t.ring_base = nullptr; t.delta_lo = nullptr; t.delta_hi = nullptr;
+        const bool delta = op_combines(a.op) && n > thresh;
+        const unsigned dgrid = unsigned(std::min<uint64_t>(2 * ((n + kSplit - 1) / kSplit), uint64_t(tile_grid_cap())));
+        e = dispatch_dtype(dtype, [&](auto tag) {
+            using Ty = decltype(tag);
+            auto go = [&](auto opt) {
+                constexpr int OPT = decltype(opt)::value;
+                hipLaunchKernelGGL((k_tile_owner<Ty, OPT>), dim3(T), dim3(1024), size_t(kTileBytes), st, t);
+                if (delta) hipLaunchKernelGGL((k_tile_delta<Ty, OPT>), dim3(dgrid), dim3(1024), size_t(kTileBytes), st, t);
+            };
+            if (a.op == LMR_OP_ADD) go(std::integral_constant<int, LMR_OP_ADD>{});
+            else go(std::integral_constant<int, -1>{});
+            return hipGetLastError();
+        });
+    }
+    s.nreg = 0;
+    s.staged = 0;
+    s.free_armed = false;
+    return e;
+}
+
 hipError_t launch_stage_region(int dtype, int index_size, const ApplyArgs& a, const TiledWs& w,
                                StageSession& s, hipStream_t st) {
     if (a.n == 0) return hipSuccess;
+    if (s.free) return stage_region_free(dtype, index_size, a, w, s, st);
     const int shift = tile_shift_for(dtype);
     const uint64_t num_tiles = (a.shard_len + (uint64_t(1) << shift) - 1) >> shift;
     if (num_tiles == 0 || num_tiles > uint64_t(kMaxTiles) || a.n > kStageMaxRegion || s.nreg >= kMaxRegions)
@@ -2424,6 +2565,7 @@ hipError_t launch_stage_region(int dtype, int index_size, const ApplyArgs& a, co
 
 hipError_t launch_stage_finish(const TiledWs& w, StageSession& s, hipStream_t st) {
     if (s.nreg == 0) return hipSuccess;
+    if (s.free) return stage_finish_free(w, s, st);
     const ApplyArgs& a = s.a;
     const int dtype = s.dtype;
     const int shift = tile_shift_for(dtype);

@@ -234,6 +234,7 @@ lmr_status_t run_apply(lmr_ctx* ctx, const lmr_apply_desc_t* d, ApplyArgs a, int
         StageSession ss;
         ss.a = a;
         ss.dtype = int(d->dtype);
+        ss.free = stage_free_applies(int(d->dtype), a.op, a.ret, d->shard_len, ctx->rec_cap);
         hipError_t e = stage_records(ctx, ss, a, int(d->dtype), iw, split, s);
         if (e == hipSuccess) e = launch_stage_finish(carve_tiled_ws(ctx->ws, ctx->rec_cap), ss, s);
         return hip_status(e);
@@ -625,6 +626,8 @@ lmr_status_t lmr_stage_begin(lmr_ctx_t* ctx, const lmr_apply_desc_t* desc) {
     S->s = StageSession();
     S->s.a = base_args(ctx, desc, nullptr, nullptr);
     S->s.a.ret = int(lmr_op_ret_kind(desc->op));     // keep the result maps for every returning op
+    S->s.free = ctx->rec_cap > 0 && stage_free_applies(int(desc->dtype), int(desc->op), S->s.a.ret,
+                                                       desc->shard_len, ctx->rec_cap);
     S->s.dtype = int(desc->dtype);
     return LMR_OK;
 }

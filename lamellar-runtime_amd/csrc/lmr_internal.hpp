@@ -134,8 +134,12 @@ struct StageSession {
     int dtype = 0;
     int nreg = 0;
     uint64_t staged = 0; // workspace slots in use
+    bool free = false;   // count-free regions (stage_free_applies): shared bucket regions, one fine pass
+    bool free_armed = false;
     StageRegion reg[kMaxRegions];
 };
+// true when a staged session of this op takes the count-free regions
+bool stage_free_applies(int dtype, int op, int ret, uint64_t shard_len, uint64_t cap);
 // partition the records of `a` into the next region (caller checks capacity:
 // s.staged + a.n <= workspace capacity, a.n <= kStageMaxRegion, s.nreg < kMaxRegions)
 hipError_t launch_stage_region(int dtype, int index_size, const ApplyArgs& a, const TiledWs& w,

@@ -690,3 +690,45 @@ def test_staged_session_collisions_many_regions(world, orc, lam):
     grp_start = np.maximum.accumulate(np.where(first, np.arange(si.size), 0))
     rank = np.arange(si.size) - grp_start
     assert np.array_equal(so, shard0[si] + rank.astype(np.uint64))
+
+
+@pytest.mark.parametrize("dt,op", [("u64", ADD), ("i32", XOR), ("u8", MUL), ("i64", SUB)])
+def test_staged_free_session_spill_and_flush(world, orc, lam, dt, op):
+    """Count-free staged regions (order-insensitive integer op, nothing returned):
+    colliding streams, the first ones all on one coarse bucket until twice its region's
+    records are staged (the rest of them are applied at once by device atomics: spill),
+    more records than the workspace holds (staged records applied in several sweeps),
+    one scalar-valued stream; exact final state against numpy's unbuffered ufunc.at."""
+    k = world.team().kernels
+    k.reserve(1 << 20)
+    R = k.reserved                                   # the workspace only grows: earlier tests may hold more
+    rng = np.random.default_rng(404 + CODE[dt])
+    t = NP[dt]
+    shard_len = (1 << 22) + 5
+    tile = 8192 if t(0).itemsize == 8 else 16384
+    C = -(-(-(-shard_len // tile)) // 128)
+    capc = (R + R // 4 + 128 * 8192) // C           # a coarse bucket's region (temp-array headroom)
+    m = 150000
+    n_skew = -(-2 * capc // m)                       # twice what bucket 0's region holds
+    n_all = max(n_skew + 8, R // m + 4)              # more than the workspace: several sweeps
+    shard0 = rand_elems(dt, shard_len, rng, op)
+    d_shard = to_dev(shard0)
+    dt_obj = lam.dtype_of(dt)
+    k.stage_begin(d_shard, shard_len, KIND_NATIVE, dt_obj, op)
+    exp = shard0.copy()
+    ufunc = {ADD: np.add, SUB: np.subtract, XOR: np.bitwise_xor, MUL: np.multiply}[op]
+    for j in range(n_all):
+        hi = 128 * tile if j < n_skew else shard_len
+        idx = rng.integers(0, hi, m).astype(np.uint64)
+        vals = rand_vals(dt, m, rng, op)
+        if j == n_skew + 1:
+            vals[:] = vals[0]
+            k.stage_soa(to_dev(idx), 8, None, dt_obj.to_bits(vals[0]), m, None, None)
+        else:
+            k.stage_soa(to_dev(idx), 8, to_dev(vals), 0, m, None, None)
+        with np.errstate(over="ignore"):
+            ufunc.at(exp, idx.astype(np.int64), vals)
+    k.stage_finish()
+    k.synchronize()
+    assert k.errors(clear=True) == 0
+    assert bits_equal(from_dev(d_shard, dt, shard_len), exp), (dt, op)
