@@ -85,7 +85,10 @@ __global__ __launch_bounds__(1024) void k_pack_count(PackK p) {
     const uint64_t hi = min(lo + p.chunk, p.n);
     const int bits = key_bits(p.npes);
     bool oob = false;
-    constexpr int U = 4;
+#ifndef LMR_PACK_COUNT_U
+#define LMR_PACK_COUNT_U 4
+#endif
+    constexpr int U = LMR_PACK_COUNT_U;
     for (uint64_t b0 = lo; b0 < hi; b0 += U * 1024) {       // block-uniform: ballots need every lane
         const uint64_t k0 = b0 + threadIdx.x;
         uint64_t g[U];

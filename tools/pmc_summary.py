@@ -16,9 +16,10 @@ import sys
 # stage -> (anchor kernels, first one present counts invocations; kernels whose bytes belong to the stage)
 STAGES = {
     "bin_count": (("k_bin_count",), ("k_bin_count",)),
-    "bin_scatter": (("k_coarse_scatter", "k_coarse_rm", "k_bin_scatter"),
-                    ("k_coarse_scatter", "k_coarse_offsets", "k_bin_scatter", "k_coarse_rm")),
-    "fine_scatter": (("k_fine_scatter", "k_fine_rm"), ("k_fine_scatter", "k_fine_rm", "k_rm_seg_sizes")),
+    "bin_scatter": (("k_coarse_free", "k_coarse_scatter", "k_coarse_rm", "k_bin_scatter"),
+                    ("k_coarse_free", "k_coarse_scatter", "k_coarse_offsets", "k_bin_scatter", "k_coarse_rm")),
+    "fine_scatter": (("k_fine_free", "k_fine_scatter", "k_fine_rm"),
+                     ("k_fine_free", "k_fine_scatter", "k_fine_rm", "k_rm_seg_sizes")),
     "tile_apply": (("k_tile_owner",), ("k_tile_owner", "k_tile_delta", "k_tile_plan_count", "k_tile_plan_extra",
                                        "k_tile_plan_fill")),
     "unpartition": (("k_tile_owner",), ("k_unpartition",)),
