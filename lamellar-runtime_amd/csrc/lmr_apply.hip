@@ -282,6 +282,7 @@ __global__ void k_coarse_offsets(PartArgs p) {
         const uint32_t c = uint32_t(i / p.G), g = uint32_t(i % p.G);
         const uint32_t t0 = c * kFine, t1 = min(t0 + kFine, p.num_tiles);
         uint32_t s = p.tile_start[t0];
+#pragma unroll 16
         for (uint32_t t = t0; t < t1; t++) s += p.fine_off[uint64_t(t) * p.G + g] - p.tile_start[t];
         p.coarse_off[i] = s;
     } else if (i == cg) {
@@ -1286,19 +1287,44 @@ __global__ __launch_bounds__(1024) void k_unpartition(const uint32_t* __restrict
     const uint64_t hi = min(lo + chunk, m);
     const V* s = reinterpret_cast<const V*>(src);
     V* d = reinterpret_cast<V*>(dst);
-    for (uint64_t k0 = lo + threadIdx.x; k0 < hi; k0 += 4 * 1024) {
-        uint32_t p[4];
+    // 8-byte values: 4 records per thread, each gathered and stored in turn; values of
+    // <= 4 bytes: 16 gathers in flight per thread before the stores (C5's u32 swap / CAS
+    // olds: 0.96 -> 0.83 ms per step same box; the same for C3's f64 olds: 0.71 -> 0.85 ms)
+    if constexpr (VB >= 8) {
+        for (uint64_t k0 = lo + threadIdx.x; k0 < hi; k0 += 4 * 1024) {
+            uint32_t p[4];
 #pragma unroll
-        for (int j = 0; j < 4; j++) {
-            const uint64_t k = k0 + uint64_t(j) * 1024;
-            p[j] = k < hi ? map[k] : 0xFFFFFFFFu;
+            for (int j = 0; j < 4; j++) {
+                const uint64_t k = k0 + uint64_t(j) * 1024;
+                p[j] = k < hi ? map[k] : 0xFFFFFFFFu;
+            }
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                if (p[j] == 0xFFFFFFFFu || p[j] >= bound) continue;
+                const uint64_t k = k0 + uint64_t(j) * 1024;
+                d[k] = s[p[j]];
+                if (ok_src) ok_dst[k] = ok_src[p[j]];
+            }
         }
+    } else {
+        constexpr int U = 16;
+        for (uint64_t k0 = lo + threadIdx.x; k0 < hi; k0 += U * 1024) {
+            uint32_t p[U];
 #pragma unroll
-        for (int j = 0; j < 4; j++) {
-            if (p[j] == 0xFFFFFFFFu || p[j] >= bound) continue;
-            const uint64_t k = k0 + uint64_t(j) * 1024;
-            d[k] = s[p[j]];
-            if (ok_src) ok_dst[k] = ok_src[p[j]];
+            for (int j = 0; j < U; j++) {
+                const uint64_t k = k0 + uint64_t(j) * 1024;
+                p[j] = k < hi ? map[k] : 0xFFFFFFFFu;
+            }
+            V v[U];
+#pragma unroll
+            for (int j = 0; j < U; j++) v[j] = (p[j] != 0xFFFFFFFFu && p[j] < bound) ? s[p[j]] : V(0);
+#pragma unroll
+            for (int j = 0; j < U; j++) {
+                if (p[j] == 0xFFFFFFFFu || p[j] >= bound) continue;
+                const uint64_t k = k0 + uint64_t(j) * 1024;
+                d[k] = v[j];
+                if (ok_src) ok_dst[k] = ok_src[p[j]];
+            }
         }
     }
 }
