@@ -52,7 +52,7 @@ def parse():
     p.add_argument("--records-log2", type=int, default=None)
     p.add_argument("--elems-log2", type=int, default=None)
     p.add_argument("--strategy", default=os.environ.get("LAMELLAR_OP_STRATEGY", "auto"))
-    p.add_argument("--cpu-threads", type=int, default=16)
+    p.add_argument("--cpu-threads", type=int, default=0, help="0: every core this process may run on")
     p.add_argument("--cpu-sample-log2", type=int, default=24)
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-verify", action="store_true")
@@ -212,7 +212,66 @@ class MixedU32(Workload):
         a.batch_compare_exchange(i4, 0, v4).spawn()
 
     def verify(self, nsteps):
-        return None
+        """One more step with every result captured, checked on a sample of elements
+        (global index % 1021 == 0, about 1 in 1000): bit_and / bit_or / bit_xor final
+        states against the oracle's serial replay, swap olds and compare_exchange
+        Results against the linearisability checker (per element, one serial order of
+        that element's records from every PE). Records of every PE that hit a sampled
+        element are gathered on every PE."""
+        from oracle import oracle as orc
+        a, dev = self.arr, self.dev
+        P = 1021
+        lo = self.me * self.elems
+        g_local = torch.arange(lo, lo + self.elems, device=dev)
+        loc = torch.nonzero(g_local % P == 0).flatten()
+        mine_g = (g_local[loc]).cpu().numpy().astype(np.uint64)
+        ops = [(10, "batch_bit_and"), (12, "batch_bit_or"), (14, "batch_bit_xor"), (18, "batch_swap"),
+               (21, "batch_compare_exchange")]
+        per_batch = []
+        for (op, fn), (i, v) in zip(ops, self.parts):
+            before = a.local_data()[loc].cpu().numpy().view(np.uint32)
+            h = getattr(a, fn)(i, 0, v) if op == 21 else getattr(a, fn)(i, v)
+            r = h.block()
+            after = a.local_data()[loc].cpu().numpy().view(np.uint32)
+            sel = torch.nonzero(i % P == 0).flatten()
+            rec_i = i[sel].cpu().numpy().astype(np.uint64)
+            rec_v = v[sel].cpu().numpy().view(np.uint32)
+            rec_r = rec_ok = None
+            if op == 18:
+                rec_r = r[sel].cpu().numpy().view(np.uint32)
+            elif op == 21:
+                rec_r = r.vals[sel].cpu().numpy().view(np.uint32)
+                rec_ok = r.ok[sel].cpu().numpy()
+            per_batch.append((mine_g, before, after, rec_i, rec_v, rec_r, rec_ok))
+        parts = [per_batch]
+        if self.npes > 1:
+            import torch.distributed as dist
+            parts = [None] * self.npes
+            dist.all_gather_object(parts, per_batch)
+        u32 = np.uint32
+        for b, (op, fn) in enumerate(ops):
+            g = np.concatenate([pp[b][0] for pp in parts])
+            order = np.argsort(g)
+            g = g[order]
+            before = np.concatenate([pp[b][1] for pp in parts])[order]
+            after = np.concatenate([pp[b][2] for pp in parts])[order]
+            ri = np.concatenate([pp[b][3] for pp in parts])
+            rv = np.concatenate([pp[b][4] for pp in parts])
+            pos = np.searchsorted(g, ri).astype(np.uint64)           # compact element of each record
+            if op in (10, 12, 14):
+                ref = before.copy()
+                L = orc.layout_new(g.size, 1, 0, 0)
+                st, _, _ = orc.batch_op(L, [ref], 1, 2, u32, op, pos, rv)
+                if st != 0 or not np.array_equal(ref, after):
+                    return False
+            else:
+                rr = np.concatenate([pp[b][5] for pp in parts])
+                ok = np.concatenate([pp[b][6] for pp in parts]).astype(np.uint8) if op == 21 else None
+                st, _ = orc.check_linearizable(1, 2, u32, op, before, after, pos, rv, rr, ok,
+                                               current=u32(0) if op == 21 else None)
+                if st != 0:
+                    return False
+        return True
 
     def describe(self):
         a = self.args
@@ -231,33 +290,113 @@ def _allsum(npes, t):
     return int(t.item())
 
 
-def cpu_baseline(args, elems_log2):
-    """Reference-structured CPU apply on a bounded sample (C2 shape, same shard size)."""
+def cpu_threads():
+    """Logical cores this process may use: the box's CPU share per GPU where the
+    environment states it (OMP_NUM_THREADS, 16 on the GPU pool, which asks worker pools
+    to stay within it), else the affinity mask. os.cpu_count() (the whole machine) is
+    recorded beside it."""
+    try:
+        n = len(os.sched_getaffinity(0))
+    except AttributeError:
+        n = os.cpu_count() or 1
+    share = os.environ.get("OMP_NUM_THREADS")
+    if share and share.isdigit() and int(share) > 0:
+        n = min(n, int(share))
+    return n
+
+
+def _timed(orc, reps, run):
+    run(True)                                              # warm-up (page-in, thread spin-up)
+    ts = sorted(run(False) for _ in range(reps))
+    return ts[len(ts) // 2], ts
+
+
+def cpu_baseline(args, cfg):
+    """The reference-structured threaded CPU apply (oracle/cpu_baseline.c: op buffers
+    of am_size_threshold = 100 kB packed by T/4 threads, applied by T threads with
+    SeqCst atomics / CAS loops (NativeAtomic) or a lock per element (GenericAtomic,
+    generic_atomic.rs:286-293)) on bounded samples of the workload, median of 10
+    (BASELINE.md). The primary line uses every core this process may run on; extra
+    lines: T = 4 (the reference's test setting, tests/add.rs:35), and C1 (configs[0],
+    the add_test pattern on 1M u64 elements) batched and as per-element 1x1 ops."""
     from oracle import oracle as orc
-    n = 1 << args.cpu_sample_log2
-    shard_len = 1 << elems_log2
-    threads = max(1, min(args.cpu_threads, os.cpu_count() or 1))
+    T = args.cpu_threads or cpu_threads()
     rng = np.random.default_rng(0x1A3E11A2)
-    gidx = rng.integers(0, shard_len, n, dtype=np.uint64)
-    vals = rng.integers(0, 2**63, n, dtype=np.uint64)
-    shard = np.zeros(shard_len, dtype=np.uint64)
-    orc.cpu_baseline(3, np.uint64, 0, shard, gidx[:1 << 16], vals[:1 << 16], threads)  # warm
-    best = None
-    for _ in range(2):
-        st, t, _ = orc.cpu_baseline(3, np.uint64, 0, shard, gidx, vals, threads)
-        assert st == 0
-        if best is None or t.total_s < best.total_s:
-            best = t
-    return {
-        "value": n / best.total_s,
-        "unit": "ops/s",
-        "cores": threads,
-        "kind": "port",
-        "sample": (f"2^{args.cpu_sample_log2} u64 add records, uniform over a 2^{elems_log2}-element "
-                   f"shard, packed into 100 kB op buffers by {max(1, threads // 4)} threads and "
-                   f"applied with SeqCst atomics by {threads} threads (best of 2; pack "
-                   f"{best.pack_s * 1e3:.0f} ms + apply {best.apply_s * 1e3:.0f} ms)"),
-    }
+    out = {}
+
+    def one(dtype, npt, op, shard_len, gidx, vals, threads, reps, threshold=100000, results=False, cur=None,
+            init=None):
+        shard = np.zeros(shard_len, dtype=npt) if init is None else init
+
+        def run(warm):
+            n = (1 << 16) if warm else gidx.size
+            st, t, _ = orc.cpu_baseline(dtype, npt, op, shard, gidx[:n], vals if np.ndim(vals) == 0 else vals[:n],
+                                        threads, threshold, want_results=results, current=cur)
+            assert st == 0
+            return t.total_s
+        med, ts = _timed(orc, reps, run)
+        return gidx.size / med, med, ts
+
+    if cfg in ("c2", "c4"):
+        el = 1 << (args.elems_log2 or 26)
+        n = 1 << args.cpu_sample_log2
+        gidx = rng.integers(0, el, n, dtype=np.uint64)
+        vals = rng.integers(0, 2**63, n, dtype=np.uint64)
+        v, med, _ = one(3, np.uint64, 0, el, gidx, vals, T, 10)
+        out["primary"] = {"value": v, "unit": "ops/s", "cores": T, "kind": "port",
+                          "sample": f"C2 shape: 2^{args.cpu_sample_log2} u64 add records uniform over a "
+                                    f"2^{args.elems_log2 or 26}-element shard, 100 kB op buffers packed by "
+                                    f"{max(1, T // 4)} threads, applied with SeqCst atomics by {T} threads "
+                                    f"(median of 10: {med * 1e3:.0f} ms; the box's CPU share; os.cpu_count() = "
+                                    f"{os.cpu_count()})"}
+        n4 = n >> 2
+        v4, med4, _ = one(3, np.uint64, 0, el, gidx[:n4], vals[:n4], 4, 10)
+        out["extra"] = [{"value": v4, "unit": "ops/s", "cores": 4, "kind": "port",
+                         "sample": f"C2 shape, T = 4 (tests/add.rs:35), 2^{args.cpu_sample_log2 - 2} records, "
+                                   f"median of 10 ({med4 * 1e3:.0f} ms)"}]
+        # C1: add_test pattern, 1M-element u64 array, every element updated 50 times, batch_add(indices, 1)
+        c1_el = 1000000
+        c1_idx = np.tile(np.arange(c1_el, dtype=np.uint64), 8)
+        rng.shuffle(c1_idx)
+        v1, med1, _ = one(3, np.uint64, 0, c1_el, c1_idx, np.uint64(1), T, 5)
+        out["extra"].append({"value": v1, "unit": "ops/s", "cores": T, "kind": "port",
+                             "sample": f"C1 (configs[0]): batch_add(indices, 1) on a 1M-element u64 array, 8 "
+                                       f"shuffled updates per element (8M ops), SVMI op buffers, median of 5 "
+                                       f"({med1 * 1e3:.0f} ms)"})
+        n11 = 1 << 18
+        v11, med11, _ = one(3, np.uint64, 0, c1_el, c1_idx[:n11], np.uint64(1), T, 5, threshold=1)
+        out["extra"].append({"value": v11, "unit": "ops/s", "cores": T, "kind": "port",
+                             "sample": f"C1 as add_test issues it: per-element add(idx, 1), one 1-record op "
+                                       f"buffer per op (2^18 ops; a lower bound on the reference's per-AM "
+                                       f"cost), median of 5 ({med11 * 1e3:.0f} ms)"})
+    elif cfg == "c3":
+        el = 1 << (args.elems_log2 or 24)
+        n = 1 << 22
+        ranks = np.arange(1, el + 1, dtype=np.float64)
+        cdf = np.cumsum(ranks ** -0.99)
+        cdf /= cdf[-1]
+        gidx = rng.permutation(el)[np.minimum(np.searchsorted(cdf, rng.random(n)), el - 1)].astype(np.uint64)
+        vals = np.ones(n, dtype=np.float64)
+        v, med, _ = one(9, np.float64, 1, el, gidx, vals, T, 10, results=True)
+        out["primary"] = {"value": v, "unit": "ops/s", "cores": T, "kind": "port",
+                          "sample": f"C3 shape: 2^22 f64 fetch_add records, Zipf(0.99) over 2^"
+                                    f"{args.elems_log2 or 24} elements, GenericAtomic per-element locks, olds "
+                                    f"returned, {T} threads (median of 10: {med * 1e3:.0f} ms)"}
+    elif cfg == "c5":
+        el = 1 << (args.elems_log2 or 26)
+        m = 1 << 21
+        tot = 0.0
+        for op in (10, 12, 14, 18, 21):
+            gidx = rng.integers(0, el, m, dtype=np.uint64)
+            vals = rng.integers(0, 2**32, m, dtype=np.uint64).astype(np.uint32)
+            _, med, _ = one(2, np.uint32, op, el, gidx, vals, T, 10, results=op in (18, 21),
+                            cur=np.uint32(0) if op == 21 else None)
+            tot += med
+        out["primary"] = {"value": 5 * m / tot, "unit": "ops/s", "cores": T, "kind": "port",
+                          "sample": f"C5 shape: u32 bit_and/bit_or/bit_xor/swap/compare_exchange, 2^21 records "
+                                    f"each uniform over 2^{args.elems_log2 or 26} elements, SeqCst atomics, "
+                                    f"{T} threads (sum of per-op medians of 10: {tot * 1e3:.0f} ms)"}
+    return out
 
 
 def main():
@@ -303,30 +442,45 @@ def main():
     value = npes * W.ops_per_step * args.steps / elapsed
     verified = None if args.no_verify else W.verify(args.warmup + args.steps)
 
-    # ---- roofline of the dominant kernel ----
+    # ---- roofline: the whole op path against HBM ----
+    # achieved = B_op (the survey's algorithmic bytes per op: packed record + element
+    # read/write (+ returned value)) x ops per step / the step time; frac against the
+    # 8.0 TB/s HBM3E spec. Per-stage figures (each kernel's own algorithmic bytes over
+    # its HIP-event launch time) live in apply_pipeline.stages.
     iw = 8 if npes == 1 else W.arr.index_size()
     per = {}
     for name, (ms, cnt) in stages.items():
         if cnt:
             per[name] = (ms / cnt, cnt / args.steps)
-    dom = max(per, key=lambda s: per[s][0] * per[s][1]) if per else None
-    roof = None
-    if dom:
-        avg_ms, launches_per_step = per[dom]
-        ops_per_launch = W.ops_per_step / launches_per_step
-        bpo = stage_bytes_per_op(dom, iw, W.vb, W.eb, ops_per_launch, W.elems, W.fetch)
-        achieved = bpo * ops_per_launch / (avg_ms * 1e-3)
-        roof = {"bound": "hbm", "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
-                "frac": achieved / HBM_PEAK, "traffic": None, "kernel": dom,
-                "bytes_per_op": bpo, "avg_launch_ms": avg_ms}
-        pmc = os.path.join(ROOT, "profiles", f"pmc_traffic_{cfg}.json")
-        if os.path.exists(pmc):
-            tr = json.load(open(pmc)).get(dom)
-            if tr:
-                roof["traffic"] = tr
-    apply_stages = [s for s in ("direct", "mvsi", "bin_count", "scan", "bin_scatter", "fine_scatter",
-                                "tile_apply", "unpartition") if s in per]
-    apply_ms = sum(per[s][0] * per[s][1] for s in apply_stages)
+    step_s = ms_per_step * 1e-3
+    achieved = W.survey_bpo * W.ops_per_step / step_s
+    traffic = None
+    pmc = os.path.join(ROOT, "profiles", f"pmc_traffic_{cfg}.json")
+    if os.path.exists(pmc) and per:
+        tr = json.load(open(pmc))
+        if all(st in tr for st in per if st not in ("scan",)):
+            traffic = sum(tr.get(st, 0.0) * per[st][1] for st in per)
+    dom = max(per, key=lambda st: per[st][0] * per[st][1]) if per else None
+    roof = {"bound": "hbm", "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
+            "frac": achieved / HBM_PEAK, "traffic": traffic,
+            "traffic_source": ("HBM bytes per step: committed rocprofv3 FETCH_SIZE/WRITE_SIZE passes "
+                               f"(profiles/pmc_traffic_{cfg}.json, FETCH_SIZE x2 per the gfx950 note) x launches "
+                               "per step of this run; not measured in this run") if traffic else None,
+            "scope": "whole step (every kernel of the op path), SURVEY 8(d) bytes per op",
+            "bytes_per_op": W.survey_bpo, "ops_per_step": W.ops_per_step, "dominant_kernel": dom}
+    stage_rows = {}
+    for st, (avg_ms, lps) in per.items():
+        ops_per_launch = W.ops_per_step / lps
+        bpo = stage_bytes_per_op(st, iw, W.vb, W.eb, ops_per_launch, W.elems, W.fetch)
+        row = {"ms_per_step": avg_ms * lps, "launches_per_step": lps, "avg_launch_ms": avg_ms,
+               "bytes_per_op": bpo}
+        if bpo:
+            row["achieved_GBps"] = bpo * ops_per_launch / (avg_ms * 1e-3) / 1e9
+            row["frac"] = row["achieved_GBps"] * 1e9 / HBM_PEAK
+        stage_rows[st] = row
+    apply_stages = [st for st in ("direct", "mvsi", "bin_count", "scan", "bin_scatter", "fine_scatter",
+                                  "tile_apply", "unpartition", "pack", "scatter_results") if st in per]
+    apply_ms = sum(per[st][0] * per[st][1] for st in apply_stages)
 
     out = {
         "metric": METRIC,
@@ -350,18 +504,20 @@ def main():
             "parallelism": f"{npes} PE(s), one per GPU",
         },
         "roofline": roof,
-        "apply_pipeline": {"stages_ms_per_step": {s: per[s][0] * per[s][1] for s in per},
-                           "apply_ms_per_step": apply_ms,
-                           "survey_bytes_per_op": W.survey_bpo,
-                           "survey_frac": (W.survey_bpo * W.ops_per_step / (apply_ms * 1e-3) / HBM_PEAK)
+        "apply_pipeline": {"stages": stage_rows,
+                           "device_ms_per_step": apply_ms,
+                           "frac_of_device_time": (W.survey_bpo * W.ops_per_step / (apply_ms * 1e-3) / HBM_PEAK)
                            if apply_ms else None},
         "verified": verified,
         "cpu_baseline": None,
     }
     if args.e2e and cfg in ("c2", "c4"):
         out["e2e"] = e2e(lam, team, W, args)
-    if me == 0 and npes == 1 and not args.no_cpu_baseline and cfg == "c2":
-        out["cpu_baseline"] = cpu_baseline(args, args.elems_log2 or 26)
+    if me == 0 and npes == 1 and not args.no_cpu_baseline:
+        cb = cpu_baseline(args, cfg)
+        out["cpu_baseline"] = cb.get("primary")
+        if cb.get("extra"):
+            out["cpu_baselines_extra"] = cb["extra"]
     if me == 0:
         print(json.dumps(out), flush=True)
     import torch.distributed as dist

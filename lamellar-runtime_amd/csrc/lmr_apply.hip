@@ -138,12 +138,10 @@ struct BinArgs {
     uint8_t* bin_val;
     uint32_t* rpos;        // [n] record k -> binned position (~0 = out of bounds); null when nothing is returned
     uint32_t* err;
-    const uint32_t* only_if;  // non-null: the kernel runs only when *only_if != 0
 };
 
 template <int IW>
 __global__ __launch_bounds__(kBinBlock) void k_bin_count(BinArgs b) {
-    if (b.only_if && *b.only_if == 0) return;
     extern __shared__ uint32_t hist[];
     for (uint32_t t = threadIdx.x; t < b.num_tiles; t += blockDim.x) hist[t] = 0;
     __syncthreads();
@@ -196,8 +194,7 @@ __global__ __launch_bounds__(kBinBlock) void k_bin_scatter(BinArgs b) {
 }
 
 __global__ void k_tile_starts(const uint32_t* counts, uint32_t num_tiles, uint32_t G,
-                              const uint32_t* total, uint32_t* tile_start, const uint32_t* only_if) {
-    if (only_if && *only_if == 0) return;
+                              const uint32_t* total, uint32_t* tile_start) {
     uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
     if (t < num_tiles) tile_start[t] = counts[uint64_t(t) * G];
     if (t == num_tiles) tile_start[t] = *total;
@@ -238,34 +235,15 @@ struct PartArgs {
     uint16_t* bin_lidx;
     uint8_t* bin_val;
     uint32_t* rpos;               // [total] temp position -> binned position; null: no results
-    // round-major partition (k_coarse_rm / k_fine_rm)
-    uint32_t* counts;             // [num_tiles][G] per-block tile counts (written by k_coarse_rm)
-    uint16_t* rhist;              // [n/kRmRound rows][C] per-round bucket counts
-    uint16_t* rbase;              // [rows][C] per-round bucket offsets inside the round region
-    uint32_t R;                   // rounds per full block (chunk / kRmRound)
+    uint32_t* counts;             // count-free partition: [G][num_tiles] per-block tile count rows
     uint32_t* err;
-    // grouped fine pass (k_fine_scatter): segments [cg_lo, cg_hi) only, bins written
-    // at (final position - *ring_base) so a group's bins reuse the start of the bin buffer
-    uint32_t cg_lo, cg_hi;
-    const uint32_t* ring_base;    // null: 0
-    int match_bits;               // > 0: rank by wave key matching on that many bucket bits
-    // slot maps (two-level count path, returning ops): instead of qpos / rpos positions the
-    // coarse pass stores each record's LDS slot in its round (qslot[k]) and logs every
-    // round's bucket cursors and counts (clog), the fine pass likewise (rslot[temp], flog);
-    // k_uncoarse / k_unfine rebuild each round in LDS from contiguous runs (see there)
-    uint16_t* qslot;
-    uint32_t* clog;
-    uint16_t* rslot;
-    uint32_t* flog;
-    // count-free partition (k_coarse_free / k_fine_free) and its counted fallback
-    const uint32_t* only_if;      // non-null: the kernel runs only when *only_if != 0
-    uint32_t* ff_flag;            // set when a coarse bucket overflows its region
+    // count-free partition (k_coarse_free / k_fine_free)
     uint32_t* ff_fill;            // [C] records reserved in each coarse bucket's region
     uint32_t* ff_tfill;           // [num_tiles] records reserved in each tile
     uint32_t capc;                // records per coarse bucket region
     uint64_t tmp_cap;             // temp arrays' capacity (records)
     int spill;                    // 1: records beyond a full bucket region are applied to the shard
-                                  //    at once (device atomics) instead of setting ff_flag
+                                  //    at once (device atomics); 0: they are dropped (never used)
     int accumulate;               // 1: add this launch's tile counts to the rows (staged regions)
     void* shard;                  // spill target
     int op;
@@ -275,7 +253,6 @@ struct PartArgs {
 // coarse_off[c][g] = start of block g's coarse-c records in the temp buffer
 //                  = tile_start[c*kFine] + sum_{t in c} (fine_off[t][g] - tile_start[t])
 __global__ void k_coarse_offsets(PartArgs p) {
-    if (p.only_if && *p.only_if == 0) return;
     const uint64_t i = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
     const uint64_t cg = uint64_t(p.C) * p.G;
     if (i < cg) {
@@ -313,11 +290,10 @@ __device__ __forceinline__ void small_excl_scan(const uint32_t* hist, uint32_t* 
 // into registers right after the current round is staged in LDS, so they are
 // in flight while the staged round is written out.
 // RPT records per thread per round (kRound = RPT * 1024 records staged in LDS).
-template <int IW, int VB, int RPT, int NT>
-__global__ __launch_bounds__(NT) void k_coarse_scatter(PartArgs p) {
-    if (p.only_if && *p.only_if == 0) return;
+template <int IW, int VB, int RPT>
+__global__ __launch_bounds__(1024) void k_coarse_scatter(PartArgs p) {
     using V = typename idx_t<VB>::I;
-    constexpr uint32_t kRound = RPT * NT;
+    constexpr uint32_t kRound = RPT * 1024;
     __shared__ uint32_t hist[kMaxCoarse], base[kMaxCoarse], cursor[kMaxCoarse], tot;
     __shared__ uint32_t s_idx[kRound];
     __shared__ V s_val[kRound];
@@ -331,7 +307,7 @@ __global__ __launch_bounds__(NT) void k_coarse_scatter(PartArgs p) {
     auto load_round = [&](uint64_t r0) {
 #pragma unroll
         for (int j = 0; j < RPT; j++) {
-            const uint64_t k = r0 + uint64_t(j) * NT + threadIdx.x;
+            const uint64_t k = r0 + uint64_t(j) * 1024 + threadIdx.x;
             const bool in = k < hi;
             m_raw[j] = in ? load_idx<IW>(p.idx, p.idx_stride, k) : ~uint64_t(0);
             m_val[j] = (in && p.val) ? *reinterpret_cast<const V*>(p.val + k * p.val_stride) : V(0);
@@ -347,32 +323,22 @@ __global__ __launch_bounds__(NT) void k_coarse_scatter(PartArgs p) {
         for (int j = 0; j < RPT; j++) {
             m_ok[j] = m_raw[j] < p.shard_len;
             m_c[j] = m_ok[j] ? uint32_t(m_raw[j] >> cshift) : 0u;
-            if (p.match_bits) m_rank[j] = wave_match_rank(hist, m_c[j], m_ok[j], p.match_bits);
-            else if (m_ok[j]) m_rank[j] = atomicAdd(&hist[m_c[j]], 1u);
+            if (m_ok[j]) m_rank[j] = atomicAdd(&hist[m_c[j]], 1u);
         }
         __syncthreads();
         small_excl_scan(hist, base, C, &tot);
         __syncthreads();
 #pragma unroll
         for (int j = 0; j < RPT; j++) {
-            const uint64_t k = r0 + uint64_t(j) * NT + threadIdx.x;
+            const uint64_t k = r0 + uint64_t(j) * 1024 + threadIdx.x;
             if (!m_ok[j]) {
                 if (p.qpos && k < hi) p.qpos[k] = 0xFFFFFFFFu;
-                if (p.qslot && k < hi) p.qslot[k] = 0xFFFFu;
                 continue;
             }
             const uint32_t q = base[m_c[j]] + m_rank[j];
             s_idx[q] = uint32_t(m_raw[j]);
             s_val[q] = m_val[j];
             if (p.qpos) p.qpos[k] = cursor[m_c[j]] + m_rank[j];   // coalesced in k
-            if (p.qslot) p.qslot[k] = uint16_t(q);
-        }
-        if (p.clog) {                                          // this round's runs, for k_uncoarse
-            uint32_t* lg = p.clog + (uint64_t(r0 / kRound) + g) * 2 * C;
-            for (uint32_t c = threadIdx.x; c < C; c += blockDim.x) {
-                lg[c] = cursor[c];
-                lg[C + c] = hist[c];
-            }
         }
         if (r0 + kRound < hi) load_round(r0 + kRound);     // prefetch the next round
         __syncthreads();
@@ -388,261 +354,24 @@ __global__ __launch_bounds__(NT) void k_coarse_scatter(PartArgs p) {
     }
 }
 
-// ---- round-major two-level partition (no count pass) -------------------------
-// k_coarse_rm: block g reads its chunk (a multiple of kRmRound records) in rounds;
-// each round is counting-sorted by coarse bucket in LDS and written as ONE
-// contiguous bucket-sorted region at the round's own input position (fully
-// coalesced stores, no global offsets needed), with the round's bucket counts /
-// offsets (u16) beside it. The per-(tile, block) counts the fine pass needs are
-// built on the way in LDS (packed u16 pairs, flushed every 15 rounds so they
-// never overflow): the separate count pass over the input is gone.
-// k_fine_rm: segment (c, g) = bucket c's piece of every round of block g; a
-// piece table (prefix of piece lengths) maps the segment's flat record index to
-// its temp slot, and the tile sort / output is that of k_fine_scatter.
-constexpr uint32_t kRmRound = 4096;
-constexpr uint32_t kRmMaxRounds = 128;     // piece tables are scanned by one wave (<= 128 entries)
-constexpr int kRmFlush = 15;               // rounds between u16 tile-counter flushes (15 * 4096 < 65536)
-
-// block copy of `total` LDS elements to 16-B-aligned global memory, 16 bytes per lane
-template <typename T>
-__device__ __forceinline__ void copy_out_16(const T* lds, T* g, uint32_t total) {
-    constexpr uint32_t per = 16 / sizeof(T);
-    const uint32_t nv = total / per;
-    const uint4* src = reinterpret_cast<const uint4*>(lds);
-    uint4* dst = reinterpret_cast<uint4*>(g);
-    for (uint32_t v = threadIdx.x; v < nv; v += blockDim.x) dst[v] = src[v];
-    for (uint32_t q = nv * per + threadIdx.x; q < total; q += blockDim.x) g[q] = lds[q];
-}
-
-template <int IW, int VB>
-__global__ __launch_bounds__(1024, 8) void k_coarse_rm(PartArgs p) {
-    using V = typename idx_t<VB>::I;
-    constexpr int RPT = kRmRound / 1024;
-    extern __shared__ uint32_t th[];                         // packed u16 tile counters
-    __shared__ uint32_t hist[kMaxCoarse], base[kMaxCoarse], tot;
-    __shared__ __align__(16) uint32_t s_idx[kRmRound];
-    __shared__ __align__(16) V s_val[kRmRound];
-    const uint32_t g = blockIdx.x, C = p.C;
-    const int cshift = p.tile_shift + kFineShift;
-    const uint32_t nw = (p.num_tiles + 1) >> 1;
-    for (uint32_t i = threadIdx.x; i < nw; i += blockDim.x) th[i] = 0;
-    const uint64_t lo = uint64_t(g) * p.chunk;
-    const uint64_t hi = min(lo + p.chunk, p.n);
-    uint64_t m_raw[RPT];
-    V m_val[RPT];
-    auto load_round = [&](uint64_t r0) {
-#pragma unroll
-        for (int j = 0; j < RPT; j++) {
-            const uint64_t k = r0 + uint64_t(j) * 1024 + threadIdx.x;
-            const bool in = k < hi;
-            m_raw[j] = in ? load_idx<IW>(p.idx, p.idx_stride, k) : ~uint64_t(0);
-            m_val[j] = (in && p.val) ? *reinterpret_cast<const V*>(p.val + k * p.val_stride) : V(0);
-        }
-    };
-    bool flushed = false;
-    auto flush = [&]() {
-        for (uint32_t i = threadIdx.x; i < nw; i += blockDim.x) {
-            const uint32_t x = th[i];
-            th[i] = 0;
-            const uint32_t t0 = 2 * i;
-            uint32_t* c0 = p.counts + uint64_t(t0) * p.G + g;
-            *c0 = (flushed ? *c0 : 0u) + (x & 0xFFFFu);
-            if (t0 + 1 < p.num_tiles) {
-                uint32_t* c1 = p.counts + uint64_t(t0 + 1) * p.G + g;
-                *c1 = (flushed ? *c1 : 0u) + (x >> 16);
-            }
-        }
-        flushed = true;
-    };
-    load_round(lo);
-    bool oob = false;
-    uint32_t r = 0;
-    for (uint64_t r0 = lo; r0 < hi; r0 += kRmRound, r++) {
-        for (uint32_t c = threadIdx.x; c < C; c += blockDim.x) hist[c] = 0;
-        __syncthreads();
-        uint32_t m_rank[RPT], m_c[RPT];
-        bool m_ok[RPT];
-#pragma unroll
-        for (int j = 0; j < RPT; j++) {
-            const bool in = r0 + uint64_t(j) * 1024 + threadIdx.x < hi;
-            m_ok[j] = m_raw[j] < p.shard_len;
-            oob |= in && !m_ok[j];
-            m_c[j] = uint32_t(m_raw[j] >> cshift);
-            if (m_ok[j]) {
-                m_rank[j] = atomicAdd(&hist[m_c[j]], 1u);
-                const uint32_t t = uint32_t(m_raw[j] >> p.tile_shift);
-                atomicAdd(&th[t >> 1], 1u << ((t & 1u) * 16));
-            }
-        }
-        __syncthreads();
-        small_excl_scan(hist, base, C, &tot);
-        __syncthreads();
-#pragma unroll
-        for (int j = 0; j < RPT; j++) {
-            const uint64_t k = r0 + uint64_t(j) * 1024 + threadIdx.x;
-            if (!m_ok[j]) {
-                if (p.qpos && k < hi) p.qpos[k] = 0xFFFFFFFFu;
-                continue;
-            }
-            const uint32_t q = base[m_c[j]] + m_rank[j];
-            s_idx[q] = uint32_t(m_raw[j]);
-            s_val[q] = m_val[j];
-            if (p.qpos) p.qpos[k] = uint32_t(r0) + q;               // coalesced in k
-        }
-        if (r0 + kRmRound < hi) load_round(r0 + kRmRound);        // prefetch the next round
-        const uint64_t row = (r0 / kRmRound) * C;
-        for (uint32_t c = threadIdx.x; c < C; c += blockDim.x) {
-            p.rhist[row + c] = uint16_t(hist[c]);
-            p.rbase[row + c] = uint16_t(base[c]);
-        }
-        __syncthreads();
-        const uint32_t total = tot;
-        // the round's region starts at input position r0 (a multiple of kRmRound): 16-B aligned
-        copy_out_16(s_idx, p.tmp_idx + r0, total);
-        if (p.val) copy_out_16(s_val, reinterpret_cast<V*>(p.tmp_val) + r0, total);
-        if ((r % kRmFlush) == kRmFlush - 1 || r0 + kRmRound >= hi) flush();
-        __syncthreads();
-    }
-    if (oob) raise_err(p.err, LMR_ERRBIT_OOB);
-}
-
-// segment sizes in (c, g) order: seg[c*G + g] = sum over block g's rounds of rhist[.][c]
-__global__ void k_rm_seg_sizes(PartArgs p, uint32_t* seg) {
-    const uint64_t i = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
-    const uint64_t cg = uint64_t(p.C) * p.G;
-    if (i < cg) {
-        const uint32_t c = uint32_t(i / p.G), g = uint32_t(i % p.G);
-        const uint64_t lo = uint64_t(g) * p.chunk, hi = min(lo + p.chunk, p.n);
-        const uint32_t nr = uint32_t((hi - lo + kRmRound - 1) / kRmRound);
-        const uint64_t row0 = lo / kRmRound;
-        uint32_t s = 0;
-        for (uint32_t r = 0; r < nr; r++) s += p.rhist[(row0 + r) * p.C + c];
-        seg[i] = s;
-    } else if (i == cg) {
-        seg[i] = 0;
-    }
-}
-
-template <int VB>
-__global__ __launch_bounds__(1024, 8) void k_fine_rm(PartArgs p) {
-    using V = typename idx_t<VB>::I;
-    constexpr int RPT = 4;
-    constexpr uint32_t kRound = RPT * 1024;
-    __shared__ uint32_t hist[kFine], base[kFine], cursor[kFine], tot;
-    __shared__ uint32_t pp[kRmMaxRounds + 1], pstart[kRmMaxRounds], plen[kRmMaxRounds], ptot;
-    __shared__ uint16_t s_l[kRound];
-    __shared__ V s_val[kRound];
-    __shared__ uint8_t s_f[kRound];
-    const uint32_t nseg = p.C * p.G;
-    const uint32_t lmask = (1u << p.tile_shift) - 1u;
-    const uint64_t total_recs = p.coarse_off[nseg];
-    auto seg_lower_bound = [&](uint64_t target) {
-        uint32_t a = 0, b = nseg;
-        while (a < b) {
-            const uint32_t mid = (a + b) >> 1;
-            if (uint64_t(p.coarse_off[mid]) < target) a = mid + 1; else b = mid;
-        }
-        return a;
-    };
-    const uint32_t cg_begin = seg_lower_bound(total_recs * blockIdx.x / gridDim.x);
-    const uint32_t cg_end = (blockIdx.x + 1 == gridDim.x) ? nseg
-                                                          : seg_lower_bound(total_recs * (blockIdx.x + 1) / gridDim.x);
-    for (uint32_t cg = cg_begin; cg < cg_end; cg++) {
-        const uint32_t seg_len = p.coarse_off[cg + 1] - p.coarse_off[cg];
-        if (seg_len == 0) continue;
-        const uint32_t c = cg / p.G, g = cg % p.G;
-        const uint32_t t0 = c * kFine;
-        const uint32_t nf = min(uint32_t(kFine), p.num_tiles - t0);
-        const uint64_t lo = uint64_t(g) * p.chunk, hi = min(lo + p.chunk, p.n);
-        const uint32_t nr = uint32_t((hi - lo + kRmRound - 1) / kRmRound);
-        const uint64_t row0 = lo / kRmRound;
-        // piece table of this segment
-        for (uint32_t r = threadIdx.x; r < nr; r += blockDim.x) {
-            const uint64_t row = (row0 + r) * p.C + c;
-            plen[r] = p.rhist[row];
-            pstart[r] = uint32_t(lo + uint64_t(r) * kRmRound) + p.rbase[row];
-        }
-        for (uint32_t f = threadIdx.x; f < nf; f += blockDim.x)
-            cursor[f] = p.fine_off[uint64_t(t0 + f) * p.G + g];
-        __syncthreads();
-        small_excl_scan(plen, pp, nr, &ptot);
-        __syncthreads();
-        for (uint32_t f0 = 0; f0 < seg_len; f0 += kRound) {
-            for (uint32_t f = threadIdx.x; f < nf; f += blockDim.x) hist[f] = 0;
-            uint32_t m_idx[RPT], m_src[RPT];
-            V m_val[RPT];
-#pragma unroll
-            for (int j = 0; j < RPT; j++) {
-                const uint32_t fl = f0 + uint32_t(j) * 1024 + threadIdx.x;
-                m_src[j] = 0xFFFFFFFFu;
-                if (fl < seg_len) {
-                    uint32_t a = 0, b = nr;               // last piece r with pp[r] <= fl
-                    while (b - a > 1) {
-                        const uint32_t mid = (a + b) >> 1;
-                        if (pp[mid] <= fl) a = mid; else b = mid;
-                    }
-                    m_src[j] = pstart[a] + (fl - pp[a]);
-                }
-            }
-#pragma unroll
-            for (int j = 0; j < RPT; j++) {
-                const bool in = m_src[j] != 0xFFFFFFFFu;
-                m_idx[j] = in ? p.tmp_idx[m_src[j]] : 0u;
-                m_val[j] = (in && p.tmp_val) ? reinterpret_cast<const V*>(p.tmp_val)[m_src[j]] : V(0);
-            }
-            __syncthreads();
-            uint32_t m_rank[RPT], m_f[RPT];
-#pragma unroll
-            for (int j = 0; j < RPT; j++) {
-                m_f[j] = (m_idx[j] >> p.tile_shift) - t0;
-                if (m_src[j] != 0xFFFFFFFFu) m_rank[j] = atomicAdd(&hist[m_f[j]], 1u);
-            }
-            __syncthreads();
-            small_excl_scan(hist, base, nf, &tot);
-            __syncthreads();
-#pragma unroll
-            for (int j = 0; j < RPT; j++) {
-                if (m_src[j] == 0xFFFFFFFFu) continue;
-                const uint32_t q = base[m_f[j]] + m_rank[j];
-                s_l[q] = uint16_t(m_idx[j] & lmask);
-                s_val[q] = m_val[j];
-                s_f[q] = uint8_t(m_f[j]);
-                if (p.rpos) p.rpos[m_src[j]] = cursor[m_f[j]] + m_rank[j];
-            }
-            __syncthreads();
-            const uint32_t total = tot;
-            for (uint32_t q = threadIdx.x; q < total; q += blockDim.x) {
-                const uint32_t f = s_f[q];
-                const uint32_t dst = cursor[f] + q - base[f];
-                p.bin_lidx[dst] = s_l[q];
-                if (p.tmp_val) reinterpret_cast<V*>(p.bin_val)[dst] = s_val[q];
-            }
-            __syncthreads();
-            for (uint32_t f = threadIdx.x; f < nf; f += blockDim.x) cursor[f] += hist[f];
-        }
-        __syncthreads();
-    }
-}
-
 // Persistent over (coarse bucket c, producer block g) segments, a contiguous
 // record-balanced range of them per block; the first round of the next segment
 // is prefetched while the current segment's last round is written out.
-template <int VB, int RPT, int NT>
-__global__ __launch_bounds__(NT) void k_fine_scatter(PartArgs p) {
-    if (p.only_if && *p.only_if == 0) return;
+template <int VB, int RPT>
+__global__ __launch_bounds__(1024) void k_fine_scatter(PartArgs p) {
     using V = typename idx_t<VB>::I;
-    constexpr uint32_t kRound = RPT * NT;
+    constexpr uint32_t kRound = RPT * 1024;
     __shared__ uint32_t hist[kFine], base[kFine], cursor[kFine], tot;
     __shared__ uint16_t s_l[kRound];
     __shared__ V s_val[kRound];
     const uint32_t lmask = (1u << p.tile_shift) - 1u;
-    const uint32_t rb = p.ring_base ? *p.ring_base : 0u;
+    const uint32_t nseg = p.C * p.G;
     uint32_t m_idx[RPT];
     V m_val[RPT];
     auto load_round = [&](uint32_t r0, uint32_t hi) {
 #pragma unroll
         for (int j = 0; j < RPT; j++) {
-            const uint32_t k = r0 + uint32_t(j) * NT + threadIdx.x;
+            const uint32_t k = r0 + uint32_t(j) * 1024 + threadIdx.x;
             const bool in = k < hi;
             m_idx[j] = in ? p.tmp_idx[k] : 0xFFFFFFFFu;
             m_val[j] = (in && p.tmp_val) ? reinterpret_cast<const V*>(p.tmp_val)[k] : V(0);
@@ -652,18 +381,18 @@ __global__ __launch_bounds__(NT) void k_fine_scatter(PartArgs p) {
     // (coarse_off is monotone in cg = c*G + g): a contiguous run of producers
     // g of one bucket, so each tile's output run keeps growing from one CU (one
     // XCD's L2 merges its partial lines) and work is balanced by records.
-    const uint64_t rec_lo = p.coarse_off[p.cg_lo];
-    const uint64_t total_recs = p.coarse_off[p.cg_hi] - rec_lo;
+    const uint64_t total_recs = p.coarse_off[nseg] - p.coarse_off[0];
     auto seg_lower_bound = [&](uint64_t target) {
-        uint32_t lo_s = p.cg_lo, hi_s = p.cg_hi;
+        uint32_t lo_s = 0, hi_s = nseg;
         while (lo_s < hi_s) {
             const uint32_t mid = (lo_s + hi_s) >> 1;
             if (uint64_t(p.coarse_off[mid]) < target) lo_s = mid + 1; else hi_s = mid;
         }
         return lo_s;
     };
+    const uint64_t rec_lo = p.coarse_off[0];
     const uint32_t cg_begin = seg_lower_bound(rec_lo + total_recs * blockIdx.x / gridDim.x);
-    const uint32_t cg_end = (blockIdx.x + 1 == gridDim.x) ? p.cg_hi
+    const uint32_t cg_end = (blockIdx.x + 1 == gridDim.x) ? nseg
                                                           : seg_lower_bound(rec_lo + total_recs * (blockIdx.x + 1) / gridDim.x);
     uint32_t cg = cg_begin;
     // segment cg's tile cursors (threads f < 128 hold tile f's), prefetched with the
@@ -704,10 +433,9 @@ __global__ __launch_bounds__(NT) void k_fine_scatter(PartArgs p) {
             bool m_ok[RPT];
 #pragma unroll
             for (int j = 0; j < RPT; j++) {
-                m_ok[j] = r0 + uint32_t(j) * NT + threadIdx.x < hi;
+                m_ok[j] = r0 + uint32_t(j) * 1024 + threadIdx.x < hi;
                 m_f[j] = m_ok[j] ? (m_idx[j] >> p.tile_shift) - t0 : 0u;
-                if (p.match_bits) m_rank[j] = wave_match_rank(hist, m_f[j], m_ok[j], p.match_bits);
-                else if (m_ok[j]) m_rank[j] = atomicAdd(&hist[m_f[j]], 1u);
+                if (m_ok[j]) m_rank[j] = atomicAdd(&hist[m_f[j]], 1u);
             }
             __syncthreads();
             small_excl_scan(hist, base, nf, &tot);
@@ -718,15 +446,7 @@ __global__ __launch_bounds__(NT) void k_fine_scatter(PartArgs p) {
                 const uint32_t q = base[m_f[j]] + m_rank[j];
                 s_l[q] = uint16_t(m_idx[j] & lmask);
                 s_val[q] = m_val[j];
-                if (p.rpos) p.rpos[r0 + uint32_t(j) * NT + threadIdx.x] = cursor[m_f[j]] + m_rank[j];
-                if (p.rslot) p.rslot[r0 + uint32_t(j) * NT + threadIdx.x] = uint16_t(q);
-            }
-            if (p.flog) {                                      // this round's runs, for k_unfine
-                uint32_t* lg = p.flog + (uint64_t(lo / kRound) + cg + (r0 - lo) / kRound) * 2 * kFine;
-                for (uint32_t f = threadIdx.x; f < nf; f += blockDim.x) {
-                    lg[f] = cursor[f];
-                    lg[kFine + f] = hist[f];
-                }
+                if (p.rpos) p.rpos[r0 + uint32_t(j) * 1024 + threadIdx.x] = cursor[m_f[j]] + m_rank[j];
             }
             if (r0 + kRound < hi) {
                 load_round(r0 + kRound, hi);
@@ -735,15 +455,14 @@ __global__ __launch_bounds__(NT) void k_fine_scatter(PartArgs p) {
                 load_cursor(ce);
             }
             __syncthreads();
-            uint16_t* bl = p.bin_lidx - rb;
-            V* bv = reinterpret_cast<V*>(p.bin_val) - rb;
+            V* bv = reinterpret_cast<V*>(p.bin_val);
             if (p.tmp_val)
                 bucket_writeout(hist, base, cursor, nf, [&](uint32_t q, uint32_t dst) {
-                    bl[dst] = s_l[q];
+                    p.bin_lidx[dst] = s_l[q];
                     bv[dst] = s_val[q];
                 });
             else
-                bucket_writeout(hist, base, cursor, nf, [&](uint32_t q, uint32_t dst) { bl[dst] = s_l[q]; });
+                bucket_writeout(hist, base, cursor, nf, [&](uint32_t q, uint32_t dst) { p.bin_lidx[dst] = s_l[q]; });
             __syncthreads();
             for (uint32_t f = threadIdx.x; f < nf; f += blockDim.x) cursor[f] += hist[f];
         }
@@ -765,9 +484,8 @@ __global__ __launch_bounds__(NT) void k_fine_scatter(PartArgs p) {
 //                   regions; each round reserves its tile runs with one atomicAdd
 //                   per tile on that tile's fill counter
 // A bucket that outgrows its region (a batch concentrated on a few 8 MB stretches
-// of the shard) sets ff_flag: the fine pass then does nothing and the counted
-// pipeline, launched behind it with only_if = ff_flag, partitions the batch again
-// from its input. Its kernels return at once when the flag is clear.
+// of the shard) applies its extra records to the shard at once with device atomics
+// (spill): the op is order-insensitive, so any split between the two is exact.
 template <int IW, int VB, int RPT>
 __global__ __launch_bounds__(1024) void k_coarse_free(PartArgs p) {
     using V = typename idx_t<VB>::I;
@@ -828,14 +546,12 @@ __global__ __launch_bounds__(1024) void k_coarse_free(PartArgs p) {
             s_val[q] = m_val[j];
         }
         if (threadIdx.x < C) {
-            if (cnt && rsv + cnt > p.capc && !p.spill) atomicOr(p.ff_flag, 1u);
             cursor[threadIdx.x] = rsv;                     // bucket-relative
         }
         if (r0 + kRound < hi) load_round(r0 + kRound);     // prefetch the next round
         __syncthreads();
-        // Records past the end of their bucket's region: spill mode applies them to
-        // the shard with device atomics (the op is order-insensitive), flag mode drops
-        // them (the partition is discarded and the counted pipeline redoes it).
+        // Records past the end of their bucket's region are applied to the shard with
+        // device atomics (the op is order-insensitive) and taken out of the tile counts.
         const uint32_t nw = blockDim.x >> 6, wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
         const uint32_t wpb = C >= nw ? 1u : nw / C, bstep = nw / wpb;
         for (uint32_t c = wave / wpb; c < C; c += bstep) {
@@ -885,7 +601,6 @@ __global__ __launch_bounds__(1024) void k_free_tile_totals(const uint32_t* rows,
 
 template <int VB, int RPT>
 __global__ __launch_bounds__(1024) void k_fine_free(PartArgs p) {
-    if (*p.ff_flag) return;                            // overflow: the counted pipeline takes over
     using V = typename idx_t<VB>::I;
     constexpr uint32_t kRound = RPT * 1024;
     __shared__ uint32_t hist[kFine], base[kFine], cursor[kFine], tot;
@@ -1048,12 +763,6 @@ struct TileArgs {
     const uint32_t* rts;
     uint32_t nreg;
     uint32_t rstride;
-    // grouped apply: the owner kernel serves items [tile_off, tile_off + grid), the delta
-    // kernel items [*delta_lo, *delta_hi); record r's bin lives at r - *ring_base (results at r)
-    uint32_t tile_off;
-    const uint32_t* ring_base;   // null: 0
-    const uint32_t* delta_lo;    // null: 0
-    const uint32_t* delta_hi;    // null: *delta_count
 };
 
 __host__ __device__ constexpr bool op_combines(int op) {
@@ -1109,15 +818,10 @@ __global__ __launch_bounds__(1024, 8) void k_tile_owner(TileArgs a) {
     using W = typename word_of<T>::W;
     extern __shared__ __align__(16) uint8_t lds_raw[];
     W* tile = reinterpret_cast<W*>(lds_raw);
-    const TileItem w = a.items[blockIdx.x + a.tile_off];
+    const TileItem w = a.items[blockIdx.x];
     if (w.mode != 0) return;
     const uint16_t* bin_lidx = a.bin_lidx;
     const T* bin_val = reinterpret_cast<const T*>(a.bin_val);
-    if (a.ring_base) {
-        const uint32_t rb = *a.ring_base;
-        bin_lidx -= rb;
-        bin_val -= rb;
-    }
     const int op = OPT >= 0 ? OPT : a.op;
     const T cmp = from_bits<T>(U(a.cmp_bits)), eps = from_bits<T>(U(a.eps_bits));
     const T sv = from_bits<T>(U(a.val_bits));
@@ -1207,20 +911,14 @@ __global__ __launch_bounds__(1024) void k_tile_delta(TileArgs a) {
     const T cmp = from_bits<T>(U(a.cmp_bits)), eps = from_bits<T>(U(a.eps_bits));
     const T sv = from_bits<T>(U(a.val_bits));
     const int ret = a.ret;
-    const uint32_t it_lo = a.delta_lo ? *a.delta_lo : 0u;
-    const uint32_t nitems = a.delta_hi ? *a.delta_hi : *a.delta_count;
+    const uint32_t nitems = *a.delta_count;
     const uint16_t* bin_lidx = a.bin_lidx;
     const T* bin_val = reinterpret_cast<const T*>(a.bin_val);
-    if (a.ring_base) {
-        const uint32_t rb = *a.ring_base;
-        bin_lidx -= rb;
-        bin_val -= rb;
-    }
     const W ident = (op == LMR_OP_AND || op == LMR_OP_FETCH_AND) ? W(~U(0)) : W(0);
     const U ident_bits = (op == LMR_OP_AND || op == LMR_OP_FETCH_AND) ? ~U(0) : U(0);
     const int acc = delta_acc_op(op);
     const int gop = delta_global_op(op);
-    for (uint32_t it = it_lo + blockIdx.x; it < nitems; it += gridDim.x) {
+    for (uint32_t it = blockIdx.x; it < nitems; it += gridDim.x) {
         const TileItem w = a.delta[it];
         const uint64_t base = uint64_t(w.tile) << a.tile_shift;
         const uint32_t len = uint32_t(min(uint64_t(1) << a.tile_shift, a.shard_len - base));
@@ -1277,12 +975,11 @@ __global__ __launch_bounds__(1024) void k_tile_delta(TileArgs a) {
 // hit L2; map[k] == ~0 marks an out-of-bounds record (left unwritten).
 template <int VB>
 __global__ __launch_bounds__(1024) void k_unpartition(const uint32_t* __restrict__ map, uint64_t n,
-                                                      const uint32_t* n_dev, const uint32_t* bound_dev, uint64_t chunk,
+                                                      const uint32_t* n_dev, uint64_t chunk,
                                                       const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
                                                       const uint8_t* __restrict__ ok_src, uint8_t* __restrict__ ok_dst) {
     using V = typename idx_t<VB>::I;
     const uint64_t m = n_dev ? uint64_t(*n_dev) : n;
-    const uint32_t bound = bound_dev ? *bound_dev : 0xFFFFFFFFu;   // round-major temp slots may be holes
     const uint64_t lo = uint64_t(blockIdx.x) * chunk;
     const uint64_t hi = min(lo + chunk, m);
     const V* s = reinterpret_cast<const V*>(src);
@@ -1300,7 +997,7 @@ __global__ __launch_bounds__(1024) void k_unpartition(const uint32_t* __restrict
             }
 #pragma unroll
             for (int j = 0; j < 4; j++) {
-                if (p[j] == 0xFFFFFFFFu || p[j] >= bound) continue;
+                if (p[j] == 0xFFFFFFFFu) continue;
                 const uint64_t k = k0 + uint64_t(j) * 1024;
                 d[k] = s[p[j]];
                 if (ok_src) ok_dst[k] = ok_src[p[j]];
@@ -1317,110 +1014,14 @@ __global__ __launch_bounds__(1024) void k_unpartition(const uint32_t* __restrict
             }
             V v[U];
 #pragma unroll
-            for (int j = 0; j < U; j++) v[j] = (p[j] != 0xFFFFFFFFu && p[j] < bound) ? s[p[j]] : V(0);
+            for (int j = 0; j < U; j++) v[j] = (p[j] != 0xFFFFFFFFu) ? s[p[j]] : V(0);
 #pragma unroll
             for (int j = 0; j < U; j++) {
-                if (p[j] == 0xFFFFFFFFu || p[j] >= bound) continue;
+                if (p[j] == 0xFFFFFFFFu) continue;
                 const uint64_t k = k0 + uint64_t(j) * 1024;
                 d[k] = v[j];
                 if (ok_src) ok_dst[k] = ok_src[p[j]];
             }
-        }
-    }
-}
-
-// ---- slot-map un-partition (two-level count path) -----------------------------
-// Round by round the forward passes know where every record went: a round's
-// records were staged in LDS sorted by bucket (record -> LDS slot) and each
-// bucket's run was written contiguously at the round's logged cursor. The
-// inverse reloads those runs (contiguous reads) into the same LDS layout and
-// returns each record's value by its slot, written in the round's own order
-// (coalesced). k_unpartition gathers 8 bytes per record from scattered lines
-// instead (C3: FETCH_SIZE 1.14 GB per launch for 0.8 GB of algorithmic reads).
-struct UnArgs {
-    const uint8_t* src;      // values in the forward pass's output order
-    uint8_t* dst;            // values in its input order
-    const uint8_t* ok_src;   // Ok flags (Result ops), or null
-    uint8_t* ok_dst;
-    const uint16_t* slot;    // per input-order record: its LDS slot (0xFFFF: dropped record)
-    const uint32_t* log;     // per round: cursor[stride], count[stride]
-    uint32_t kround;         // records per forward round
-    uint32_t stride;         // log entries per half (C coarse buckets / kFine tiles)
-    uint64_t n, chunk;       // k_uncoarse: block g's chunk [g*chunk, min(+chunk, n))
-    const uint32_t* coarse_off;   // k_unfine: the forward fine pass's segments
-    uint32_t cg_lo, cg_hi, G, num_tiles;
-};
-
-template <int VB>
-__device__ __forceinline__ void un_round(const UnArgs& u, const uint32_t* lg, uint32_t nb, uint64_t r0,
-                                         uint32_t len, typename idx_t<VB>::I* lv, uint8_t* lok,
-                                         uint32_t* base, uint32_t* tot) {
-    using V = typename idx_t<VB>::I;
-    const uint32_t* cur = lg;
-    const uint32_t* cnt = lg + u.stride;
-    small_excl_scan(cnt, base, nb, tot);
-    __syncthreads();
-    const V* src = reinterpret_cast<const V*>(u.src);
-    if (u.ok_src)
-        bucket_writeout(cnt, base, cur, nb, [&](uint32_t q, uint32_t g) {
-            lv[q] = src[g];
-            lok[q] = u.ok_src[g];
-        });
-    else
-        bucket_writeout(cnt, base, cur, nb, [&](uint32_t q, uint32_t g) { lv[q] = src[g]; });
-    __syncthreads();
-    V* dst = reinterpret_cast<V*>(u.dst);
-    for (uint32_t i = threadIdx.x; i < len; i += blockDim.x) {
-        const uint32_t sl = u.slot[r0 + i];
-        if (sl == 0xFFFFu) continue;
-        dst[r0 + i] = lv[sl];
-        if (u.ok_src) u.ok_dst[r0 + i] = lok[sl];
-    }
-    __syncthreads();
-}
-
-// temp order -> input order: block g replays the coarse rounds of its chunk
-template <int VB, int KR>
-__global__ __launch_bounds__(1024) void k_uncoarse(UnArgs u) {
-    __shared__ typename idx_t<VB>::I lv[KR];
-    __shared__ uint8_t lok[KR];
-    __shared__ uint32_t base[kMaxCoarse], tot;
-    const uint32_t g = blockIdx.x;
-    const uint64_t lo = uint64_t(g) * u.chunk;
-    const uint64_t hi = min(lo + u.chunk, u.n);
-    for (uint64_t r0 = lo; r0 < hi; r0 += u.kround) {
-        const uint32_t* lg = u.log + (r0 / u.kround + g) * 2 * u.stride;
-        un_round<VB>(u, lg, u.stride, r0, uint32_t(min(uint64_t(u.kround), hi - r0)), lv, lok, base, &tot);
-    }
-}
-
-// binned order -> temp order: the fine pass's segments, rounds replayed per segment
-template <int VB, int KR>
-__global__ __launch_bounds__(1024) void k_unfine(UnArgs u) {
-    __shared__ typename idx_t<VB>::I lv[KR];
-    __shared__ uint8_t lok[KR];
-    __shared__ uint32_t base[kFine], tot;
-    const uint64_t rec_lo = u.coarse_off[u.cg_lo];
-    const uint64_t total_recs = u.coarse_off[u.cg_hi] - rec_lo;
-    auto seg_lower_bound = [&](uint64_t target) {
-        uint32_t lo_s = u.cg_lo, hi_s = u.cg_hi;
-        while (lo_s < hi_s) {
-            const uint32_t mid = (lo_s + hi_s) >> 1;
-            if (uint64_t(u.coarse_off[mid]) < target) lo_s = mid + 1; else hi_s = mid;
-        }
-        return lo_s;
-    };
-    const uint32_t cg_begin = seg_lower_bound(rec_lo + total_recs * blockIdx.x / gridDim.x);
-    const uint32_t cg_end = (blockIdx.x + 1 == gridDim.x) ? u.cg_hi
-                                                          : seg_lower_bound(rec_lo + total_recs * (blockIdx.x + 1) / gridDim.x);
-    for (uint32_t cg = cg_begin, ce; cg < cg_end; cg = ce) {     // merged as in k_fine_scatter
-        ce = min(cg_end, (cg / u.G + 1) * u.G);
-        const uint32_t lo = u.coarse_off[cg], hi = u.coarse_off[ce];
-        const uint32_t t0 = (cg / u.G) * kFine;
-        const uint32_t nf = min(uint32_t(kFine), u.num_tiles - t0);
-        for (uint32_t r0 = lo; r0 < hi; r0 += u.kround) {
-            const uint32_t* lg = u.log + (uint64_t(lo / u.kround) + cg + (r0 - lo) / u.kround) * 2 * kFine;
-            un_round<VB>(u, lg, nf, r0, min(u.kround, hi - r0), lv, lok, base, &tot);
         }
     }
 }
@@ -1496,16 +1097,19 @@ bool tiled_supported(int dtype, uint64_t shard_len) {
     return tiles >= 1 && tiles <= uint64_t(kMaxTiles);
 }
 
-// round logs: both passes log 2 x (C or 128) u32 per LDS round of >= 4096 records;
-// the fine pass has at most one extra round per (bucket, block) segment
-static size_t rlog_words(uint64_t cap) {
-    return (size_t(cap / 2048) + 2 * size_t(kMaxBinBlocks) * 64 + 4096) * 2 * kFine;
-}
+// count-free partition counters: [0] unused (was the overflow flag), [64, 64 + C) bucket
+// fills, then one fill per tile
+static size_t ff_words() { return 64 + size_t(kMaxCoarse) + size_t(kMaxTiles); }
 
 // temp arrays: 25 % (+ 8192 records per coarse bucket) above the piece capacity, the
 // headroom the count-free partition's fixed per-bucket regions need (3 B per record)
 static uint64_t tmp_cap_for(uint64_t cap) {
     return cap + cap / 4 + uint64_t(kMaxCoarse) * 8192;
+}
+
+uint64_t max_rec_cap() {
+    // every temp slot index (< tmp_cap_for(cap)) must fit the kernels' uint32 slot math
+    return (uint64_t(0xFFFFFFFFull) - uint64_t(kMaxCoarse) * 8192) / 5 * 4;
 }
 
 size_t tiled_ws_bytes(uint64_t cap) {
@@ -1519,10 +1123,9 @@ size_t tiled_ws_bytes(uint64_t cap) {
     b += al(tmp_cap_for(cap) * 4) + al(tmp_cap_for(cap) * 8) + al(cap * 4);
     b += 2 * al((size_t(kMaxTiles) + 1) * 4) + al(size_t(kMaxTiles) / kScanItems * 4 + 256) + al(4);
     b += al((size_t(kMaxTiles) + 2 * (cap / kSplit) + 2) * 16);   // owner items + delta pieces
-    b += 2 * al((cap / 4096 + 2) * size_t(kMaxCoarse) * 2);         // round-major rhist / rbase
     b += al(size_t(kMaxRegions) * (kMaxTiles + 1) * 4);             // staged regions' tile starts
     b += al(size_t(kStageInfoWords) * 4);                            // staged piece table / totals
-    b += al(rlog_words(cap) * 4);                                    // round logs (slot-map un-partition)
+    b += al(ff_words() * 4);                                         // count-free fill counters
     return b;
 }
 
@@ -1548,12 +1151,9 @@ TiledWs carve_tiled_ws(uint8_t* base, uint64_t cap) {
     w.item_count = reinterpret_cast<uint32_t*>(p); p += al(4);
     w.items = p;                                   // [kMaxTiles] owner items, then delta pieces
     p += al((size_t(kMaxTiles) + 2 * (cap / kSplit) + 2) * 16);
-    w.rhist = reinterpret_cast<uint16_t*>(p); p += al((cap / 4096 + 2) * size_t(kMaxCoarse) * 2);
-    w.rbase = reinterpret_cast<uint16_t*>(p); p += al((cap / 4096 + 2) * size_t(kMaxCoarse) * 2);
     w.rts = reinterpret_cast<uint32_t*>(p); p += al(size_t(kMaxRegions) * (kMaxTiles + 1) * 4);
     w.sinfo = reinterpret_cast<uint32_t*>(p); p += al(size_t(kStageInfoWords) * 4);
-    w.rlog = reinterpret_cast<uint32_t*>(p);
-    w.rlog_words = rlog_words(cap);
+    w.ff = reinterpret_cast<uint32_t*>(p);
     w.cap = cap;
     w.tmp_cap = tmp_cap_for(cap);
     return w;
@@ -1603,13 +1203,12 @@ static int piece_fine_rpt(int vb) {
 }
 // f(vb, rpt) with rpt the largest supported value <= the request whose round
 // (rpt * 1024 records of Extra + VB bytes in LDS) fits in 150 KiB
-template <int Extra, int NT = 1024, typename F>
+template <int Extra, typename F>
 static void dispatch_vb_rpt(int vb, int rpt, F&& f) {
     using std::integral_constant;
     auto with_vb = [&](auto vbt) {
         constexpr int VB = decltype(vbt)::value;
-        // 1024-thread blocks may take 150 KiB (one per CU); 512-thread blocks 75 KiB (two per CU)
-        constexpr int kMaxR = (NT == 1024 ? 150 * 1024 : 75 * 1024) / ((Extra + VB) * NT);
+        constexpr int kMaxR = (150 * 1024) / ((Extra + VB) * 1024);
         auto call = [&](auto r) {
             constexpr int R = decltype(r)::value;
             if constexpr (R <= kMaxR) f(vbt, r);
@@ -1631,69 +1230,17 @@ static void dispatch_vb_rpt(int vb, int rpt, F&& f) {
     default: with_vb(integral_constant<int, 8>{}); break;
     }
 }
-// the rpt dispatch_vb_rpt<Extra> (1024 threads) picks for a request (same rule)
-static int eff_rpt(int extra, int vb, int rpt) {
-    const int maxr = (150 * 1024) / ((extra + vb) * 1024);
-    int r = rpt >= 16 ? 16 : rpt >= 12 ? 12 : rpt >= 10 ? 10 : rpt >= 8 ? 8 : rpt >= 6 ? 6 : 4;
-    if (r > maxr) r = maxr >= 12 ? 12 : (maxr >= 8 ? 8 : 4);
-    return r;
-}
-// LMR_SLOT_UNPARTITION=1: returned values go back through the slot maps and round
-// logs (k_unfine / k_uncoarse: contiguous reads, no fetch amplification) instead of
-// the position maps and k_unpartition's scattered gathers. Off: measured slower
-// (C3 un-partition 0.92 -> 1.43 ms): with one 1024-thread block per CU each replayed
-// round waits on three dependent global round trips. Read per call (tests).
-static bool slot_unpartition() {
-    const char* e = getenv("LMR_SLOT_UNPARTITION");
-    return e && e[0] == '1';
-}
-// LMR_PARTITION=rm selects the round-major two-level partition (no count pass)
-static bool partition_rm_enabled() {      // read per call: tests switch it within one process
-    const char* e = getenv("LMR_PARTITION");
-    return e && e[0] == 'r' && e[1] == 'm';
-}
 static int fine_blocks_cap() {
     static int v = env_int("LMR_FINE_BLOCKS", 512, 1, 1 << 20);
     return v;
 }
 
-// threads per block of the coarse / fine passes (LMR_PART_NT: 1024 = one block per CU
-// with the largest rounds, 512 = two blocks per CU, each with half the LDS)
-static int part_nt() {
-    static int v = env_int("LMR_PART_NT", 1024, 512, 1024);
-    return v >= 1024 ? 1024 : 512;
-}
-// LMR_MATCH_RANK=1: rank records in the coarse / fine LDS rounds by wave key
-// matching (one LDS atomic per distinct bucket and wave) instead of one LDS
-// atomic per record; read per call (A/B measurements)
-static bool match_rank() {
-    const char* e = getenv("LMR_MATCH_RANK");
-    return e && e[0] == '1';
-}
-// records per fine+apply group (LMR_GROUP_RECORDS; 0 = one fine pass, then one tile
-// sweep); read per call: tests switch it within one process
-static int group_records() {
-    return env_int("LMR_GROUP_RECORDS", 0, 0, 1 << 30);
-}
-static void launch_fine(const PartArgs& q, int vb, hipStream_t s) {
-    const uint64_t nseg = uint64_t(q.cg_hi - q.cg_lo);
-    const unsigned fgrid = unsigned(nseg < uint64_t(fine_blocks_cap()) ? nseg : fine_blocks_cap());
-    if (part_nt() == 512)
-        dispatch_vb_rpt<2, 512>(vb, fine_rpt(vb), [&](auto vbt, auto rpt) {
-            constexpr int VBc = decltype(vbt)::value, R = decltype(rpt)::value;
-            hipLaunchKernelGGL((k_fine_scatter<VBc, R, 512>), dim3(fgrid ? fgrid : 1u), dim3(512), 0, s, q);
-        });
-    else
-        dispatch_vb_rpt<2>(vb, fine_rpt(vb), [&](auto vbt, auto rpt) {
-            constexpr int VBc = decltype(vbt)::value, R = decltype(rpt)::value;
-            hipLaunchKernelGGL((k_fine_scatter<VBc, R, 1024>), dim3(fgrid ? fgrid : 1u), dim3(1024), 0, s, q);
-        });
-}
-
 // Count-free partition (k_coarse_free / k_fine_free): order-insensitive ops with
 // nothing returned, two-level shards, and >= 25 % headroom per coarse bucket region
-// in the temp arrays (always, for pieces within the workspace capacity). Returns its coarse round (records per thread), 0 when not
-// used. LMR_FREE=0 disables it (read per call: tests switch it in one process).
+// in the temp arrays for a uniform stream of n records (records past a full region
+// are applied at once with device atomics, so a skewed stream stays correct).
+// Returns its coarse round (records per thread), 0 when not used. LMR_FREE=0
+// disables it (read per call: tests switch it in one process).
 static int free_partition_rpt(int dtype, int op, int ret, uint64_t n, uint64_t num_tiles, uint64_t tmp_cap) {
     const char* e = getenv("LMR_FREE");
     if (e && e[0] == '0') return 0;
@@ -1702,7 +1249,6 @@ static int free_partition_rpt(int dtype, int op, int ret, uint64_t n, uint64_t n
         op != LMR_OP_OR && op != LMR_OP_XOR)
         return 0;
     if (num_tiles <= uint64_t(kFine) || num_tiles > uint64_t(kMaxTiles)) return 0;
-    if (partition_rm_enabled() || group_records() > 0 || match_rank() || part_nt() != 1024) return 0;
     const uint64_t C = (num_tiles + kFine - 1) / kFine;
     const uint64_t capc = tmp_cap / C;
     if (n / C + n / (4 * C) + 8192 > capc) return 0;
@@ -1723,7 +1269,6 @@ bool free_partition_applies(int dtype, int op, int ret, uint64_t shard_len, uint
 }
 
 bool piece_partition_pays(int dtype, uint64_t shard_len, uint64_t n) {
-    if (partition_rm_enabled()) return false;
     const int shift = tile_shift_for(dtype);
     const uint64_t num_tiles = (shard_len + (uint64_t(1) << shift) - 1) >> shift;
     if (num_tiles <= uint64_t(kFine) || num_tiles > uint64_t(kMaxTiles) || n == 0) return false;
@@ -1734,6 +1279,96 @@ bool piece_partition_pays(int dtype, uint64_t shard_len, uint64_t n) {
     return n / (G * C) < 8192;
 }
 
+// count-free partition arguments shared by the one-shot path and the staged
+// regions: bucket c's region is temp slots [c * capc, (c + 1) * capc); records that
+// find it full are applied to the shard with device atomics (spill)
+static PartArgs free_args(int dtype, const ApplyArgs& a, const TiledWs& w, uint32_t G) {
+    const int shift = tile_shift_for(dtype);
+    const uint32_t T = uint32_t((a.shard_len + (uint64_t(1) << shift) - 1) >> shift);
+    PartArgs q{};
+    q.shard_len = a.shard_len; q.tile_shift = shift; q.num_tiles = T;
+    q.G = G; q.C = (T + kFine - 1) / kFine;
+    q.tile_start = w.tile_start; q.counts = w.counts;
+    q.tmp_idx = w.tmp_idx; q.tmp_val = w.tmp_val;          // values always materialised
+    q.bin_lidx = w.bin_lidx; q.bin_val = w.bin_val;
+    q.err = a.err;
+    q.ff_fill = w.ff + 64; q.ff_tfill = w.ff + 64 + kMaxCoarse;
+    q.capc = uint32_t(w.tmp_cap / q.C); q.tmp_cap = w.tmp_cap;
+    q.spill = 1; q.shard = a.shard; q.op = a.op;
+    return q;
+}
+
+static hipError_t launch_coarse_free(int index_size, int vb, int frpt, const PartArgs& q, hipStream_t s) {
+    return dispatch_iw(index_size, [&](auto iw) {
+        constexpr int IW = decltype(iw)::value;
+        dispatch_vb_rpt<4>(vb, frpt, [&](auto vbt, auto rpt) {
+            constexpr int VBc = decltype(vbt)::value, R = decltype(rpt)::value;
+            hipLaunchKernelGGL((k_coarse_free<IW, VBc, R>), dim3(q.G), dim3(1024), size_t(q.num_tiles) * 4, s, q);
+        });
+        return hipGetLastError();
+    });
+}
+
+// exact tile starts from the coarse pass's tile-count rows, then the fine pass
+static hipError_t launch_free_finish(int vb, const PartArgs& q, const TiledWs& w, Prof* prof, hipStream_t s) {
+    const uint32_t T = q.num_tiles;
+    hipError_t e;
+    {
+        ProfScope ps(prof, LMR_STAGE_SCAN, s);
+        hipLaunchKernelGGL(k_free_tile_totals, dim3((T + 63) / 64), dim3(1024), 0, s, w.counts, T, q.G, w.tile_start);
+        e = scan_exclusive_u32(w.tile_start, T, w.partials, w.tile_start + T, s);
+    }
+    if (e != hipSuccess) return e;
+    ProfScope ps(prof, LMR_STAGE_FINE_SCATTER, s);
+    dispatch_vb_rpt<2>(vb, fine_rpt(vb), [&](auto vbt, auto rpt) {
+        constexpr int VBc = decltype(vbt)::value, R = decltype(rpt)::value;
+        hipLaunchKernelGGL((k_fine_free<VBc, R>), dim3(unsigned(fine_blocks_cap())), dim3(1024), 0, s, q);
+    });
+    return hipGetLastError();
+}
+
+// work plan (owner items, delta pieces of hot tiles for combinable ops) and the tile
+// sweep over the binned records [tile_start[t], tile_start[t + 1]) of every tile
+static hipError_t launch_tile_sweep(int dtype, const ApplyArgs& a, const TiledWs& w, uint32_t T, uint64_t n,
+                                    bool scalar, void* res_bin, uint8_t* ok_bin, hipStream_t s) {
+    ProfScope ps(a.prof, LMR_STAGE_TILE_APPLY, s);
+    const uint64_t avg = (n + T - 1) / T;
+    const uint32_t thresh = uint32_t(std::min<uint64_t>(0xFFFFFFFFull, std::max<uint64_t>(4 * avg, 65536)));
+    const unsigned pg = (T + 255) / 256;
+    hipLaunchKernelGGL(k_tile_plan_count, dim3(pg), dim3(256), 0, s, w.tile_start, T, thresh,
+                       op_combines(a.op) ? 1 : 0, w.tile_items);
+    hipLaunchKernelGGL(k_tile_plan_extra, dim3(pg), dim3(256), 0, s, w.tile_items, T, w.tile_items2);
+    hipError_t e = scan_exclusive_u32(w.tile_items2, T, w.plan_partials, w.item_count, s);
+    if (e != hipSuccess) return e;
+    TileItem* items = reinterpret_cast<TileItem*>(w.items);
+    hipLaunchKernelGGL(k_tile_plan_fill, dim3(pg), dim3(256), 0, s, w.tile_start, T, w.tile_items2,
+                       w.tile_items, items, items + kMaxTiles);
+    TileArgs t;
+    t.shard = a.shard; t.shard_len = a.shard_len; t.tile_shift = tile_shift_for(dtype);
+    t.kind = a.kind; t.op = a.op; t.ret = res_bin ? a.ret : LMR_RET_NONE;
+    t.cmp_bits = a.cmp_bits; t.eps_bits = a.eps_bits; t.val_bits = a.val_bits;
+    t.scalar = scalar;
+    t.items = items; t.delta = items + kMaxTiles; t.delta_count = w.item_count;
+    t.num_tiles = T;
+    t.bin_lidx = w.bin_lidx; t.bin_val = w.bin_val;
+    t.results = res_bin; t.ok = ok_bin; t.err = a.err;
+    t.rts = nullptr; t.nreg = 0; t.rstride = 0;
+    const bool delta = op_combines(a.op) && n > thresh;
+    const unsigned dgrid = unsigned(std::min<uint64_t>(2 * ((n + kSplit - 1) / kSplit), uint64_t(tile_grid_cap())));
+    return dispatch_dtype(dtype, [&](auto tag) {
+        using Ty = decltype(tag);
+        auto go = [&](auto opt) {
+            constexpr int OPT = decltype(opt)::value;
+            hipLaunchKernelGGL((k_tile_owner<Ty, OPT>), dim3(T), dim3(1024), size_t(kTileBytes), s, t);
+            if (delta) hipLaunchKernelGGL((k_tile_delta<Ty, OPT>), dim3(dgrid), dim3(1024), size_t(kTileBytes), s, t);
+        };
+        if (a.op == LMR_OP_ADD) go(std::integral_constant<int, LMR_OP_ADD>{});
+        else if (a.op == LMR_OP_FETCH_ADD) go(std::integral_constant<int, LMR_OP_FETCH_ADD>{});
+        else go(std::integral_constant<int, -1>{});
+        return hipGetLastError();
+    });
+}
+
 // One tiled piece: a.n <= workspace capacity, a.n < 2^32.
 hipError_t launch_apply_tiled(int dtype, int index_size, const ApplyArgs& a, const TiledWs& w,
                               hipStream_t s) {
@@ -1741,7 +1376,30 @@ hipError_t launch_apply_tiled(int dtype, int index_size, const ApplyArgs& a, con
     const int shift = tile_shift_for(dtype);
     const uint64_t num_tiles = (a.shard_len + (uint64_t(1) << shift) - 1) >> shift;
     if (num_tiles == 0 || num_tiles > uint64_t(kMaxTiles)) return hipErrorNotSupported;
+    const uint32_t T = uint32_t(num_tiles);
     const int vb = dtype_bytes(dtype);
+    const bool has_res = a.ret != LMR_RET_NONE;
+    hipError_t e;
+    // ---- count-free partition: order-insensitive integer ops that return nothing
+    if (const int frpt = free_partition_rpt(dtype, a.op, a.ret, a.n, num_tiles, w.tmp_cap)) {
+        // one coarse block per CU once a round takes most of the LDS
+        uint64_t Gf = (a.n + 65535) / 65536;
+        Gf = std::max<uint64_t>(1, std::min<uint64_t>(Gf, frpt >= 8 ? 256 : 512));
+        PartArgs q = free_args(dtype, a, w, uint32_t(Gf));
+        q.idx = a.idx; q.idx_stride = a.idx_stride; q.val = a.val; q.val_stride = a.val_stride;
+        q.val_bits = a.val_bits; q.n = a.n; q.chunk = (a.n + Gf - 1) / Gf;
+        q.tmp_val = a.val ? w.tmp_val : nullptr;            // one scalar value: bins carry indices only
+        e = hipMemsetAsync(w.ff, 0, ff_words() * 4, s);
+        if (e != hipSuccess) return e;
+        {
+            ProfScope ps(a.prof, LMR_STAGE_BIN_SCATTER, s);
+            e = launch_coarse_free(index_size, vb, frpt, q, s);
+        }
+        if (e == hipSuccess) e = launch_free_finish(vb, q, w, a.prof, s);
+        if (e == hipSuccess) e = launch_tile_sweep(dtype, a, w, T, a.n, a.val == nullptr, nullptr, nullptr, s);
+        return e;
+    }
+    // ---- counted partition: records keep input order within every tile
     // G blocks: >= 64K records each, at most kMaxBinBlocks
     uint64_t G = (a.n + 65535) / 65536;
     if (G > uint64_t(bin_blocks_cap(vb))) G = bin_blocks_cap(vb);
@@ -1751,347 +1409,98 @@ hipError_t launch_apply_tiled(int dtype, int index_size, const ApplyArgs& a, con
     b.val = a.val; b.val_stride = a.val_stride;
     b.n = a.n; b.shard_len = a.shard_len;
     b.chunk = (a.n + G - 1) / G;
-    b.tile_shift = shift; b.num_tiles = uint32_t(num_tiles); b.G = uint32_t(G);
+    b.tile_shift = shift; b.num_tiles = T; b.G = uint32_t(G);
     b.counts = w.counts; b.bin_lidx = w.bin_lidx; b.bin_val = w.bin_val;
-    const bool has_res = a.ret != LMR_RET_NONE;
     b.rpos = has_res ? w.rpos : nullptr;
     b.err = a.err;
     const size_t hist_lds = size_t(num_tiles) * 4;
-    hipError_t e;
-    // Round-major two-level partition (LMR_PARTITION=rm): no count pass. Block
-    // chunks become multiples of kRmRound with at most kRmMaxRounds rounds each.
-    bool rm = false;
-    if (num_tiles > uint64_t(kFine) && partition_rm_enabled()) {
-        uint64_t ch = ((a.n + G - 1) / G + kRmRound - 1) / kRmRound * kRmRound;
-        const uint64_t ch_max = uint64_t(kRmMaxRounds) * kRmRound;
-        if (ch > ch_max) ch = ch_max;
-        const uint64_t Gr = (a.n + ch - 1) / ch;
-        if (Gr <= uint64_t(kMaxBinBlocks)) {
-            rm = true;
-            G = Gr;
-            b.G = uint32_t(G);
-            b.chunk = ch;
-        }
+    {
+        ProfScope ps(a.prof, LMR_STAGE_BIN_COUNT, s);
+        e = dispatch_iw(index_size, [&](auto iw) {
+            hipLaunchKernelGGL((k_bin_count<decltype(iw)::value>), dim3(unsigned(G)), dim3(kBinBlock),
+                               hist_lds, s, b);
+            return hipGetLastError();
+        });
     }
-    PartArgs qf{};            // grouped fine pass (launched per group of coarse buckets below)
-    bool grouped = false;
-    bool slot_maps = false;   // returning ops: slot maps + round logs (k_unfine / k_uncoarse)
-    size_t clog_words = 0;
-    if (rm) {
+    if (e != hipSuccess) return e;
+    {
+        ProfScope ps(a.prof, LMR_STAGE_SCAN, s);
+        e = scan_exclusive_u32(w.counts, num_tiles * G, w.partials, w.total, s);
+        if (e != hipSuccess) return e;
+        hipLaunchKernelGGL(k_tile_starts, dim3(unsigned((num_tiles + 1 + 255) / 256)), dim3(256), 0, s,
+                           w.counts, T, uint32_t(G), w.total, w.tile_start);
+    }
+    if (num_tiles > uint64_t(kFine)) {
+        // two-level LDS-staged partition: coarse buckets of kFine tiles, then tiles
         PartArgs q{};
         q.idx = a.idx; q.idx_stride = a.idx_stride; q.val = a.val; q.val_stride = a.val_stride;
         q.n = a.n; q.shard_len = a.shard_len; q.chunk = b.chunk; q.tile_shift = shift;
-        q.num_tiles = uint32_t(num_tiles); q.G = uint32_t(G);
+        q.num_tiles = T; q.G = uint32_t(G);
         q.C = uint32_t((num_tiles + kFine - 1) / kFine);
         q.fine_off = w.counts; q.tile_start = w.tile_start; q.coarse_off = w.coarse_off;
         q.tmp_idx = w.tmp_idx; q.tmp_val = a.val ? w.tmp_val : nullptr;
         q.qpos = has_res ? w.qpos : nullptr;
         q.bin_lidx = w.bin_lidx; q.bin_val = w.bin_val; q.rpos = b.rpos;
-        q.counts = w.counts; q.rhist = w.rhist; q.rbase = w.rbase;
-        q.R = uint32_t(b.chunk / kRmRound); q.err = a.err;
-        {
-        ProfScope ps(a.prof, LMR_STAGE_BIN_SCATTER, s);
-        const size_t th_lds = size_t((num_tiles + 1) / 2) * 4;
-        e = dispatch_iw(index_size, [&](auto iw) {
-            constexpr int IW = decltype(iw)::value;
-            switch (vb) {
-            case 1: hipLaunchKernelGGL((k_coarse_rm<IW, 1>), dim3(unsigned(G)), dim3(1024), th_lds, s, q); break;
-            case 2: hipLaunchKernelGGL((k_coarse_rm<IW, 2>), dim3(unsigned(G)), dim3(1024), th_lds, s, q); break;
-            case 4: hipLaunchKernelGGL((k_coarse_rm<IW, 4>), dim3(unsigned(G)), dim3(1024), th_lds, s, q); break;
-            default: hipLaunchKernelGGL((k_coarse_rm<IW, 8>), dim3(unsigned(G)), dim3(1024), th_lds, s, q); break;
-            }
-            return hipGetLastError();
-        });
-        }
-        if (e != hipSuccess) return e;
-        {
-        ProfScope ps(a.prof, LMR_STAGE_SCAN, s);
-        const uint64_t ncg = uint64_t(q.C) * G;
-        hipLaunchKernelGGL(k_rm_seg_sizes, dim3(unsigned((ncg + 1 + 255) / 256)), dim3(256), 0, s, q, w.coarse_off);
-        e = scan_exclusive_u32(w.coarse_off, ncg + 1, w.partials, w.total, s);
-        if (e != hipSuccess) return e;
-        e = scan_exclusive_u32(w.counts, num_tiles * G, w.partials, w.total, s);
-        if (e != hipSuccess) return e;
-        hipLaunchKernelGGL(k_tile_starts, dim3(unsigned((num_tiles + 1 + 255) / 256)), dim3(256), 0, s,
-                           w.counts, uint32_t(num_tiles), uint32_t(G), w.total, w.tile_start, nullptr);
-        }
-        {
-        ProfScope pf(a.prof, LMR_STAGE_FINE_SCATTER, s);
-        const uint64_t nseg = uint64_t(q.C) * G;
-        const unsigned fgrid = unsigned(nseg < uint64_t(fine_blocks_cap()) ? nseg : fine_blocks_cap());
-        switch (vb) {
-        case 1: hipLaunchKernelGGL((k_fine_rm<1>), dim3(fgrid), dim3(1024), 0, s, q); break;
-        case 2: hipLaunchKernelGGL((k_fine_rm<2>), dim3(fgrid), dim3(1024), 0, s, q); break;
-        case 4: hipLaunchKernelGGL((k_fine_rm<4>), dim3(fgrid), dim3(1024), 0, s, q); break;
-        default: hipLaunchKernelGGL((k_fine_rm<8>), dim3(fgrid), dim3(1024), 0, s, q); break;
-        }
-        e = hipGetLastError();
-        }
-    } else {
-    // count-free partition first; the counted one below then runs only if it overflowed
-    const uint32_t* guard = nullptr;
-    const int frpt = free_partition_rpt(dtype, a.op, a.ret, a.n, num_tiles, w.tmp_cap);
-    if (frpt > 0) {
-        const uint32_t T = uint32_t(num_tiles);
-        uint32_t* ff_flag = w.rlog;
-        // one coarse block per CU once a round takes most of the LDS
-        uint64_t Gf = (a.n + 65535) / 65536;
-        Gf = std::max<uint64_t>(1, std::min<uint64_t>(Gf, frpt >= 8 ? 256 : 512));
-        PartArgs q{};
-        q.idx = a.idx; q.idx_stride = a.idx_stride; q.val = a.val; q.val_stride = a.val_stride;
-        q.n = a.n; q.shard_len = a.shard_len; q.chunk = (a.n + Gf - 1) / Gf; q.tile_shift = shift;
-        q.num_tiles = T; q.G = uint32_t(Gf); q.C = (T + kFine - 1) / kFine;
-        q.tile_start = w.tile_start; q.counts = w.counts;
-        q.tmp_idx = w.tmp_idx; q.tmp_val = a.val ? w.tmp_val : nullptr;
-        q.bin_lidx = w.bin_lidx; q.bin_val = w.bin_val;
-        q.err = a.err;
-        q.ff_flag = ff_flag; q.ff_fill = w.rlog + 64; q.ff_tfill = w.rlog + 64 + kMaxCoarse;
-        q.capc = uint32_t(w.tmp_cap / q.C); q.tmp_cap = w.tmp_cap;
-        e = hipMemsetAsync(w.rlog, 0, (64 + kMaxCoarse + size_t(T)) * 4, s);
-        if (e != hipSuccess) return e;
         {
             ProfScope ps(a.prof, LMR_STAGE_BIN_SCATTER, s);
+            const uint64_t ncg = uint64_t(q.C) * G + 1;
+            hipLaunchKernelGGL(k_coarse_offsets, dim3(unsigned((ncg + 255) / 256)), dim3(256), 0, s, q);
             e = dispatch_iw(index_size, [&](auto iw) {
                 constexpr int IW = decltype(iw)::value;
-                dispatch_vb_rpt<4>(vb, frpt, [&](auto vbt, auto rpt) {
+                dispatch_vb_rpt<4>(vb, coarse_rpt(vb), [&](auto vbt, auto rpt) {
                     constexpr int VBc = decltype(vbt)::value, R = decltype(rpt)::value;
-                    hipLaunchKernelGGL((k_coarse_free<IW, VBc, R>), dim3(unsigned(Gf)), dim3(1024), size_t(T) * 4, s, q);
+                    hipLaunchKernelGGL((k_coarse_scatter<IW, VBc, R>), dim3(unsigned(G)), dim3(1024), 0, s, q);
                 });
                 return hipGetLastError();
             });
         }
         if (e != hipSuccess) return e;
-        {
-            ProfScope ps(a.prof, LMR_STAGE_SCAN, s);
-            hipLaunchKernelGGL(k_free_tile_totals, dim3((T + 63) / 64), dim3(1024), 0, s, w.counts, T, uint32_t(Gf),
-                               w.tile_start);
-            e = scan_exclusive_u32(w.tile_start, T, w.partials, w.tile_start + T, s);
-        }
-        if (e != hipSuccess) return e;
-        {
-            ProfScope ps(a.prof, LMR_STAGE_FINE_SCATTER, s);
-            const unsigned fgrid = unsigned(fine_blocks_cap());
-            dispatch_vb_rpt<2>(vb, fine_rpt(vb), [&](auto vbt, auto rpt) {
-                constexpr int VBc = decltype(vbt)::value, R = decltype(rpt)::value;
-                hipLaunchKernelGGL((k_fine_free<VBc, R>), dim3(fgrid), dim3(1024), 0, s, q);
-            });
-            e = hipGetLastError();
-        }
-        if (e != hipSuccess) return e;
-        guard = ff_flag;
-    }
-    b.only_if = guard;
-    // behind the count-free partition the counted kernels return at once (unless it
-    // overflowed): their time is booked as one scan-stage entry, so the per-launch
-    // stage times stay those of the kernels that did the work
-    Prof* cprof = guard ? nullptr : a.prof;
-    ProfScope gscope(guard ? a.prof : nullptr, LMR_STAGE_SCAN, s);
-    {
-    ProfScope ps(cprof, LMR_STAGE_BIN_COUNT, s);
-    e = dispatch_iw(index_size, [&](auto iw) {
-        hipLaunchKernelGGL((k_bin_count<decltype(iw)::value>), dim3(unsigned(G)), dim3(kBinBlock),
-                           hist_lds, s, b);
-        return hipGetLastError();
-    });
-    }
-    if (e != hipSuccess) return e;
-    {
-    ProfScope ps(cprof, LMR_STAGE_SCAN, s);
-    e = scan_exclusive_u32(w.counts, num_tiles * G, w.partials, w.total, s, guard);
-    if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(k_tile_starts, dim3(unsigned((num_tiles + 1 + 255) / 256)), dim3(256), 0, s,
-                       w.counts, uint32_t(num_tiles), uint32_t(G), w.total, w.tile_start, guard);
-    }
-    if (num_tiles > uint64_t(kFine)) {
-        // two-level LDS-staged partition: coarse buckets of kFine tiles, then tiles
-        if (cprof) prof_begin(cprof, LMR_STAGE_BIN_SCATTER, s);
-        PartArgs q{};
-        q.idx = a.idx; q.idx_stride = a.idx_stride; q.val = a.val; q.val_stride = a.val_stride;
-        q.n = a.n; q.shard_len = a.shard_len; q.chunk = b.chunk; q.tile_shift = shift;
-        q.num_tiles = uint32_t(num_tiles); q.G = uint32_t(G);
-        q.C = uint32_t((num_tiles + kFine - 1) / kFine);
-        q.fine_off = w.counts; q.tile_start = w.tile_start; q.coarse_off = w.coarse_off;
-        q.tmp_idx = w.tmp_idx; q.tmp_val = a.val ? w.tmp_val : nullptr;
-        q.qpos = has_res ? w.qpos : nullptr;
-        q.bin_lidx = w.bin_lidx; q.bin_val = w.bin_val; q.rpos = b.rpos;
-        q.match_bits = match_rank() ? key_bits(q.C) : 0;
-        q.only_if = guard;
-        if (has_res && slot_unpartition() && part_nt() == 1024) {
-            const uint64_t kr_c = uint64_t(eff_rpt(4, vb, coarse_rpt(vb))) * 1024;
-            const uint64_t kr_f = uint64_t(eff_rpt(2, vb, fine_rpt(vb))) * 1024;
-            clog_words = size_t(a.n / kr_c + G + 2) * 2 * q.C;
-            const size_t flog_words = size_t(a.n / kr_f + uint64_t(q.C) * G + 2) * 2 * kFine;
-            if (clog_words + flog_words <= w.rlog_words) {
-                slot_maps = true;
-                q.qpos = nullptr; q.qslot = reinterpret_cast<uint16_t*>(w.qpos); q.clog = w.rlog;
-                q.rpos = nullptr; q.rslot = reinterpret_cast<uint16_t*>(w.rpos); q.flog = w.rlog + clog_words;
-            }
-        }
-        const uint64_t ncg = uint64_t(q.C) * G + 1;
-        hipLaunchKernelGGL(k_coarse_offsets, dim3(unsigned((ncg + 255) / 256)), dim3(256), 0, s, q);
+        ProfScope pf(a.prof, LMR_STAGE_FINE_SCATTER, s);
+        const uint64_t nseg = uint64_t(q.C) * G;
+        const unsigned fgrid = unsigned(std::min<uint64_t>(nseg, uint64_t(fine_blocks_cap())));
+        dispatch_vb_rpt<2>(vb, fine_rpt(vb), [&](auto vbt, auto rpt) {
+            constexpr int VBc = decltype(vbt)::value, R = decltype(rpt)::value;
+            hipLaunchKernelGGL((k_fine_scatter<VBc, R>), dim3(fgrid ? fgrid : 1u), dim3(1024), 0, s, q);
+        });
+        e = hipGetLastError();
+    } else {
+        ProfScope ps(a.prof, LMR_STAGE_BIN_SCATTER, s);
         e = dispatch_iw(index_size, [&](auto iw) {
             constexpr int IW = decltype(iw)::value;
-            if (part_nt() == 512)
-                dispatch_vb_rpt<4, 512>(vb, coarse_rpt(vb), [&](auto vbt, auto rpt) {
-                    constexpr int VBc = decltype(vbt)::value, R = decltype(rpt)::value;
-                    hipLaunchKernelGGL((k_coarse_scatter<IW, VBc, R, 512>), dim3(unsigned(G)), dim3(512), 0, s, q);
-                });
-            else
-                dispatch_vb_rpt<4>(vb, coarse_rpt(vb), [&](auto vbt, auto rpt) {
-                    constexpr int VBc = decltype(vbt)::value, R = decltype(rpt)::value;
-                    hipLaunchKernelGGL((k_coarse_scatter<IW, VBc, R, 1024>), dim3(unsigned(G)), dim3(1024), 0, s, q);
-                });
+            switch (vb) {
+            case 1: hipLaunchKernelGGL((k_bin_scatter<IW, 1>), dim3(unsigned(G)), dim3(kBinBlock), hist_lds, s, b); break;
+            case 2: hipLaunchKernelGGL((k_bin_scatter<IW, 2>), dim3(unsigned(G)), dim3(kBinBlock), hist_lds, s, b); break;
+            case 4: hipLaunchKernelGGL((k_bin_scatter<IW, 4>), dim3(unsigned(G)), dim3(kBinBlock), hist_lds, s, b); break;
+            default: hipLaunchKernelGGL((k_bin_scatter<IW, 8>), dim3(unsigned(G)), dim3(kBinBlock), hist_lds, s, b); break;
+            }
             return hipGetLastError();
         });
-        if (cprof) prof_end(cprof, LMR_STAGE_BIN_SCATTER, s);
-        if (e != hipSuccess) return e;
-        q.cg_lo = 0; q.cg_hi = q.C * uint32_t(G); q.ring_base = nullptr;
-        q.match_bits = match_rank() ? key_bits(kFine) : 0;
-        if (group_records() > 0 && q.C > 1) {
-            qf = q;
-            grouped = true;
-        } else {
-            ProfScope pf(cprof, LMR_STAGE_FINE_SCATTER, s);
-            launch_fine(q, vb, s);
-            e = hipGetLastError();
-        }
-    } else {
-    ProfScope ps(cprof, LMR_STAGE_BIN_SCATTER, s);
-    e = dispatch_iw(index_size, [&](auto iw) {
-        constexpr int IW = decltype(iw)::value;
-        switch (vb) {
-        case 1: hipLaunchKernelGGL((k_bin_scatter<IW, 1>), dim3(unsigned(G)), dim3(kBinBlock), hist_lds, s, b); break;
-        case 2: hipLaunchKernelGGL((k_bin_scatter<IW, 2>), dim3(unsigned(G)), dim3(kBinBlock), hist_lds, s, b); break;
-        case 4: hipLaunchKernelGGL((k_bin_scatter<IW, 4>), dim3(unsigned(G)), dim3(kBinBlock), hist_lds, s, b); break;
-        default: hipLaunchKernelGGL((k_bin_scatter<IW, 8>), dim3(unsigned(G)), dim3(kBinBlock), hist_lds, s, b); break;
-        }
-        return hipGetLastError();
-    });
     }
-    gscope.end();
-    }   // count-based partition
     if (e != hipSuccess) return e;
-    ProfScope ps(a.prof, LMR_STAGE_TILE_APPLY, s);
-    // work plan: owner items, and delta items for hot tiles of combinable ops
-    const uint64_t avg = (a.n + num_tiles - 1) / num_tiles;
-    const uint32_t thresh = uint32_t(std::min<uint64_t>(0xFFFFFFFFull, std::max<uint64_t>(4 * avg, 65536)));
-    const unsigned pg = unsigned((num_tiles + 255) / 256);
-    hipLaunchKernelGGL(k_tile_plan_count, dim3(pg), dim3(256), 0, s, w.tile_start, uint32_t(num_tiles), thresh,
-                       op_combines(a.op) ? 1 : 0, w.tile_items);
-    hipLaunchKernelGGL(k_tile_plan_extra, dim3(pg), dim3(256), 0, s, w.tile_items, uint32_t(num_tiles),
-                       w.tile_items2);
-    e = scan_exclusive_u32(w.tile_items2, num_tiles, w.plan_partials, w.item_count, s);
-    if (e != hipSuccess) return e;
-    TileItem* items = reinterpret_cast<TileItem*>(w.items);
-    hipLaunchKernelGGL(k_tile_plan_fill, dim3(pg), dim3(256), 0, s, w.tile_start, uint32_t(num_tiles),
-                       w.tile_items2, w.tile_items, items, items + kMaxTiles);
-    TileArgs t;
-    t.shard = a.shard; t.shard_len = a.shard_len; t.tile_shift = shift;
-    t.kind = a.kind; t.op = a.op; t.ret = a.ret;
-    t.cmp_bits = a.cmp_bits; t.eps_bits = a.eps_bits; t.val_bits = a.val_bits;
-    t.scalar = (a.val == nullptr);
-    t.items = items; t.delta = items + kMaxTiles; t.delta_count = w.item_count;
-    t.num_tiles = uint32_t(num_tiles);
-    t.bin_lidx = w.bin_lidx; t.bin_val = w.bin_val;
     // results in binned order: reuse the temp buffers the partition is done with
     uint8_t* res_bin = w.tmp_val;
     uint8_t* ok_bin = reinterpret_cast<uint8_t*>(w.tmp_idx);
-    t.results = res_bin; t.ok = ok_bin; t.err = a.err;
-    t.rts = nullptr; t.nreg = 0; t.rstride = 0;
-    t.tile_off = 0; t.ring_base = nullptr; t.delta_lo = nullptr; t.delta_hi = nullptr;
-    const size_t tile_lds = size_t(kTileBytes);
-    const bool delta = op_combines(a.op) && a.n > thresh;
-    const unsigned dgrid = unsigned(std::min<uint64_t>(2 * ((a.n + kSplit - 1) / kSplit), uint64_t(tile_grid_cap())));
-    auto apply_tiles = [&](unsigned ntiles) {
-        return dispatch_dtype(dtype, [&](auto tag) {
-            using T = decltype(tag);
-            auto go = [&](auto opt) {
-                constexpr int OPT = decltype(opt)::value;
-                hipLaunchKernelGGL((k_tile_owner<T, OPT>), dim3(ntiles), dim3(1024), tile_lds, s, t);
-                if (delta) hipLaunchKernelGGL((k_tile_delta<T, OPT>), dim3(dgrid), dim3(1024), tile_lds, s, t);
-            };
-            if (a.op == LMR_OP_ADD) go(std::integral_constant<int, LMR_OP_ADD>{});
-            else if (a.op == LMR_OP_FETCH_ADD) go(std::integral_constant<int, LMR_OP_FETCH_ADD>{});
-            else go(std::integral_constant<int, -1>{});
-            return hipGetLastError();
-        });
-    };
-    if (!grouped) {
-        e = apply_tiles(unsigned(num_tiles));
-        ps.end();
-    } else {
-        // Fine pass and tile apply per group of coarse buckets: a group's bins are
-        // written at the start of the bin buffer and read back by its tile apply at
-        // once, so that round trip stays in the 256 MiB Infinity Cache instead of HBM
-        // (tools/mallbench: write+read of a <= 256 MB ring at 6.3-6.9 TB/s vs 4.8 TB/s).
-        ps.end();
-        const uint32_t C = qf.C;
-        const uint64_t per_bucket = (a.n + C - 1) / C;
-        uint32_t gb = uint32_t(std::max<uint64_t>(1, uint64_t(group_records()) / std::max<uint64_t>(per_bucket, 1)));
-        if (gb > C) gb = C;
-        for (uint32_t c0 = 0; c0 < C && e == hipSuccess; c0 += gb) {
-            const uint32_t c1 = std::min(C, c0 + gb);
-            const uint32_t t0 = c0 * kFine, t1 = std::min(uint32_t(num_tiles), c1 * kFine);
-            {
-                ProfScope pf(a.prof, LMR_STAGE_FINE_SCATTER, s);
-                PartArgs qg = qf;
-                qg.cg_lo = c0 * qf.G; qg.cg_hi = c1 * qf.G; qg.ring_base = w.tile_start + t0;
-                launch_fine(qg, vb, s);
-            }
-            ProfScope pt(a.prof, LMR_STAGE_TILE_APPLY, s);
-            t.tile_off = t0;
-            t.ring_base = w.tile_start + t0;
-            t.delta_lo = w.tile_items2 + t0;                              // exclusive scan of delta pieces
-            t.delta_hi = (t1 < uint32_t(num_tiles)) ? w.tile_items2 + t1 : w.item_count;
-            e = apply_tiles(t1 - t0);
-        }
-    }
+    e = launch_tile_sweep(dtype, a, w, T, a.n, a.val == nullptr, has_res ? res_bin : nullptr,
+                          has_res ? ok_bin : nullptr, s);
     if (e != hipSuccess || !has_res) return e;
     // un-partition: binned -> (temp ->) input order, each a block-contiguous gather
     ProfScope pu(a.prof, LMR_STAGE_UNPARTITION, s);
     const uint8_t* ok_src = (a.ret == LMR_RET_RESULT) ? ok_bin : nullptr;
-    auto gather = [&](const uint32_t* map, const uint32_t* n_dev, const uint32_t* bound_dev, const uint8_t* src,
-                      uint8_t* dst, const uint8_t* oks, uint8_t* okd) {
+    auto gather = [&](const uint32_t* map, const uint32_t* n_dev, const uint8_t* src, uint8_t* dst,
+                      const uint8_t* oks, uint8_t* okd) {
         switch (vb) {
-        case 1: hipLaunchKernelGGL((k_unpartition<1>), dim3(unsigned(G)), dim3(1024), 0, s, map, a.n, n_dev, bound_dev, b.chunk, src, dst, oks, okd); break;
-        case 2: hipLaunchKernelGGL((k_unpartition<2>), dim3(unsigned(G)), dim3(1024), 0, s, map, a.n, n_dev, bound_dev, b.chunk, src, dst, oks, okd); break;
-        case 4: hipLaunchKernelGGL((k_unpartition<4>), dim3(unsigned(G)), dim3(1024), 0, s, map, a.n, n_dev, bound_dev, b.chunk, src, dst, oks, okd); break;
-        default: hipLaunchKernelGGL((k_unpartition<8>), dim3(unsigned(G)), dim3(1024), 0, s, map, a.n, n_dev, bound_dev, b.chunk, src, dst, oks, okd); break;
+        case 1: hipLaunchKernelGGL((k_unpartition<1>), dim3(unsigned(G)), dim3(1024), 0, s, map, a.n, n_dev, b.chunk, src, dst, oks, okd); break;
+        case 2: hipLaunchKernelGGL((k_unpartition<2>), dim3(unsigned(G)), dim3(1024), 0, s, map, a.n, n_dev, b.chunk, src, dst, oks, okd); break;
+        case 4: hipLaunchKernelGGL((k_unpartition<4>), dim3(unsigned(G)), dim3(1024), 0, s, map, a.n, n_dev, b.chunk, src, dst, oks, okd); break;
+        default: hipLaunchKernelGGL((k_unpartition<8>), dim3(unsigned(G)), dim3(1024), 0, s, map, a.n, n_dev, b.chunk, src, dst, oks, okd); break;
         }
     };
-    if (num_tiles > uint64_t(kFine) && slot_maps) {
+    if (num_tiles > uint64_t(kFine)) {
         uint8_t* ok_tmp = ok_src ? reinterpret_cast<uint8_t*>(w.bin_lidx) : nullptr;
-        const uint32_t C = uint32_t((num_tiles + kFine - 1) / kFine);
-        UnArgs u{};
-        u.coarse_off = w.coarse_off; u.cg_lo = 0; u.cg_hi = C * uint32_t(G); u.G = uint32_t(G);
-        u.num_tiles = uint32_t(num_tiles); u.n = a.n; u.chunk = b.chunk;
-        // binned -> temp order, replaying the fine rounds
-        u.src = res_bin; u.dst = w.bin_val; u.ok_src = ok_src; u.ok_dst = ok_tmp;
-        u.slot = reinterpret_cast<const uint16_t*>(w.rpos); u.log = w.rlog + clog_words; u.stride = kFine;
-        const uint64_t nseg = uint64_t(C) * G;
-        const unsigned fgrid = unsigned(nseg < uint64_t(fine_blocks_cap()) ? nseg : fine_blocks_cap());
-        dispatch_vb_rpt<2>(vb, fine_rpt(vb), [&](auto vbt, auto rpt) {
-            constexpr int VBc = decltype(vbt)::value, KR = decltype(rpt)::value * 1024;
-            u.kround = KR;
-            hipLaunchKernelGGL((k_unfine<VBc, KR>), dim3(fgrid ? fgrid : 1u), dim3(1024), 0, s, u);
-        });
-        // temp -> input order, replaying the coarse rounds
-        u.src = w.bin_val; u.dst = reinterpret_cast<uint8_t*>(a.results); u.ok_src = ok_tmp; u.ok_dst = a.ok;
-        u.slot = reinterpret_cast<const uint16_t*>(w.qpos); u.log = w.rlog; u.stride = C;
-        dispatch_vb_rpt<4>(vb, coarse_rpt(vb), [&](auto vbt, auto rpt) {
-            constexpr int VBc = decltype(vbt)::value, KR = decltype(rpt)::value * 1024;
-            u.kround = KR;
-            hipLaunchKernelGGL((k_uncoarse<VBc, KR>), dim3(unsigned(G)), dim3(1024), 0, s, u);
-        });
-    } else if (num_tiles > uint64_t(kFine)) {
-        uint8_t* ok_tmp = ok_src ? reinterpret_cast<uint8_t*>(w.bin_lidx) : nullptr;
-        if (rm)   // temp slots are input positions (holes where records were out of bounds)
-            gather(w.rpos, nullptr, w.total, res_bin, w.bin_val, ok_src, ok_tmp);
-        else
-            gather(w.rpos, w.total, nullptr, res_bin, w.bin_val, ok_src, ok_tmp);          // binned -> temp
-        gather(w.qpos, nullptr, nullptr, w.bin_val, reinterpret_cast<uint8_t*>(a.results), ok_tmp, a.ok);  // temp -> input
+        gather(w.rpos, w.total, res_bin, w.bin_val, ok_src, ok_tmp);                                       // binned -> temp
+        gather(w.qpos, nullptr, w.bin_val, reinterpret_cast<uint8_t*>(a.results), ok_tmp, a.ok);           // temp -> input
     } else {
-        gather(w.rpos, nullptr, nullptr, res_bin, reinterpret_cast<uint8_t*>(a.results), ok_src, a.ok);
+        gather(w.rpos, nullptr, res_bin, reinterpret_cast<uint8_t*>(a.results), ok_src, a.ok);
     }
     return hipGetLastError();
 }
@@ -2389,31 +1798,16 @@ bool stage_free_applies(int dtype, int op, int ret, uint64_t shard_len, uint64_t
     return free_partition_applies(dtype, op, ret, shard_len, 0, cap);
 }
 
-static PartArgs stage_free_args(int dtype, const ApplyArgs& a, const TiledWs& w) {
-    const int shift = tile_shift_for(dtype);
-    const uint32_t T = uint32_t((a.shard_len + (uint64_t(1) << shift) - 1) >> shift);
-    PartArgs q{};
-    q.shard_len = a.shard_len; q.tile_shift = shift; q.num_tiles = T;
-    q.G = kStageFreeBlocks; q.C = (T + kFine - 1) / kFine;
-    q.tile_start = w.tile_start; q.counts = w.counts;
-    q.tmp_idx = w.tmp_idx; q.tmp_val = w.tmp_val;          // values always materialised
-    q.bin_lidx = w.bin_lidx; q.bin_val = w.bin_val;
-    q.err = a.err;
-    q.ff_flag = w.rlog; q.ff_fill = w.rlog + 64; q.ff_tfill = w.rlog + 64 + kMaxCoarse;
-    q.capc = uint32_t(w.tmp_cap / q.C); q.tmp_cap = w.tmp_cap;
-    q.spill = 1; q.accumulate = 1; q.shard = a.shard; q.op = a.op;
-    return q;
-}
-
 static hipError_t stage_region_free(int dtype, int index_size, const ApplyArgs& a, const TiledWs& w,
                                     StageSession& s, hipStream_t st) {
-    PartArgs q = stage_free_args(dtype, a, w);
+    PartArgs q = free_args(dtype, a, w, kStageFreeBlocks);
+    q.accumulate = 1;                                      // tile-count rows add up over the session
     const int vb = dtype_bytes(dtype);
     const int frpt = free_partition_rpt(dtype, a.op, a.ret, 0, q.num_tiles, w.tmp_cap);
     if (frpt == 0 || s.nreg >= kMaxRegions) return hipErrorInvalidValue;
     hipError_t e;
-    if (!s.free_armed) {                                    // fill counters, flag, tile-count rows
-        e = hipMemsetAsync(w.rlog, 0, (64 + kMaxCoarse + size_t(q.num_tiles)) * 4, st);
+    if (!s.free_armed) {                                   // fill counters, tile-count rows
+        e = hipMemsetAsync(w.ff, 0, ff_words() * 4, st);
         if (e == hipSuccess) e = hipMemsetAsync(w.counts, 0, size_t(q.G) * q.num_tiles * 4, st);
         if (e != hipSuccess) return e;
         s.free_armed = true;
@@ -2422,14 +1816,7 @@ static hipError_t stage_region_free(int dtype, int index_size, const ApplyArgs& 
     q.val_bits = a.val_bits; q.n = a.n; q.chunk = (a.n + q.G - 1) / q.G;
     {
         ProfScope ps(a.prof, LMR_STAGE_BIN_SCATTER, st);
-        e = dispatch_iw(index_size, [&](auto iw) {
-            constexpr int IW = decltype(iw)::value;
-            dispatch_vb_rpt<4>(vb, frpt, [&](auto vbt, auto rpt) {
-                constexpr int VBc = decltype(vbt)::value, R = decltype(rpt)::value;
-                hipLaunchKernelGGL((k_coarse_free<IW, VBc, R>), dim3(q.G), dim3(1024), size_t(q.num_tiles) * 4, st, q);
-            });
-            return hipGetLastError();
-        });
+        e = launch_coarse_free(index_size, vb, frpt, q, st);
     }
     if (e != hipSuccess) return e;
     s.reg[s.nreg] = StageRegion{0, a.n, nullptr, nullptr};
@@ -2441,63 +1828,10 @@ static hipError_t stage_region_free(int dtype, int index_size, const ApplyArgs& 
 static hipError_t stage_finish_free(const TiledWs& w, StageSession& s, hipStream_t st) {
     const ApplyArgs& a = s.a;
     const int dtype = s.dtype, vb = dtype_bytes(dtype);
-    PartArgs q = stage_free_args(dtype, a, w);
-    const uint32_t T = q.num_tiles;
-    hipError_t e;
-    {
-        ProfScope ps(a.prof, LMR_STAGE_SCAN, st);
-        hipLaunchKernelGGL(k_free_tile_totals, dim3((T + 63) / 64), dim3(1024), 0, st, w.counts, T, q.G, w.tile_start);
-        e = scan_exclusive_u32(w.tile_start, T, w.partials, w.tile_start + T, st);
-    }
-    if (e != hipSuccess) return e;
-    {
-        ProfScope ps(a.prof, LMR_STAGE_FINE_SCATTER, st);
-        dispatch_vb_rpt<2>(vb, fine_rpt(vb), [&](auto vbt, auto rpt) {
-            constexpr int VBc = decltype(vbt)::value, R = decltype(rpt)::value;
-            hipLaunchKernelGGL((k_fine_free<VBc, R>), dim3(unsigned(fine_blocks_cap())), dim3(1024), 0, st, q);
-        });
-        e = hipGetLastError();
-    }
-    if (e != hipSuccess) return e;
-    {
-        ProfScope ps(a.prof, LMR_STAGE_TILE_APPLY, st);
-        const uint64_t n = s.staged;
-        const uint64_t avg = (n + T - 1) / T;
-        const uint32_t thresh = uint32_t(std::min<uint64_t>(0xFFFFFFFFull, std::max<uint64_t>(4 * avg, 65536)));
-        const unsigned pg = (T + 255) / 256;
-        hipLaunchKernelGGL(k_tile_plan_count, dim3(pg), dim3(256), 0, st, w.tile_start, T, thresh,
-                           op_combines(a.op) ? 1 : 0, w.tile_items);
-        hipLaunchKernelGGL(k_tile_plan_extra, dim3(pg), dim3(256), 0, st, w.tile_items, T, w.tile_items2);
-        e = scan_exclusive_u32(w.tile_items2, T, w.plan_partials, w.item_count, st);
-        if (e != hipSuccess) return e;
-        TileItem* items = reinterpret_cast<TileItem*>(w.items);
-        hipLaunchKernelGGL(k_tile_plan_fill, dim3(pg), dim3(256), 0, st, w.tile_start, T, w.tile_items2,
-                           w.tile_items, items, items + kMaxTiles);
-        TileArgs t;
-        t.shard = a.shard; t.shard_len = a.shard_len; t.tile_shift = q.tile_shift;
-        t.kind = a.kind; t.op = a.op; t.ret = LMR_RET_NONE;
-        t.cmp_bits = 0; t.eps_bits = 0; t.val_bits = 0;
-        t.scalar = false;                                         // values are materialised in the bins
-        t.items = items; t.delta = items + kMaxTiles; t.delta_count = w.item_count;
-        t.num_tiles = T;
-        t.bin_lidx = w.bin_lidx; t.bin_val = w.bin_val;
-        t.results = nullptr; t.ok = nullptr; t.err = a.err;
-        t.rts = nullptr; t.nreg = 0; t.rstride = 0;
-        t.tile_off = 0; t.ring_base = nullptr; t.delta_lo = nullptr; t.delta_hi = nullptr;
-        const bool delta = op_combines(a.op) && n > thresh;
-        const unsigned dgrid = unsigned(std::min<uint64_t>(2 * ((n + kSplit - 1) / kSplit), uint64_t(tile_grid_cap())));
-        e = dispatch_dtype(dtype, [&](auto tag) {
-            using Ty = decltype(tag);
-            auto go = [&](auto opt) {
-                constexpr int OPT = decltype(opt)::value;
-                hipLaunchKernelGGL((k_tile_owner<Ty, OPT>), dim3(T), dim3(1024), size_t(kTileBytes), st, t);
-                if (delta) hipLaunchKernelGGL((k_tile_delta<Ty, OPT>), dim3(dgrid), dim3(1024), size_t(kTileBytes), st, t);
-            };
-            if (a.op == LMR_OP_ADD) go(std::integral_constant<int, LMR_OP_ADD>{});
-            else go(std::integral_constant<int, -1>{});
-            return hipGetLastError();
-        });
-    }
+    PartArgs q = free_args(dtype, a, w, kStageFreeBlocks);
+    hipError_t e = launch_free_finish(vb, q, w, a.prof, st);
+    // values are materialised in the bins (regions may mix array and scalar values)
+    if (e == hipSuccess) e = launch_tile_sweep(dtype, a, w, q.num_tiles, s.staged, false, nullptr, nullptr, st);
     s.nreg = 0;
     s.staged = 0;
     s.free_armed = false;
@@ -2553,7 +1887,7 @@ hipError_t launch_stage_region(int dtype, int index_size, const ApplyArgs& a, co
             constexpr int IW = decltype(iw)::value;
             dispatch_vb_rpt<4>(vb, coarse_rpt(vb), [&](auto vbt, auto rpt) {
                 constexpr int VBc = decltype(vbt)::value, RP = decltype(rpt)::value;
-                hipLaunchKernelGGL((k_coarse_scatter<IW, VBc, RP, 1024>), dim3(unsigned(G)), dim3(1024), 0, st, q);
+                hipLaunchKernelGGL((k_coarse_scatter<IW, VBc, RP>), dim3(unsigned(G)), dim3(1024), 0, st, q);
             });
             return hipGetLastError();
         });
@@ -2625,7 +1959,6 @@ hipError_t launch_stage_finish(const TiledWs& w, StageSession& s, hipStream_t st
         t.bin_lidx = w.bin_lidx; t.bin_val = w.bin_val;
         t.results = res_bin; t.ok = ok_bin; t.err = a.err;
         t.rts = w.rts; t.nreg = uint32_t(s.nreg); t.rstride = stride;
-        t.tile_off = 0; t.ring_base = nullptr; t.delta_lo = nullptr; t.delta_hi = nullptr;
         const bool delta = op_combines(a.op) && s.staged > thresh;
         const unsigned dgrid = unsigned(std::min<uint64_t>(2 * ((s.staged + kSplit - 1) / kSplit) + 2 * uint64_t(s.nreg),
                                                            uint64_t(tile_grid_cap())));
@@ -2655,10 +1988,10 @@ hipError_t launch_stage_finish(const TiledWs& w, StageSession& s, hipStream_t st
             if (Gu < 1) Gu = 1;
             const uint64_t chunk = (n + Gu - 1) / Gu;
             switch (vb) {
-            case 1: hipLaunchKernelGGL((k_unpartition<1>), dim3(unsigned(Gu)), dim3(1024), 0, st, map, n, n_dev, nullptr, chunk, src, dst, oks, okd); break;
-            case 2: hipLaunchKernelGGL((k_unpartition<2>), dim3(unsigned(Gu)), dim3(1024), 0, st, map, n, n_dev, nullptr, chunk, src, dst, oks, okd); break;
-            case 4: hipLaunchKernelGGL((k_unpartition<4>), dim3(unsigned(Gu)), dim3(1024), 0, st, map, n, n_dev, nullptr, chunk, src, dst, oks, okd); break;
-            default: hipLaunchKernelGGL((k_unpartition<8>), dim3(unsigned(Gu)), dim3(1024), 0, st, map, n, n_dev, nullptr, chunk, src, dst, oks, okd); break;
+            case 1: hipLaunchKernelGGL((k_unpartition<1>), dim3(unsigned(Gu)), dim3(1024), 0, st, map, n, n_dev, chunk, src, dst, oks, okd); break;
+            case 2: hipLaunchKernelGGL((k_unpartition<2>), dim3(unsigned(Gu)), dim3(1024), 0, st, map, n, n_dev, chunk, src, dst, oks, okd); break;
+            case 4: hipLaunchKernelGGL((k_unpartition<4>), dim3(unsigned(Gu)), dim3(1024), 0, st, map, n, n_dev, chunk, src, dst, oks, okd); break;
+            default: hipLaunchKernelGGL((k_unpartition<8>), dim3(unsigned(Gu)), dim3(1024), 0, st, map, n, n_dev, chunk, src, dst, oks, okd); break;
             }
         };
         for (int r = 0; r < s.nreg; r++) {

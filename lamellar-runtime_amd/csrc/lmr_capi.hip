@@ -309,7 +309,7 @@ lmr_status_t lmr_ctx_destroy(lmr_ctx_t* ctx) {
 
 lmr_status_t lmr_ctx_reserve(lmr_ctx_t* ctx, uint64_t max_records) {
     if (!ctx) return LMR_E_INVALID;
-    if (max_records > 0xFFFFFFFFull) max_records = 0xFFFFFFFFull;
+    if (max_records > max_rec_cap()) max_records = max_rec_cap();
     if (ctx->stage && ctx->stage->s.nreg > 0) return LMR_E_INVALID;   // staged records live in the workspace
     (void)hipSetDevice(ctx->device);
     if (ctx->ws) { (void)hipFree(ctx->ws); ctx->ws = nullptr; ctx->ws_bytes = 0; ctx->rec_cap = 0; }

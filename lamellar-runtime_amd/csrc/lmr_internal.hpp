@@ -65,17 +65,15 @@ struct TiledWs {
     uint32_t* plan_partials;
     uint32_t* item_count;  // [1]
     uint8_t* items;        // TileItem[kMaxTiles] owner items, then delta pieces
-    uint16_t* rhist;       // round-major partition: per-round bucket counts
-    uint16_t* rbase;       //                         per-round bucket offsets
     uint32_t* rts;         // staged apply: [kMaxRegions][kMaxTiles + 1] tile starts of each region
     uint32_t* sinfo;       // staged apply: piece table (pbase, bstart) + per-region in-bounds totals
-    uint32_t* rlog;        // per-round bucket cursors / counts of the partition passes (returning ops);
-                           // the count-free partition's flag and fill counters otherwise
-    size_t rlog_words;
+    uint32_t* ff;          // count-free partition: bucket and tile fill counters
     uint64_t cap;          // records of one tiled piece (bin arrays, position maps)
     uint64_t tmp_cap;      // records the temp arrays (tmp_idx / tmp_val) hold, > cap
 };
 size_t tiled_ws_bytes(uint64_t cap);
+// largest workspace capacity (records) whose temp slots fit the kernels' uint32 slot math
+uint64_t max_rec_cap();
 TiledWs carve_tiled_ws(uint8_t* base, uint64_t cap);
 
 // exclusive scan of d[0..m) in place; *d_total = sum (may be null). partials

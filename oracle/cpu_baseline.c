@@ -28,6 +28,7 @@ typedef struct {
     uint64_t num_per_batch;
     uint8_t* bytes;        /* n records */
     uint8_t* locks;        /* per element, floats only */
+    uint64_t cmp_bits;     /* compare_exchange(current) */
     void* results;
     /* op buffers: [buf_start[b], buf_start[b+1]) record ranges */
     uint64_t* buf_start;
@@ -73,9 +74,15 @@ static void* pack_thread(void* p) {
     } while (0)
 
 #define NATIVE_APPLY(NAME, T, UT, WT)                                                      \
-static T native_##NAME(T* a, T v, uint32_t op) {                                           \
+static T native_##NAME(T* a, T v, uint32_t op, uint64_t cmp_bits) {                        \
     T res = 0;                                                                             \
     switch (op) {                                                                          \
+    case LMR_OP_COMPARE_EXCHANGE: {                                                        \
+        /* array_ops.rs:387-390: compare_exchange(current, new) -> Ok(current) / Err(actual) */ \
+        T cur; memcpy(&cur, &cmp_bits, sizeof(T));                                          \
+        T exp = cur;                                                                       \
+        __atomic_compare_exchange_n(a, &exp, v, 0, __ATOMIC_SEQ_CST, __ATOMIC_SEQ_CST);   \
+        res = exp; break; }                                                                \
     case LMR_OP_ADD: case LMR_OP_FETCH_ADD: res = __atomic_fetch_add(a, v, __ATOMIC_SEQ_CST); break; \
     case LMR_OP_SUB: case LMR_OP_FETCH_SUB: res = __atomic_fetch_sub(a, v, __ATOMIC_SEQ_CST); break; \
     case LMR_OP_AND: case LMR_OP_FETCH_AND: res = __atomic_fetch_and(a, v, __ATOMIC_SEQ_CST); break; \
@@ -132,7 +139,7 @@ static void* apply_thread(void* p) {
             const uint8_t* vp = r + j->vo;
 #define DO(D, NAME, T)                                                                     \
             case D: { T v; memcpy(&v, vp, sizeof(T));                                      \
-                T o = native_##NAME((T*)j->shard + idx, v, j->op);                         \
+                T o = native_##NAME((T*)j->shard + idx, v, j->op, j->cmp_bits);            \
                 if (ret) { ((T*)j->results)[k] = o; } break; }
 #define DOF(D, NAME, T)                                                                    \
             case D: { T v; memcpy(&v, vp, sizeof(T));                                      \
@@ -154,7 +161,7 @@ static void* apply_thread(void* p) {
 
 int cpu_baseline_run(uint32_t dtype, uint32_t op, void* shard, uint64_t shard_len,
                      const uint64_t* gidx, const void* vals, const void* val, uint64_t n,
-                     uint32_t threads, uint64_t am_size_threshold, void* results,
+                     uint32_t threads, uint64_t am_size_threshold, const void* cmp, void* results,
                      cpu_times_t* out) {
     if (threads == 0) threads = 1;
     if (threads > 1024) threads = 1024;
@@ -170,6 +177,7 @@ int cpu_baseline_run(uint32_t dtype, uint32_t op, void* shard, uint64_t shard_le
     j->shard = shard; j->shard_len = shard_len; j->gidx = gidx;
     j->vals = (const uint8_t*)vals; j->val = (const uint8_t*)val; j->n = n;
     j->results = results;
+    if (cmp) memcpy(&j->cmp_bits, cmp, j->tb);
     j->num_per_batch = (uint64_t)ceilf((float)am_size_threshold / (float)j->rb);
     if (j->num_per_batch == 0) j->num_per_batch = 1;
     j->bytes = (uint8_t*)malloc(n * j->rb + 1);

@@ -35,7 +35,7 @@ typedef struct {
  * results (may be NULL) receive fetch values in input order. */
 int cpu_baseline_run(uint32_t dtype, uint32_t op, void* shard, uint64_t shard_len,
                      const uint64_t* gidx, const void* vals, const void* val, uint64_t n,
-                     uint32_t threads, uint64_t am_size_threshold, void* results,
+                     uint32_t threads, uint64_t am_size_threshold, const void* cmp, void* results,
                      cpu_times_t* out);
 
 #ifdef __cplusplus

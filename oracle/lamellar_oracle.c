@@ -391,6 +391,21 @@ static int apply_elem(void* slice, uint64_t index, uint32_t kind, uint32_t dtype
 #undef CASE
 }
 
+int orc_elem_step(uint32_t kind, uint32_t dtype, uint32_t op, uint64_t state_bits, uint64_t val_bits,
+                  const void* cmp, const void* eps, uint64_t* new_bits, uint64_t* ret_bits, uint8_t* ok) {
+    const uint32_t eb = orc_dtype_bytes(dtype);
+    uint8_t elem[8] = {0}, val[8] = {0}, res[8] = {0};
+    memcpy(elem, &state_bits, eb);          /* little endian: the low eb bytes */
+    memcpy(val, &val_bits, eb);
+    *ok = 0;
+    const int st = apply_elem(elem, 0, kind, dtype, op, val, cmp, eps, res, ok);
+    *new_bits = 0;
+    *ret_bits = 0;
+    memcpy(new_bits, elem, eb);
+    memcpy(ret_bits, res, eb);
+    return st;
+}
+
 static uint64_t read_index(const uint8_t* p, uint32_t index_size) {
     switch (index_size) {
     case 1: return p[0];

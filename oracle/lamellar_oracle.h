@@ -114,6 +114,23 @@ void orc_reduce(uint32_t dtype, uint32_t op, const void* data, uint64_t n, void*
 void orc_reduce_tree(uint32_t dtype, uint32_t op, const void* vals, const uint8_t* has, uint32_t npes,
                      void* out, uint8_t* out_has);
 
+/* ---- per-record step and the linearisability checker (linearize.c) ----
+ * orc_elem_step: one record applied to a register copy of an element (the
+ * semantics of apply_elem above): new state, returned bits, Ok flag.
+ * orc_check_linearizable: for every element of one slice, is there a serial order
+ * of that element's records (idx[k] == element) that reproduces each record's
+ * returned value (rets, element-sized; NULL = not checked) and Ok flag (oks, NULL =
+ * not checked) and ends at final_slice[element]? vals: n values, or one (v_len == 1).
+ * Records with idx >= slice_len are ignored. Returns 0 = linearisable, 1 = not (the
+ * element in *bad_elem), 2 = undecided within max_nodes branch steps, < 0 = error. */
+int orc_elem_step(uint32_t kind, uint32_t dtype, uint32_t op, uint64_t state_bits, uint64_t val_bits,
+                  const void* cmp, const void* eps, uint64_t* new_bits, uint64_t* ret_bits, uint8_t* ok);
+int orc_check_linearizable(uint32_t kind, uint32_t dtype, uint32_t op, const void* cmp, const void* eps,
+                           const void* init_slice, const void* final_slice, uint64_t slice_len,
+                           const uint64_t* idx, uint64_t n, const void* vals, uint64_t v_len,
+                           const void* rets, const uint8_t* oks, uint64_t max_nodes,
+                           uint64_t* bad_elem);
+
 /* result reorder: ArrayFetchBatchOpHandle (operations/handle.rs:315-317) */
 void orc_scatter_results(const void* res_in, const uint64_t* res_pos, uint64_t n,
                          uint32_t elem_bytes, void* res_out);

@@ -77,8 +77,13 @@ def lib():
             "orc_scatter_results": (None, [c_void_p, c_void_p, c_uint64, c_uint32, c_void_p]),
             "orc_reduce": (None, [c_uint32, c_uint32, c_void_p, c_uint64, c_void_p, c_void_p]),
             "orc_reduce_tree": (None, [c_uint32, c_uint32, c_void_p, c_void_p, c_uint32, c_void_p, c_void_p]),
+            "orc_elem_step": (c_int, [c_uint32, c_uint32, c_uint32, c_uint64, c_uint64, c_void_p, c_void_p,
+                                      POINTER(c_uint64), POINTER(c_uint64), POINTER(c_uint8)]),
+            "orc_check_linearizable": (c_int, [c_uint32, c_uint32, c_uint32, c_void_p, c_void_p, c_void_p,
+                                               c_void_p, c_uint64, c_void_p, c_uint64, c_void_p, c_uint64,
+                                               c_void_p, c_void_p, c_uint64, POINTER(c_uint64)]),
             "cpu_baseline_run": (c_int, [c_uint32, c_uint32, c_void_p, c_uint64, c_void_p, c_void_p,
-                                         c_void_p, c_uint64, c_uint32, c_uint64, c_void_p,
+                                         c_void_p, c_uint64, c_uint32, c_uint64, c_void_p, c_void_p,
                                          POINTER(CpuTimes)]),
         }
         for k, (r, a) in sig.items():
@@ -216,7 +221,7 @@ def pack(L, dtype_code, np_dtype, gidx, vals, iw, threshold=100000, threads=1):
 
 
 def cpu_baseline(dtype_code, np_dtype, op, shard, gidx, vals, threads, threshold=100000,
-                 want_results=False):
+                 want_results=False, current=None):
     """Reference-structured threaded CPU apply (bench.py cpu_baseline leg)."""
     gidx = np.ascontiguousarray(gidx, dtype=np.uint64)
     n = gidx.size
@@ -228,9 +233,30 @@ def cpu_baseline(dtype_code, np_dtype, op, shard, gidx, vals, threads, threshold
         v = np.ascontiguousarray(np.asarray(vals).astype(np_dtype))
     res = np.zeros(n, dtype=np_dtype) if want_results else None
     t = CpuTimes()
+    c = _scalar_buf(current, np_dtype)
     st = lib().cpu_baseline_run(dtype_code, op, shard.ctypes.data, shard.size, _ptr(gidx), _ptr(v),
-                                _ptr(sv), n, threads, threshold, _ptr(res), ctypes.byref(t))
+                                _ptr(sv), n, threads, threshold, _ptr(c), _ptr(res), ctypes.byref(t))
     return st, t, res
+
+
+def check_linearizable(kind, dtype_code, np_dtype, op, init, final, idx, vals, rets=None, oks=None,
+                       current=None, eps=None, max_nodes=1 << 22):
+    """Per element: do the returned values / Ok flags and the final value come from
+    some serial order of that element's records (linearize.c)? -> (status, element):
+    status 0 = linearisable, 1 = not (element names one), 2 = undecided."""
+    init = np.ascontiguousarray(np.asarray(init).astype(np_dtype))
+    final = np.ascontiguousarray(np.asarray(final).astype(np_dtype))
+    assert init.size == final.size
+    idx = np.ascontiguousarray(np.asarray(idx, dtype=np.uint64).reshape(-1))
+    vals = np.ascontiguousarray(np.asarray(vals).astype(np_dtype).reshape(-1))
+    rets = None if rets is None else np.ascontiguousarray(np.asarray(rets).astype(np_dtype).reshape(-1))
+    oks = None if oks is None else np.ascontiguousarray(np.asarray(oks, dtype=np.uint8).reshape(-1))
+    c, e = _scalar_buf(current, np_dtype), _scalar_buf(eps, np_dtype)
+    bad = c_uint64(0)
+    st = lib().orc_check_linearizable(kind, dtype_code, op, _ptr(c), _ptr(e), _ptr(init), _ptr(final), init.size,
+                                      _ptr(idx), idx.size, _ptr(vals), vals.size, _ptr(rets), _ptr(oks),
+                                      max_nodes, ctypes.byref(bad))
+    return st, bad.value
 
 
 REDUCE_OPS = {"sum": 0, "prod": 1, "max": 2, "min": 3}

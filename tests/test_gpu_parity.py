@@ -377,32 +377,16 @@ def test_device_errors(world, lam, strategy):
         k.strategy = old
 
 
-@pytest.fixture(params=["count", "free", "rm", "staged", "grouped", "match", "slotmap"])
+@pytest.fixture(params=["count", "free", "staged"])
 def partition(request, monkeypatch):
     """Two-level partition variant: count pass + bucket-major temp ("count"), the
-    round-major temp with the tile counts built in the coarse pass ("rm"), or the
     staged pipeline (coarse pass, then fixed-size pieces counted and sorted by tile)
-    with every call cut into 3 regions applied in one sweep ("staged"), or the count
-    pass with the fine pass and tile apply run per group of coarse buckets ("grouped"), or the
-    count pass with records ranked by wave key matching in the LDS rounds ("match"), or the count
-    pass with returned values brought back by slot maps and round logs ("slotmap"), or the
-    default selection, where order-insensitive integer ops that return nothing take the
+    with every call cut into 3 regions applied in one sweep ("staged"), or the default
+    selection, where order-insensitive integer ops that return nothing take the
     count-free partition ("free"; "count" switches it off)."""
     monkeypatch.setenv("LMR_FREE", "0" if request.param == "count" else "1")
-    monkeypatch.delenv("LMR_PARTITION", raising=False)
     monkeypatch.setenv("LMR_STAGED", "0")          # the segment-based fine pass unless "staged"
-    monkeypatch.delenv("LMR_GROUP_RECORDS", raising=False)
-    monkeypatch.delenv("LMR_MATCH_RANK", raising=False)
-    monkeypatch.delenv("LMR_SLOT_UNPARTITION", raising=False)
-    if request.param == "slotmap":
-        monkeypatch.setenv("LMR_SLOT_UNPARTITION", "1")
-    if request.param == "match":
-        monkeypatch.setenv("LMR_MATCH_RANK", "1")
-    if request.param == "grouped":
-        monkeypatch.setenv("LMR_GROUP_RECORDS", "100000")
-    if request.param == "rm":
-        monkeypatch.setenv("LMR_PARTITION", "rm")
-    elif request.param == "staged":
+    if request.param == "staged":
         monkeypatch.setenv("LMR_STAGED", "1")
         monkeypatch.setenv("LMR_STAGE_SPLIT", "3")
     return request.param
@@ -545,19 +529,26 @@ def test_free_partition_collisions_bit_exact(world, orc, lam, dt, shape, monkeyp
 
 
 @pytest.mark.parametrize("dt", ["u64", "u16"])
-def test_free_partition_bucket_overflow_falls_back(world, orc, lam, dt, monkeypatch):
+def test_free_partition_bucket_overflow_spills(world, orc, lam, dt, monkeypatch):
     """Records concentrated on one coarse bucket (128 tiles) overflow its region in the
-    count-free partition; the counted pipeline queued behind it takes over on the
-    device, and the state is still the oracle's. Also a batch split over two buckets and
-    one with 1 % out-of-bounds records (error bit raised, the rest applied)."""
+    count-free partition: the records that find the region full are applied at once with
+    device atomics (spill), the rest through the tiles, and the state is still the
+    oracle's. The batch holds at least twice the region, so the spill surely runs (the
+    region size follows the reserved workspace, which earlier tests may have grown). Also
+    a batch split over two buckets and one with 1 % out-of-bounds records (error bit
+    raised, the rest applied)."""
     monkeypatch.setenv("LMR_FREE", "1")
     k = world.team().kernels
     k.reserve(1 << 22)
+    R = k.reserved
     rng = np.random.default_rng(5)
     t = NP[dt]
     tile = 8192 if t(0).itemsize == 8 else 16384
     shard_len = 640 * tile + 3                     # 641 tiles: 6 coarse buckets
-    n = 1 << 21
+    C = 6
+    capc = (R + R // 4 + 128 * 8192) // C           # one coarse bucket's region of the temp arrays
+    n = min(max(1 << 21, 2 * capc + 4096), R)
+    assert n >= 2 * capc, "workspace too large for a forced spill"
     shard0 = rand_elems(dt, shard_len, rng, ADD)
     cases = [rng.integers(0, 128 * tile, n),                                   # all in bucket 0
              np.where(rng.random(n) < 0.5, rng.integers(0, 50, n),

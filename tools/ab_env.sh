@@ -10,6 +10,6 @@ steps=20; [ "$cfg" = c4 ] && steps=10
 for i in $(seq $reps); do
   for s in "$@"; do
     env $extra $s timeout -k 10 200 python bench.py --config $cfg --steps $steps --warmup 5 --no-cpu-baseline 2>/dev/null | grep '^{' | \
-      python -c "import sys,json; d=json.loads(sys.stdin.read()); st=d.get('apply_pipeline',{}).get('stages_ms_per_step',{}); print('$cfg', '[$s]', round(d['ms_per_step'],3), {k: round(v,3) for k,v in st.items()})" || exit 1
+      python -c "import sys,json; d=json.loads(sys.stdin.read()); st=d.get('apply_pipeline',{}).get('stages',{}); print('$cfg', '[$s]', round(d['ms_per_step'],3), {k: round(v['ms_per_step'],3) for k,v in st.items()})" || exit 1
   done
 done

@@ -10,6 +10,6 @@ for i in $(seq $reps); do
   for lib in "$@"; do
     if [ "$lib" = cur ]; then unset LAMELLAR_GPU_OPS_LIB; else export LAMELLAR_GPU_OPS_LIB=$PWD/$lib; fi
     env $extra timeout -k 10 200 python bench.py --config $cfg --steps $steps --warmup 5 --no-cpu-baseline 2>/dev/null | grep '^{' | \
-      python -c "import sys,json; d=json.loads(sys.stdin.read()); st=d.get('apply_pipeline',{}).get('stages_ms_per_step',{}); print('$cfg', '$(basename $lib)', round(d['ms_per_step'],3), {k: round(v,3) for k,v in st.items()})" || exit 1
+      python -c "import sys,json; d=json.loads(sys.stdin.read()); st=d.get('apply_pipeline',{}).get('stages',{}); print('$cfg', '$(basename $lib)', round(d['ms_per_step'],3), {k: round(v['ms_per_step'],3) for k,v in st.items()})" || exit 1
   done
 done
