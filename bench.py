@@ -449,9 +449,9 @@ def main():
     # its HIP-event launch time) live in apply_pipeline.stages.
     iw = 8 if npes == 1 else W.arr.index_size()
     per = {}
-    for name, (ms, cnt) in stages.items():
+    for name, (ms, cnt, recs) in stages.items():
         if cnt:
-            per[name] = (ms / cnt, cnt / args.steps)
+            per[name] = (ms / cnt, cnt / args.steps, recs / cnt)
     step_s = ms_per_step * 1e-3
     achieved = W.survey_bpo * W.ops_per_step / step_s
     traffic = None
@@ -461,6 +461,8 @@ def main():
         if all(st in tr for st in per if st not in ("scan",)):
             traffic = sum(tr.get(st, 0.0) * per[st][1] for st in per)
     dom = max(per, key=lambda st: per[st][0] * per[st][1]) if per else None
+    # per stage: records per launch from the library's own count (a stage may run on a
+    # subset of a step's batches, e.g. C5's counted stages)
     roof = {"bound": "hbm", "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
             "frac": achieved / HBM_PEAK, "traffic": traffic,
             "traffic_source": ("HBM bytes per step: committed rocprofv3 FETCH_SIZE/WRITE_SIZE passes "
@@ -469,11 +471,11 @@ def main():
             "scope": "whole step (every kernel of the op path), SURVEY 8(d) bytes per op",
             "bytes_per_op": W.survey_bpo, "ops_per_step": W.ops_per_step, "dominant_kernel": dom}
     stage_rows = {}
-    for st, (avg_ms, lps) in per.items():
-        ops_per_launch = W.ops_per_step / lps
+    for st, (avg_ms, lps, rpl) in per.items():
+        ops_per_launch = rpl if rpl else W.ops_per_step / lps
         bpo = stage_bytes_per_op(st, iw, W.vb, W.eb, ops_per_launch, W.elems, W.fetch)
         row = {"ms_per_step": avg_ms * lps, "launches_per_step": lps, "avg_launch_ms": avg_ms,
-               "bytes_per_op": bpo}
+               "records_per_launch": ops_per_launch, "bytes_per_op": bpo}
         if bpo:
             row["achieved_GBps"] = bpo * ops_per_launch / (avg_ms * 1e-3) / 1e9
             row["frac"] = row["achieved_GBps"] * 1e9 / HBM_PEAK

@@ -62,7 +62,8 @@ SIGNATURES = {
     "lmr_ctx_reserve": (c_int, [c_void_p, c_uint64]),
     "lmr_ctx_error": (c_int, [c_void_p, c_void_p, POINTER(c_uint32), c_int]),
     "lmr_ctx_profile": (c_int, [c_void_p, c_int]),
-    "lmr_ctx_profile_read": (c_int, [c_void_p, c_void_p, POINTER(ctypes.c_double), POINTER(c_uint64), c_int]),
+    "lmr_ctx_profile_read": (c_int, [c_void_p, c_void_p, POINTER(ctypes.c_double), POINTER(c_uint64),
+                                     POINTER(c_uint64), c_int]),
     "lmr_layout_new": (c_int, [POINTER(lmr_layout_t), c_uint64, c_uint32, c_uint32, c_uint32]),
     "lmr_layout_sub": (c_int, [POINTER(lmr_layout_t), c_uint64, c_uint64, POINTER(lmr_layout_t)]),
     "lmr_pe_and_offset": (c_int, [POINTER(lmr_layout_t), c_uint64, POINTER(c_uint64), POINTER(c_uint64)]),

@@ -1063,7 +1063,7 @@ static unsigned grid_for(uint64_t n, unsigned block, unsigned cap) {
 
 hipError_t launch_apply_direct(int dtype, int index_size, const ApplyArgs& a, hipStream_t s) {
     if (a.n == 0) return hipSuccess;
-    ProfScope ps(a.prof, LMR_STAGE_DIRECT, s);
+    ProfScope ps(a.prof, LMR_STAGE_DIRECT, s, a.n);
     return dispatch_dtype(dtype, [&](auto tag) {
         using T = decltype(tag);
         return dispatch_iw(index_size, [&](auto iw) {
@@ -1076,7 +1076,7 @@ hipError_t launch_apply_direct(int dtype, int index_size, const ApplyArgs& a, hi
 
 hipError_t launch_apply_mvsi(int dtype, const ApplyArgs& a, uint64_t index, hipStream_t s) {
     if (a.n == 0) return hipSuccess;
-    ProfScope ps(a.prof, LMR_STAGE_MVSI, s);
+    ProfScope ps(a.prof, LMR_STAGE_MVSI, s, a.n);
     return dispatch_dtype(dtype, [&](auto tag) {
         using T = decltype(tag);
         hipLaunchKernelGGL((k_apply_mvsi<T>), dim3(1), dim3(64), 0, s, a, index);
@@ -1310,7 +1310,8 @@ static hipError_t launch_coarse_free(int index_size, int vb, int frpt, const Par
 }
 
 // exact tile starts from the coarse pass's tile-count rows, then the fine pass
-static hipError_t launch_free_finish(int vb, const PartArgs& q, const TiledWs& w, Prof* prof, hipStream_t s) {
+static hipError_t launch_free_finish(int vb, const PartArgs& q, const TiledWs& w, uint64_t n, Prof* prof,
+                                     hipStream_t s) {
     const uint32_t T = q.num_tiles;
     hipError_t e;
     {
@@ -1319,7 +1320,7 @@ static hipError_t launch_free_finish(int vb, const PartArgs& q, const TiledWs& w
         e = scan_exclusive_u32(w.tile_start, T, w.partials, w.tile_start + T, s);
     }
     if (e != hipSuccess) return e;
-    ProfScope ps(prof, LMR_STAGE_FINE_SCATTER, s);
+    ProfScope ps(prof, LMR_STAGE_FINE_SCATTER, s, n);
     dispatch_vb_rpt<2>(vb, fine_rpt(vb), [&](auto vbt, auto rpt) {
         constexpr int VBc = decltype(vbt)::value, R = decltype(rpt)::value;
         hipLaunchKernelGGL((k_fine_free<VBc, R>), dim3(unsigned(fine_blocks_cap())), dim3(1024), 0, s, q);
@@ -1331,7 +1332,7 @@ static hipError_t launch_free_finish(int vb, const PartArgs& q, const TiledWs& w
 // sweep over the binned records [tile_start[t], tile_start[t + 1]) of every tile
 static hipError_t launch_tile_sweep(int dtype, const ApplyArgs& a, const TiledWs& w, uint32_t T, uint64_t n,
                                     bool scalar, void* res_bin, uint8_t* ok_bin, hipStream_t s) {
-    ProfScope ps(a.prof, LMR_STAGE_TILE_APPLY, s);
+    ProfScope ps(a.prof, LMR_STAGE_TILE_APPLY, s, n);
     const uint64_t avg = (n + T - 1) / T;
     const uint32_t thresh = uint32_t(std::min<uint64_t>(0xFFFFFFFFull, std::max<uint64_t>(4 * avg, 65536)));
     const unsigned pg = (T + 255) / 256;
@@ -1392,10 +1393,10 @@ hipError_t launch_apply_tiled(int dtype, int index_size, const ApplyArgs& a, con
         e = hipMemsetAsync(w.ff, 0, ff_words() * 4, s);
         if (e != hipSuccess) return e;
         {
-            ProfScope ps(a.prof, LMR_STAGE_BIN_SCATTER, s);
+            ProfScope ps(a.prof, LMR_STAGE_BIN_SCATTER, s, a.n);
             e = launch_coarse_free(index_size, vb, frpt, q, s);
         }
-        if (e == hipSuccess) e = launch_free_finish(vb, q, w, a.prof, s);
+        if (e == hipSuccess) e = launch_free_finish(vb, q, w, a.n, a.prof, s);
         if (e == hipSuccess) e = launch_tile_sweep(dtype, a, w, T, a.n, a.val == nullptr, nullptr, nullptr, s);
         return e;
     }
@@ -1415,7 +1416,7 @@ hipError_t launch_apply_tiled(int dtype, int index_size, const ApplyArgs& a, con
     b.err = a.err;
     const size_t hist_lds = size_t(num_tiles) * 4;
     {
-        ProfScope ps(a.prof, LMR_STAGE_BIN_COUNT, s);
+        ProfScope ps(a.prof, LMR_STAGE_BIN_COUNT, s, a.n);
         e = dispatch_iw(index_size, [&](auto iw) {
             hipLaunchKernelGGL((k_bin_count<decltype(iw)::value>), dim3(unsigned(G)), dim3(kBinBlock),
                                hist_lds, s, b);
@@ -1442,7 +1443,7 @@ hipError_t launch_apply_tiled(int dtype, int index_size, const ApplyArgs& a, con
         q.qpos = has_res ? w.qpos : nullptr;
         q.bin_lidx = w.bin_lidx; q.bin_val = w.bin_val; q.rpos = b.rpos;
         {
-            ProfScope ps(a.prof, LMR_STAGE_BIN_SCATTER, s);
+            ProfScope ps(a.prof, LMR_STAGE_BIN_SCATTER, s, a.n);
             const uint64_t ncg = uint64_t(q.C) * G + 1;
             hipLaunchKernelGGL(k_coarse_offsets, dim3(unsigned((ncg + 255) / 256)), dim3(256), 0, s, q);
             e = dispatch_iw(index_size, [&](auto iw) {
@@ -1455,7 +1456,7 @@ hipError_t launch_apply_tiled(int dtype, int index_size, const ApplyArgs& a, con
             });
         }
         if (e != hipSuccess) return e;
-        ProfScope pf(a.prof, LMR_STAGE_FINE_SCATTER, s);
+        ProfScope pf(a.prof, LMR_STAGE_FINE_SCATTER, s, a.n);
         const uint64_t nseg = uint64_t(q.C) * G;
         const unsigned fgrid = unsigned(std::min<uint64_t>(nseg, uint64_t(fine_blocks_cap())));
         dispatch_vb_rpt<2>(vb, fine_rpt(vb), [&](auto vbt, auto rpt) {
@@ -1464,7 +1465,7 @@ hipError_t launch_apply_tiled(int dtype, int index_size, const ApplyArgs& a, con
         });
         e = hipGetLastError();
     } else {
-        ProfScope ps(a.prof, LMR_STAGE_BIN_SCATTER, s);
+        ProfScope ps(a.prof, LMR_STAGE_BIN_SCATTER, s, a.n);
         e = dispatch_iw(index_size, [&](auto iw) {
             constexpr int IW = decltype(iw)::value;
             switch (vb) {
@@ -1484,7 +1485,7 @@ hipError_t launch_apply_tiled(int dtype, int index_size, const ApplyArgs& a, con
                           has_res ? ok_bin : nullptr, s);
     if (e != hipSuccess || !has_res) return e;
     // un-partition: binned -> (temp ->) input order, each a block-contiguous gather
-    ProfScope pu(a.prof, LMR_STAGE_UNPARTITION, s);
+    ProfScope pu(a.prof, LMR_STAGE_UNPARTITION, s, a.n);
     const uint8_t* ok_src = (a.ret == LMR_RET_RESULT) ? ok_bin : nullptr;
     auto gather = [&](const uint32_t* map, const uint32_t* n_dev, const uint8_t* src, uint8_t* dst,
                       const uint8_t* oks, uint8_t* okd) {
@@ -1815,7 +1816,7 @@ static hipError_t stage_region_free(int dtype, int index_size, const ApplyArgs& 
     q.idx = a.idx; q.idx_stride = a.idx_stride; q.val = a.val; q.val_stride = a.val_stride;
     q.val_bits = a.val_bits; q.n = a.n; q.chunk = (a.n + q.G - 1) / q.G;
     {
-        ProfScope ps(a.prof, LMR_STAGE_BIN_SCATTER, st);
+        ProfScope ps(a.prof, LMR_STAGE_BIN_SCATTER, st, a.n);
         e = launch_coarse_free(index_size, vb, frpt, q, st);
     }
     if (e != hipSuccess) return e;
@@ -1829,7 +1830,7 @@ static hipError_t stage_finish_free(const TiledWs& w, StageSession& s, hipStream
     const ApplyArgs& a = s.a;
     const int dtype = s.dtype, vb = dtype_bytes(dtype);
     PartArgs q = free_args(dtype, a, w, kStageFreeBlocks);
-    hipError_t e = launch_free_finish(vb, q, w, a.prof, st);
+    hipError_t e = launch_free_finish(vb, q, w, s.staged, a.prof, st);
     // values are materialised in the bins (regions may mix array and scalar values)
     if (e == hipSuccess) e = launch_tile_sweep(dtype, a, w, q.num_tiles, s.staged, false, nullptr, nullptr, st);
     s.nreg = 0;
@@ -1869,7 +1870,7 @@ hipError_t launch_stage_region(int dtype, int index_size, const ApplyArgs& a, co
     q.err = a.err;
     hipError_t e;
     {
-        ProfScope ps(a.prof, LMR_STAGE_BIN_COUNT, st);
+        ProfScope ps(a.prof, LMR_STAGE_BIN_COUNT, st, a.n);
         e = dispatch_iw(index_size, [&](auto iw) {
             hipLaunchKernelGGL((k_ccount<decltype(iw)::value>), dim3(unsigned(G)), dim3(1024), 0, st, q);
             return hipGetLastError();
@@ -1882,7 +1883,7 @@ hipError_t launch_stage_region(int dtype, int index_size, const ApplyArgs& a, co
     }
     if (e != hipSuccess) return e;
     {
-        ProfScope ps(a.prof, LMR_STAGE_BIN_SCATTER, st);
+        ProfScope ps(a.prof, LMR_STAGE_BIN_SCATTER, st, a.n);
         e = dispatch_iw(index_size, [&](auto iw) {
             constexpr int IW = decltype(iw)::value;
             dispatch_vb_rpt<4>(vb, coarse_rpt(vb), [&](auto vbt, auto rpt) {
@@ -1900,7 +1901,7 @@ hipError_t launch_stage_region(int dtype, int index_size, const ApplyArgs& a, co
     pa.rpos = has_res ? w.rpos + R : nullptr; pa.R = R;
     const uint64_t max_pieces = (a.n + kPiece - 1) / kPiece + C;
     {
-        ProfScope ps(a.prof, LMR_STAGE_FINE_SCATTER, st);
+        ProfScope ps(a.prof, LMR_STAGE_FINE_SCATTER, st, a.n);
         hipLaunchKernelGGL(k_piece_table, dim3(1), dim3(128), 0, st, w.coarse_off, C, uint32_t(G), inb, pbase, bstart);
         e = hipMemsetAsync(w.counts, 0, size_t(max_pieces) * kFine * 4, st);
         if (e != hipSuccess) return e;
@@ -1937,7 +1938,7 @@ hipError_t launch_stage_finish(const TiledWs& w, StageSession& s, hipStream_t st
     uint8_t* ok_bin = reinterpret_cast<uint8_t*>(w.tmp_idx);
     hipError_t e;
     {
-        ProfScope ps(a.prof, LMR_STAGE_TILE_APPLY, st);
+        ProfScope ps(a.prof, LMR_STAGE_TILE_APPLY, st, s.staged);
         const uint64_t avg = (s.staged + T - 1) / T;
         const uint32_t thresh = uint32_t(std::min<uint64_t>(0xFFFFFFFFull, std::max<uint64_t>(4 * avg, 65536)));
         const unsigned pg = unsigned((T + 255) / 256);
@@ -1977,7 +1978,7 @@ hipError_t launch_stage_finish(const TiledWs& w, StageSession& s, hipStream_t st
     }
     if (e == hipSuccess && has_res) {
         // binned -> temp slot (in-bounds slots of each region) -> arrival order
-        ProfScope pu(a.prof, LMR_STAGE_UNPARTITION, st);
+        ProfScope pu(a.prof, LMR_STAGE_UNPARTITION, st, s.staged);
         uint8_t* tmpres = w.bin_val;                              // bins are free after the tile sweep
         uint8_t* ok_tmp = (a.ret == LMR_RET_RESULT) ? reinterpret_cast<uint8_t*>(w.bin_lidx) : nullptr;
         const uint8_t* ok_src = (a.ret == LMR_RET_RESULT) ? ok_bin : nullptr;

@@ -14,11 +14,12 @@ namespace lmr {
 struct Prof {
     std::vector<hipEvent_t> pool;
     size_t next = 0;
-    struct Rec { int stage; hipEvent_t a, b; };
+    struct Rec { int stage; hipEvent_t a, b; uint64_t n; };
     std::vector<Rec> pending;
     hipEvent_t open_ev[LMR_NUM_STAGES] = {};
     double ms[LMR_NUM_STAGES] = {};
     uint64_t cnt[LMR_NUM_STAGES] = {};
+    uint64_t recs[LMR_NUM_STAGES] = {};
     hipEvent_t get() {
         if (next == pool.size()) {
             hipEvent_t e = nullptr;
@@ -33,10 +34,10 @@ void prof_begin(Prof* p, int st, hipStream_t s) {
     if (e && hipEventRecord(e, s) == hipSuccess) p->open_ev[st] = e;
     else p->open_ev[st] = nullptr;
 }
-void prof_end(Prof* p, int st, hipStream_t s) {
+void prof_end(Prof* p, int st, hipStream_t s, uint64_t n) {
     hipEvent_t e = p->get();
     if (e && p->open_ev[st] && hipEventRecord(e, s) == hipSuccess)
-        p->pending.push_back({st, p->open_ev[st], e});
+        p->pending.push_back({st, p->open_ev[st], e, n});
 }
 
 // Staged-apply session of a context (lmr_stage_begin / _soa / _finish).
@@ -349,13 +350,14 @@ lmr_status_t lmr_ctx_profile(lmr_ctx_t* ctx, int enable) {
 }
 
 lmr_status_t lmr_ctx_profile_read(lmr_ctx_t* ctx, lmr_stream_t stream, double* stage_ms,
-                                  uint64_t* stage_launches, int reset) {
+                                  uint64_t* stage_launches, uint64_t* stage_records, int reset) {
     if (!ctx) return LMR_E_INVALID;
     Prof* p = ctx->prof;
     if (!p) {
         for (int i = 0; i < LMR_NUM_STAGES; i++) {
             if (stage_ms) stage_ms[i] = 0;
             if (stage_launches) stage_launches[i] = 0;
+            if (stage_records) stage_records[i] = 0;
         }
         return LMR_OK;
     }
@@ -365,6 +367,7 @@ lmr_status_t lmr_ctx_profile_read(lmr_ctx_t* ctx, lmr_stream_t stream, double* s
         if (hipEventSynchronize(r.b) == hipSuccess && hipEventElapsedTime(&ms, r.a, r.b) == hipSuccess) {
             p->ms[r.stage] += ms;
             p->cnt[r.stage] += 1;
+            p->recs[r.stage] += r.n;
         }
     }
     p->pending.clear();
@@ -372,7 +375,8 @@ lmr_status_t lmr_ctx_profile_read(lmr_ctx_t* ctx, lmr_stream_t stream, double* s
     for (int i = 0; i < LMR_NUM_STAGES; i++) {
         if (stage_ms) stage_ms[i] = p->ms[i];
         if (stage_launches) stage_launches[i] = p->cnt[i];
-        if (reset) { p->ms[i] = 0; p->cnt[i] = 0; }
+        if (stage_records) stage_records[i] = p->recs[i];
+        if (reset) { p->ms[i] = 0; p->cnt[i] = 0; p->recs[i] = 0; }
     }
     return LMR_OK;
 }

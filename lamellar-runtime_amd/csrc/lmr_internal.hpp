@@ -38,13 +38,16 @@ constexpr int kStageInfoWords = 512;      // staged-apply piece table + per-regi
 constexpr uint64_t kStageMaxRegion = uint64_t(1) << 30;   // records per staged region
 
 // ---- stage timing: HIP events around kernel stages (see lmr_ctx_profile) ----
+// n: records the stage processes (reported per stage by lmr_ctx_profile_read)
 void prof_begin(Prof* p, int stage, hipStream_t s);
-void prof_end(Prof* p, int stage, hipStream_t s);
+void prof_end(Prof* p, int stage, hipStream_t s, uint64_t n);
 struct ProfScope {
-    Prof* p; int st; hipStream_t s;
-    ProfScope(Prof* p_, int st_, hipStream_t s_) : p(p_), st(st_), s(s_) { if (p) prof_begin(p, st, s); }
+    Prof* p; int st; hipStream_t s; uint64_t n;
+    ProfScope(Prof* p_, int st_, hipStream_t s_, uint64_t n_ = 0) : p(p_), st(st_), s(s_), n(n_) {
+        if (p) prof_begin(p, st, s);
+    }
     ~ProfScope() { end(); }
-    void end() { if (p) prof_end(p, st, s); p = nullptr; }
+    void end() { if (p) prof_end(p, st, s, n); p = nullptr; }
 };
 
 // Workspace carve-up of one tiled piece.

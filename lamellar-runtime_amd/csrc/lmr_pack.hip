@@ -334,7 +334,7 @@ hipError_t launch_pack(const PackArgs& a, uint32_t* counts, uint32_t* partials, 
     p.iw = a.index_size; p.chunk = (a.n + G - 1) / G; if (p.chunk == 0) p.chunk = 1;
     p.G = uint32_t(G); p.npes = npes; p.counts = counts;
     p.out_idx = a.out_idx; p.out_vals = a.out_vals; p.out_pos = a.out_pos; p.err = a.err;
-    ProfScope ps(a.prof, LMR_STAGE_PACK, s);
+    ProfScope ps(a.prof, LMR_STAGE_PACK, s, a.n);
     const int mode = layout_map_mode(a.layout);
     auto by_mode = [&](auto f) {
         using std::integral_constant;
@@ -392,7 +392,7 @@ hipError_t launch_scatter_results(const uint8_t* in, const uint32_t* pos, uint64
                                   uint32_t elem_bytes, uint8_t* out, const uint8_t* ok_in,
                                   uint8_t* ok_out, Prof* prof, hipStream_t s) {
     if (n == 0) return hipSuccess;
-    ProfScope ps(prof, LMR_STAGE_SCATTER_RESULTS, s);
+    ProfScope ps(prof, LMR_STAGE_SCATTER_RESULTS, s, n);
     uint64_t g = (n + 255) / 256;
     if (g > 8192) g = 8192;
     switch (elem_bytes) {

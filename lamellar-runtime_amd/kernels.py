@@ -95,13 +95,14 @@ class DeviceKernels:
         check(self.lib.lmr_ctx_profile(self.ctx, 1 if enable else 0), "lmr_ctx_profile")
 
     def profile_read(self, reset=True):
-        """{stage: (total_ms, launches)} accumulated since the last reset."""
+        """{stage: (total_ms, launches, records)} accumulated since the last reset."""
         n = len(_capi.STAGES)
         ms = (ctypes.c_double * n)()
         cnt = (c_uint64 * n)()
-        check(self.lib.lmr_ctx_profile_read(self.ctx, self.stream(), ms, cnt, 1 if reset else 0),
+        rec = (c_uint64 * n)()
+        check(self.lib.lmr_ctx_profile_read(self.ctx, self.stream(), ms, cnt, rec, 1 if reset else 0),
               "lmr_ctx_profile_read")
-        return {name: (ms[i], cnt[i]) for i, name in enumerate(_capi.STAGES)}
+        return {name: (ms[i], cnt[i], rec[i]) for i, name in enumerate(_capi.STAGES)}
 
     def synchronize(self):
         torch.cuda.current_stream(self.device).synchronize()

@@ -165,3 +165,131 @@ def test_reference_add_program_c1(world, lam):
     s.batch_add(np.tile(np.arange(s.len(), dtype=np.uint64), 50), 1).block()
     got = a.to_numpy()
     assert np.all(got[n // 4:n // 4 + n // 2] == 100) and np.all(got[:n // 4] == 50) and np.all(got[n // 4 + n // 2:] == 50)
+
+
+# ---------------------------------------------------------------- the remaining payloads
+# tests/payloads.py restates fetch_sub / fetch_mul / fetch_div / rem / fetch_rem /
+# fetch_and / fetch_or / load_store / compare_exchange_epsilon and the OpInput `input`
+# variants once; the CPU oracle runs them over 1-4 simulated PEs
+# (tests/test_oracle_reference_payloads.py), the device runs them here at 1 PE through
+# the op-builder API.
+import payloads as P  # noqa: E402
+import torch  # noqa: E402
+
+from opgen import (ADD, CAS, CAS_EPS, FETCH_ADD, FETCH_AND, FETCH_DIV, FETCH_MUL, FETCH_OR,  # noqa: E402
+                   FETCH_REM, FETCH_SUB, LOAD, REM, STORE)
+
+_METHOD = {ADD: "batch_add", FETCH_ADD: "batch_fetch_add", FETCH_SUB: "batch_fetch_sub",
+           FETCH_MUL: "batch_fetch_mul", FETCH_DIV: "batch_fetch_div", REM: "batch_rem",
+           FETCH_REM: "batch_fetch_rem", FETCH_AND: "batch_fetch_bit_and", FETCH_OR: "batch_fetch_bit_or",
+           STORE: "batch_store"}
+
+
+class _DevArr:
+    def __init__(self, a, dt):
+        self.a, self.dt = a, dt
+
+    def fill(self, v):
+        self.a.fill(v)
+        self.a.wait_all()
+
+    def set(self, vals):
+        t = torch.from_numpy(np.ascontiguousarray(np.asarray(vals).astype(NP[self.dt])).view(np.int64)
+                             if NP[self.dt](0).itemsize == 8 else np.asarray(vals).astype(NP[self.dt]))
+        self.a.local_data().copy_(t.to(self.a.local_data().device).view(self.a.local_data().dtype))
+
+    def _res(self, h):
+        r = h.block()
+        if r is None:
+            return None, None
+        if isinstance(r, torch.Tensor):
+            return r.cpu().numpy().view(NP[self.dt]), None
+        v, ok = r.numpy()
+        return v, ok.astype(np.uint8)
+
+    def op(self, op, idx, vals, current=None, eps=None, pe=0):
+        a = self.a
+        if op == LOAD:
+            return self._res(a.batch_load(idx))
+        if op == CAS:
+            return self._res(a.batch_compare_exchange(idx, current, vals))
+        if op == CAS_EPS:
+            return self._res(a.batch_compare_exchange_epsilon(idx, current, vals, eps))
+        return self._res(getattr(a, _METHOD[op])(idx, vals))
+
+    def op_mvsi(self, op, index, vals, pe=0):
+        return self._res(getattr(self.a, _METHOD[op])(int(index), vals))
+
+    def to_numpy(self):
+        return host(self.a, self.dt)
+
+    def sub_array(self, lo, hi):
+        return _DevArr(self.a.sub_array(lo, hi), self.dt)
+
+    def len(self):
+        return self.a.len()
+
+
+class DevWorld:
+    npes = 1
+
+    def __init__(self, lam, world):
+        self.lam, self.world = lam, world
+
+    def array(self, kind, length, dist, dt):
+        d = self.lam.Distribution.Block if dist == 0 else self.lam.Distribution.Cyclic
+        return _DevArr(new(self.lam, self.world, kind, length, d, dt), dt)
+
+
+@pytest.mark.parametrize("dt", DTS)
+@pytest.mark.parametrize("kind", KINDS)
+def test_reference_fetch_arith_payloads(world, lam, kind, dt):
+    """fetch_sub_test.rs, fetch_mul_test.rs, fetch_div_test.rs, rem_test.rs, fetch_rem_test.rs
+    on the device (known answers as pinned in tests/payloads.py)."""
+    W = DevWorld(lam, world)
+    for dist in (0, 1):
+        for n in LENS:
+            P.fetch_sub_payload(W, kind, dt, n, dist, np.random.default_rng(n))
+            P.fetch_mul_div_payload(W, kind, dt, n, dist)
+            P.rem_payload(W, kind, dt, n, dist)
+
+
+@pytest.mark.parametrize("dt", [d for d in DTS if not d.startswith("f")])
+@pytest.mark.parametrize("kind", KINDS)
+def test_reference_fetch_bitwise_and_load_store_payloads(world, lam, kind, dt):
+    """fetch_and_test.rs, fetch_or_test.rs, load_store_test.rs on the device."""
+    W = DevWorld(lam, world)
+    for dist in (0, 1):
+        for n in LENS:
+            P.fetch_and_or_payload(W, kind, dt, n, dist)
+            P.load_store_payload(W, kind, dt, n, dist)
+
+
+@pytest.mark.parametrize("dt", ["f32", "f64"])
+@pytest.mark.parametrize("kind", ["AtomicArray", "LocalLockArray"])
+def test_reference_compare_exchange_epsilon_payload(world, lam, kind, dt):
+    """compare_exchange_test.rs:235-412 (f32 / f64) and load_store on floats, on the device."""
+    W = DevWorld(lam, world)
+    for dist in (0, 1):
+        for n in LENS:
+            P.cas_epsilon_payload(W, kind, dt, n, dist)
+            P.load_store_payload(W, kind, dt, n, dist)
+
+
+@pytest.mark.parametrize("kind", KINDS)
+def test_reference_input_payloads(world, lam, kind):
+    """The `input` variants (add_test.rs:326-505, fetch_add_test.rs:371-560,
+    compare_exchange_test.rs:448-470) at len 4 / 100 / 2000: every OpInput container --
+    Python ints and numpy scalars per element, a numpy slice, a list, and another array's
+    local data (a device tensor) -- on the device."""
+    W = DevWorld(lam, world)
+    for dist in (0, 1):
+        d = lam.Distribution.Block if dist == 0 else lam.Distribution.Cyclic
+        for n in (4, 100, 2000):
+            inp = lam.UnsafeArray(world.team(), n, d, "usize")
+            inp.local_data().copy_(torch.arange(n, dtype=torch.int64, device=inp.local_data().device))
+            cont = P.index_containers(lambda m, pe, inp=inp: [inp.local_data()])
+            P.add_input_payload(W, kind, n, dist, cont)
+            P.fetch_add_input_payload(W, kind, n, dist, cont)
+            if kind != "UnsafeArray":
+                P.cas_input_payload(W, kind, n, dist)
