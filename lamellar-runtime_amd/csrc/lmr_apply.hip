@@ -599,10 +599,14 @@ __global__ __launch_bounds__(1024) void k_free_tile_totals(const uint32_t* rows,
     }
 }
 
-template <int VB, int RPT>
-__global__ __launch_bounds__(1024) void k_fine_free(PartArgs p) {
+// Rounds are read through buffer descriptors (BufStream): with flat loads the compiler kept
+// one 64-bit pointer per record of the round alive and spilled them. Measured on one box
+// (tools/ab_mix.sh): fine pass 1.558 -> 1.548 ms at 12K rounds; 768-thread blocks with
+// 16 records per thread (168 VGPRs) and 1024 threads with 8 or 10 were all slower.
+template <int VB, int RPT, int NT>
+__global__ __launch_bounds__(NT) void k_fine_free(PartArgs p) {
     using V = typename idx_t<VB>::I;
-    constexpr uint32_t kRound = RPT * 1024;
+    constexpr uint32_t kRound = RPT * NT;
     __shared__ uint32_t hist[kFine], base[kFine], cursor[kFine], tot;
     __shared__ uint32_t s_fill[kMaxCoarse], s_vs[kMaxCoarse], s_total;
     __shared__ uint16_t s_l[kRound];
@@ -620,13 +624,16 @@ __global__ __launch_bounds__(1024) void k_fine_free(PartArgs p) {
     while (c + 1 < C && s_vs[c + 1] <= v_lo) c++;
     uint32_t m_idx[RPT];
     V m_val[RPT];
+    // the round [r0, hi) through buffer descriptors based at r0 (records past hi read 0)
     auto load_round = [&](uint32_t r0, uint32_t hi) {
+        const uint32_t m = hi > r0 ? min(hi - r0, kRound) : 0u;
+        const BufStream bi(p.tmp_idx + r0, m * 4);
+        const BufStream bv(p.tmp_val + uint64_t(r0) * VB, p.tmp_val ? m * VB : 0u);
 #pragma unroll
         for (int j = 0; j < RPT; j++) {
-            const uint32_t k = r0 + uint32_t(j) * 1024 + threadIdx.x;
-            const bool in = k < hi;
-            m_idx[j] = in ? p.tmp_idx[k] : 0xFFFFFFFFu;
-            m_val[j] = (in && p.tmp_val) ? reinterpret_cast<const V*>(p.tmp_val)[k] : V(0);
+            const uint32_t o = uint32_t(j) * NT + threadIdx.x;
+            m_idx[j] = bi.load<uint32_t>(o * 4);
+            m_val[j] = bv.load<V>(o * VB);
         }
     };
     // bucket c's slice of [v_lo, v_hi) as physical temp slots
@@ -653,12 +660,11 @@ __global__ __launch_bounds__(1024) void k_fine_free(PartArgs p) {
         for (uint32_t r0 = lo; r0 < hi; r0 += kRound) {
             for (uint32_t f = threadIdx.x; f < nf; f += blockDim.x) hist[f] = 0;
             __syncthreads();
-            // (tile, validity) are recomputed from m_idx where needed: with 12-record
-            // rounds the kernel sits at the 128-VGPR limit of a 1024-thread block
+            // (tile, validity) are recomputed from m_idx where needed (registers)
             uint32_t m_rank[RPT];
 #pragma unroll
             for (int j = 0; j < RPT; j++)
-                if (r0 + uint32_t(j) * 1024 + threadIdx.x < hi)
+                if (r0 + uint32_t(j) * NT + threadIdx.x < hi)
                     m_rank[j] = atomicAdd(&hist[(m_idx[j] >> p.tile_shift) - t0], 1u);
             __syncthreads();
             small_excl_scan(hist, base, nf, &tot);
@@ -670,14 +676,17 @@ __global__ __launch_bounds__(1024) void k_fine_free(PartArgs p) {
             }
 #pragma unroll
             for (int j = 0; j < RPT; j++) {
-                if (r0 + uint32_t(j) * 1024 + threadIdx.x >= hi) continue;
+                if (r0 + uint32_t(j) * NT + threadIdx.x >= hi) continue;
                 const uint32_t q = base[(m_idx[j] >> p.tile_shift) - t0] + m_rank[j];
                 s_l[q] = uint16_t(m_idx[j] & lmask);
                 s_val[q] = m_val[j];
             }
             if (threadIdx.x < nf) cursor[threadIdx.x] = ts + rsv;
-            if (r0 + kRound < hi) load_round(r0 + kRound, hi);
-            else if (nlo < nhi) load_round(nlo, nhi);
+            {   // one prefetch site (the next round of this bucket, else the next bucket's
+                // first; an empty range reads nothing): one set of registers for the round
+                const bool more = r0 + kRound < hi;
+                load_round(more ? r0 + kRound : nlo, more ? hi : nhi);
+            }
             __syncthreads();
             V* bv = reinterpret_cast<V*>(p.bin_val);
             if (p.tmp_val)
@@ -1323,7 +1332,7 @@ static hipError_t launch_free_finish(int vb, const PartArgs& q, const TiledWs& w
     ProfScope ps(prof, LMR_STAGE_FINE_SCATTER, s, n);
     dispatch_vb_rpt<2>(vb, fine_rpt(vb), [&](auto vbt, auto rpt) {
         constexpr int VBc = decltype(vbt)::value, R = decltype(rpt)::value;
-        hipLaunchKernelGGL((k_fine_free<VBc, R>), dim3(unsigned(fine_blocks_cap())), dim3(1024), 0, s, q);
+        hipLaunchKernelGGL((k_fine_free<VBc, R, 1024>), dim3(unsigned(fine_blocks_cap())), dim3(1024), 0, s, q);
     });
     return hipGetLastError();
 }

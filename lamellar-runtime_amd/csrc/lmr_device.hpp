@@ -501,6 +501,33 @@ __device__ __forceinline__ void bucket_writeout(const uint32_t* hist, const uint
     }
 }
 
+// ---------------------------------------------------------------- buffer loads
+// A block-uniform stream [base, base + bytes) read through a buffer descriptor:
+// 32-bit per-lane offsets instead of 64-bit pointers (the fine passes otherwise
+// keep one hoisted 64-bit pointer per record of a round alive and spill them),
+// and loads past `bytes` return 0. base / bytes must be the same on every lane:
+// they go through readfirstlane so the compiler knows (no waterfall loops).
+struct BufStream {
+    __amdgpu_buffer_rsrc_t r;
+    __device__ __forceinline__ BufStream(const void* base, uint32_t bytes) {
+        const uint64_t b = reinterpret_cast<uint64_t>(base);
+        const uint32_t lo = __builtin_amdgcn_readfirstlane(uint32_t(b));
+        const uint32_t hi = __builtin_amdgcn_readfirstlane(uint32_t(b >> 32));
+        const uint32_t n = __builtin_amdgcn_readfirstlane(bytes);
+        r = __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>((uint64_t(hi) << 32) | lo), 0, n, 0x00020000);
+    }
+    template <typename V>
+    __device__ __forceinline__ V load(uint32_t byte_off) const {
+        if constexpr (sizeof(V) == 1) return V(__builtin_amdgcn_raw_buffer_load_b8(r, byte_off, 0, 0));
+        else if constexpr (sizeof(V) == 2) return V(__builtin_amdgcn_raw_buffer_load_b16(r, byte_off, 0, 0));
+        else if constexpr (sizeof(V) == 4) return V(__builtin_amdgcn_raw_buffer_load_b32(r, byte_off, 0, 0));
+        else {
+            auto x = __builtin_amdgcn_raw_buffer_load_b64(r, byte_off, 0, 0);
+            return __builtin_bit_cast(V, x);
+        }
+    }
+};
+
 // ---------------------------------------------------------------- index load
 template <int IW> struct idx_t;
 template <> struct idx_t<1> { using I = uint8_t; };
