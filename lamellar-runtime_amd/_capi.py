@@ -53,6 +53,29 @@ class lmr_apply_desc_t(Structure):
     ]
 
 
+# lmr_transport_t callbacks (include/lamellar_gpu_ops.h, exchange section)
+ALLTOALL_FN = ctypes.CFUNCTYPE(c_int, c_void_p, c_void_p, c_void_p, c_uint64, c_void_p)
+ALLTOALLV_FN = ctypes.CFUNCTYPE(c_int, c_void_p, c_void_p, POINTER(c_uint64), POINTER(c_uint64), c_void_p,
+                                POINTER(c_uint64), POINTER(c_uint64), c_uint32, c_void_p)
+
+
+class lmr_transport_t(Structure):
+    """The exchange's all-to-all(v) provider: RCCL (lmr_transport_rccl_create) or
+    a caller's callbacks (host_buffers = 1: the library stages through pinned host
+    memory and the callbacks see host pointers)."""
+    _fields_ = [
+        ("num_pes", c_uint32),
+        ("my_pe", c_uint32),
+        ("host_buffers", c_uint32),
+        ("reserved_", c_uint32),
+        ("self", c_void_p),
+        ("alltoall", ALLTOALL_FN),
+        ("alltoallv", ALLTOALLV_FN),
+    ]
+
+
+XHDR_WORDS = 5     # LMR_XHDR_WORDS
+
 # name -> (restype, argtypes). Every symbol of include/lamellar_gpu_ops.h.
 SIGNATURES = {
     "lmr_abi_version": (c_uint32, []),
@@ -97,6 +120,13 @@ SIGNATURES = {
     "lmr_stage_soa": (c_int, [c_void_p, c_void_p, c_uint32, c_void_p, c_void_p, c_uint64, c_void_p,
                               c_void_p, c_void_p]),
     "lmr_stage_finish": (c_int, [c_void_p, c_void_p]),
+    "lmr_rccl_unique_id": (c_int, [c_void_p]),
+    "lmr_transport_rccl_create": (c_int, [c_void_p, c_uint32, c_uint32, c_int, POINTER(c_void_p)]),
+    "lmr_transport_rccl_destroy": (c_int, [c_void_p]),
+    "lmr_batch_exchange": (c_int, [c_void_p, c_void_p, POINTER(lmr_layout_t), POINTER(lmr_apply_desc_t),
+                                   c_void_p, c_uint64, c_uint64, c_void_p, c_void_p, c_uint64, c_void_p,
+                                   c_void_p, c_void_p]),
+    "lmr_exchange_plan": (c_uint64, [c_uint32, c_uint32, c_uint32, c_void_p, c_void_p] + [c_void_p] * 8),
 }
 
 STAGES = ["direct", "mvsi", "bin_count", "scan", "bin_scatter", "tile_apply", "pack",

@@ -47,6 +47,11 @@ struct StageState {
     StageSession s;
 };
 void stage_state_free(StageState* s) { delete s; }
+void stage_abort(StageState* s) {
+    if (!s) return;
+    s->open = false;
+    s->s = StageSession();
+}
 }  // namespace lmr
 
 using namespace lmr;
@@ -298,6 +303,7 @@ lmr_status_t lmr_ctx_destroy(lmr_ctx_t* ctx) {
     (void)hipSetDevice(ctx->device);
     host_stage_free(ctx->host);
     stage_state_free(ctx->stage);
+    xstate_free(ctx->xch);
     if (ctx->ws) (void)hipFree(ctx->ws);
     if (ctx->d_err) (void)hipFree(ctx->d_err);
     if (ctx->prof) {

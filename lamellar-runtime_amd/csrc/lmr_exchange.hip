@@ -1,0 +1,579 @@
+// lmr_exchange.hip — the multi-PE exchange of one batched op behind the C ABI
+// (lmr_batch_exchange), its transports (RCCL over xGMI; host-buffer callbacks),
+// and the host planning it shares with the tests (lmr_exchange_plan).
+//
+// Replaces, for num_pes > 1, the trip of the reference's op AMs over a lamellae:
+// the pack loops put records into per-destination buffers
+// (src/array/unsafe/operations.rs:663-811), each full buffer becomes an AM sent with
+// Shmem::send_to_pes_async (src/lamellae/shmem_lamellae.rs:168-186 ->
+// command_queues.rs:725-807), the owner's recv_data loop (:1395-1531) hands it to
+// exec_am (registered_active_message.rs:443-497), and fetch results come back as
+// AM data (:307-359) into the handle's reorder (operations/handle.rs:315-317).
+// Here, per chunk of the batch:
+//   pack stream : lmr_pack_unordered -> header all-to-all (per PE: count, MVSI local
+//                 index, scalar flag + bits, chunk count) -> [host waits for the
+//                 headers: RCCL's all-to-all-v takes host counts] -> all-to-all-v of
+//                 local indices and values
+//   apply stream: waits for the chunk's exchange, stages every source's records
+//                 (lmr_stage_soa; MVSI sources lmr_apply_mvsi) -> after the last
+//                 chunk one shard sweep (lmr_stage_finish) -> reverse all-to-all-v of
+//                 each chunk's results -> lmr_scatter_results into input order.
+// Chunk j's exchange overlaps chunk j-1's staging on the apply stream; receive
+// buffers are double-buffered between the two streams.
+#include <stdlib.h>
+#include <string.h>
+#include <vector>
+#include <algorithm>
+#include <dlfcn.h>
+#include <mutex>
+#include <rccl/rccl.h>
+#include "../../include/lamellar_gpu_ops.h"
+#include "lmr_internal.hpp"
+#include "lmr_device.hpp"
+
+namespace lmr {
+
+namespace {
+
+struct DevBuf {
+    void* p = nullptr;
+    size_t cap = 0;
+    // grow-only: a larger request waits for the device (the old buffer may be in use)
+    hipError_t need(size_t bytes) {
+        if (bytes <= cap) return hipSuccess;
+        if (p) {
+            hipError_t e = hipDeviceSynchronize();
+            if (e != hipSuccess) return e;
+            (void)hipFree(p);
+            p = nullptr;
+            cap = 0;
+        }
+        size_t c = std::max<size_t>(bytes, 4096);
+        c = c + c / 8;
+        hipError_t e = hipMalloc(&p, c);
+        if (e != hipSuccess) { p = nullptr; return e; }
+        cap = c;
+        return hipSuccess;
+    }
+    void release() { if (p) (void)hipFree(p); p = nullptr; cap = 0; }
+    template <typename T> T* as() const { return reinterpret_cast<T*>(p); }
+};
+
+struct HostBuf {
+    void* p = nullptr;
+    size_t cap = 0;
+    hipError_t need(size_t bytes) {
+        if (bytes <= cap) return hipSuccess;
+        if (p) (void)hipHostFree(p);
+        p = nullptr;
+        cap = 0;
+        size_t c = std::max<size_t>(bytes, 4096);
+        hipError_t e = hipHostMalloc(&p, c, hipHostMallocDefault);
+        if (e != hipSuccess) { p = nullptr; return e; }
+        cap = c;
+        return hipSuccess;
+    }
+    void release() { if (p) (void)hipHostFree(p); p = nullptr; cap = 0; }
+};
+
+}  // namespace
+
+// Exchange state of a context: internal streams, events, grow-only buffers.
+struct XState {
+    hipStream_t sp = nullptr, sa = nullptr;
+    hipEvent_t ev_begin = nullptr, ev_hdr = nullptr, ev_x = nullptr, ev_pack_done = nullptr, ev_apply_done = nullptr;
+    hipEvent_t ev_recv_free[2] = {nullptr, nullptr};
+    bool recv_used[2] = {false, false};
+    DevBuf hdr_send, hdr_recv, counts, offsets, one_idx, send_idx, send_vals;
+    DevBuf recv_idx[2], recv_vals[2];
+    std::vector<DevBuf> pos, res, rok;   // per chunk (returning ops)
+    DevBuf back, back_ok;
+    HostBuf h_hdr;                       // [send rows | recv rows] int64
+    HostBuf h_send, h_recv;              // host-buffer transports
+};
+
+void xstate_free(XState* x) {
+    if (!x) return;
+    (void)hipDeviceSynchronize();
+    for (DevBuf* b : {&x->hdr_send, &x->hdr_recv, &x->counts, &x->offsets, &x->one_idx, &x->send_idx, &x->send_vals,
+                      &x->recv_idx[0], &x->recv_idx[1], &x->recv_vals[0], &x->recv_vals[1], &x->back, &x->back_ok})
+        b->release();
+    for (auto* v : {&x->pos, &x->res, &x->rok})
+        for (DevBuf& b : *v) b.release();
+    x->h_hdr.release();
+    x->h_send.release();
+    x->h_recv.release();
+    for (hipEvent_t e : {x->ev_begin, x->ev_hdr, x->ev_x, x->ev_pack_done, x->ev_apply_done, x->ev_recv_free[0],
+                         x->ev_recv_free[1]})
+        if (e) (void)hipEventDestroy(e);
+    if (x->sp) (void)hipStreamDestroy(x->sp);
+    if (x->sa) (void)hipStreamDestroy(x->sa);
+    delete x;
+}
+
+static hipError_t xstate_init(XState* x) {
+    if (x->sp) return hipSuccess;
+    hipError_t e = hipStreamCreateWithFlags(&x->sp, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&x->sa, hipStreamNonBlocking);
+    for (hipEvent_t* ev : {&x->ev_begin, &x->ev_hdr, &x->ev_x, &x->ev_pack_done, &x->ev_apply_done,
+                           &x->ev_recv_free[0], &x->ev_recv_free[1]})
+        if (e == hipSuccess) e = hipEventCreateWithFlags(ev, hipEventDisableTiming);
+    return e;
+}
+
+// per-PE header rows of one chunk: [count, MVSI local index or -1, scalar flag, scalar bits, chunk count]
+__global__ void k_xhdr(const uint64_t* counts, uint32_t npes, int64_t mvsi_pe, int64_t mvsi_off, int64_t mvsi_n,
+                       int64_t scalar, uint64_t sbits, int64_t my_k, int64_t* hdr) {
+    const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= npes) return;
+    int64_t* r = hdr + uint64_t(p) * LMR_XHDR_WORDS;
+    const bool mv = mvsi_pe >= 0 && int64_t(p) == mvsi_pe;
+    r[0] = mvsi_pe >= 0 ? (mv ? mvsi_n : 0) : (counts ? int64_t(counts[p]) : 0);
+    r[1] = mv ? mvsi_off : -1;
+    r[2] = scalar;
+    r[3] = int64_t(sbits);
+    r[4] = my_k;
+}
+
+}  // namespace lmr
+
+using namespace lmr;
+
+namespace {
+
+inline lmr_status_t hs(hipError_t e) { return e == hipSuccess ? LMR_OK : LMR_E_HIP; }
+
+// Transport calls; host-buffer transports get pinned staging around the callback.
+lmr_status_t tp_alltoall(const lmr_transport_t* tp, XState* x, const void* send, void* recv, uint64_t bytes,
+                         hipStream_t s) {
+    if (!tp->host_buffers) return tp->alltoall(tp->self, send, recv, bytes, reinterpret_cast<lmr_stream_t>(s));
+    const size_t tot = size_t(bytes) * tp->num_pes;
+    if (x->h_send.need(tot) != hipSuccess || x->h_recv.need(tot) != hipSuccess) return LMR_E_HIP;
+    if (hipMemcpyAsync(x->h_send.p, send, tot, hipMemcpyDeviceToHost, s) != hipSuccess ||
+        hipStreamSynchronize(s) != hipSuccess)
+        return LMR_E_HIP;
+    lmr_status_t st = tp->alltoall(tp->self, x->h_send.p, x->h_recv.p, bytes, reinterpret_cast<lmr_stream_t>(s));
+    if (st != LMR_OK) return st;
+    return hs(hipMemcpyAsync(recv, x->h_recv.p, tot, hipMemcpyHostToDevice, s));
+}
+
+lmr_status_t tp_alltoallv(const lmr_transport_t* tp, XState* x, const void* send, const uint64_t* sb,
+                          const uint64_t* so, void* recv, const uint64_t* rb, const uint64_t* ro, uint32_t unit,
+                          hipStream_t s) {
+    if (!tp->host_buffers)
+        return tp->alltoallv(tp->self, send, sb, so, recv, rb, ro, unit, reinterpret_cast<lmr_stream_t>(s));
+    uint64_t st_end = 0, rt_end = 0;
+    for (uint32_t p = 0; p < tp->num_pes; p++) {
+        st_end = std::max(st_end, so[p] + sb[p]);
+        rt_end = std::max(rt_end, ro[p] + rb[p]);
+    }
+    if (x->h_send.need(st_end + 8) != hipSuccess || x->h_recv.need(rt_end + 8) != hipSuccess) return LMR_E_HIP;
+    if (st_end && hipMemcpyAsync(x->h_send.p, send, st_end, hipMemcpyDeviceToHost, s) != hipSuccess) return LMR_E_HIP;
+    if (hipStreamSynchronize(s) != hipSuccess) return LMR_E_HIP;
+    lmr_status_t st = tp->alltoallv(tp->self, x->h_send.p, sb, so, x->h_recv.p, rb, ro, unit,
+                                    reinterpret_cast<lmr_stream_t>(s));
+    if (st != LMR_OK) return st;
+    if (rt_end) return hs(hipMemcpyAsync(recv, x->h_recv.p, rt_end, hipMemcpyHostToDevice, s));
+    return LMR_OK;
+}
+
+// ---- the RCCL transport: grouped ncclSend / ncclRecv on the caller's stream.
+// RCCL is bound at run time: a process that already loaded librccl (torch does) keeps
+// that one copy, so the library and torch.distributed never hold two RCCL runtimes.
+struct RcclApi {
+    decltype(&ncclGetUniqueId) get_unique_id = nullptr;
+    decltype(&ncclCommInitRank) comm_init_rank = nullptr;
+    decltype(&ncclCommDestroy) comm_destroy = nullptr;
+    decltype(&ncclGroupStart) group_start = nullptr;
+    decltype(&ncclGroupEnd) group_end = nullptr;
+    decltype(&ncclSend) send = nullptr;
+    decltype(&ncclRecv) recv = nullptr;
+    bool ok = false;
+};
+
+const RcclApi& rccl() {
+    static RcclApi api;
+    static std::once_flag once;
+    std::call_once(once, [] {
+        void* h = dlopen("librccl.so.1", RTLD_NOW | RTLD_NOLOAD);
+        if (!h) h = dlopen("librccl.so.1", RTLD_NOW);
+        if (!h) h = dlopen("/opt/rocm/lib/librccl.so.1", RTLD_NOW);
+        if (!h) return;
+        api.get_unique_id = reinterpret_cast<decltype(api.get_unique_id)>(dlsym(h, "ncclGetUniqueId"));
+        api.comm_init_rank = reinterpret_cast<decltype(api.comm_init_rank)>(dlsym(h, "ncclCommInitRank"));
+        api.comm_destroy = reinterpret_cast<decltype(api.comm_destroy)>(dlsym(h, "ncclCommDestroy"));
+        api.group_start = reinterpret_cast<decltype(api.group_start)>(dlsym(h, "ncclGroupStart"));
+        api.group_end = reinterpret_cast<decltype(api.group_end)>(dlsym(h, "ncclGroupEnd"));
+        api.send = reinterpret_cast<decltype(api.send)>(dlsym(h, "ncclSend"));
+        api.recv = reinterpret_cast<decltype(api.recv)>(dlsym(h, "ncclRecv"));
+        api.ok = api.get_unique_id && api.comm_init_rank && api.comm_destroy && api.group_start &&
+                 api.group_end && api.send && api.recv;
+    });
+    return api;
+}
+
+struct RcclTransport {
+    lmr_transport_t tp;
+    ncclComm_t comm = nullptr;
+    int device = 0;
+};
+
+ncclDataType_t nccl_type(uint32_t unit) {
+    switch (unit) {
+    case 8: return ncclUint64;
+    case 4: return ncclUint32;
+    default: return ncclUint8;
+    }
+}
+
+lmr_status_t rccl_alltoall(void* self, const void* send, void* recv, uint64_t bytes, lmr_stream_t stream) {
+    RcclTransport* t = static_cast<RcclTransport*>(self);
+    const uint32_t unit = (bytes % 8 == 0) ? 8 : (bytes % 4 == 0 ? 4 : 1);
+    const size_t cnt = size_t(bytes / unit);
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    const RcclApi& R = rccl();
+    if (R.group_start() != ncclSuccess) return LMR_E_HIP;
+    for (uint32_t p = 0; p < t->tp.num_pes; p++) {
+        R.send(static_cast<const uint8_t*>(send) + uint64_t(p) * bytes, cnt, nccl_type(unit), int(p), t->comm, s);
+        R.recv(static_cast<uint8_t*>(recv) + uint64_t(p) * bytes, cnt, nccl_type(unit), int(p), t->comm, s);
+    }
+    return R.group_end() == ncclSuccess ? LMR_OK : LMR_E_HIP;
+}
+
+lmr_status_t rccl_alltoallv(void* self, const void* send, const uint64_t* sb, const uint64_t* so, void* recv,
+                            const uint64_t* rb, const uint64_t* ro, uint32_t unit, lmr_stream_t stream) {
+    RcclTransport* t = static_cast<RcclTransport*>(self);
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    const ncclDataType_t ty = nccl_type(unit == 2 ? 1 : unit);
+    const uint32_t u = (unit == 8 || unit == 4) ? unit : 1;
+    const RcclApi& R = rccl();
+    if (R.group_start() != ncclSuccess) return LMR_E_HIP;
+    for (uint32_t p = 0; p < t->tp.num_pes; p++) {
+        if (sb[p]) R.send(static_cast<const uint8_t*>(send) + so[p], size_t(sb[p] / u), ty, int(p), t->comm, s);
+        if (rb[p]) R.recv(static_cast<uint8_t*>(recv) + ro[p], size_t(rb[p] / u), ty, int(p), t->comm, s);
+    }
+    return R.group_end() == ncclSuccess ? LMR_OK : LMR_E_HIP;
+}
+
+bool valid_layout(const lmr_layout_t* L) {
+    return L && L->num_pes > 0 && L->my_pe < L->num_pes && L->distribution <= 1 && L->orig_elem_per_pe > 0;
+}
+
+uint64_t exchange_chunk() {
+    const char* e = getenv("LAMELLAR_EXCHANGE_CHUNK");
+    uint64_t c = (e && *e) ? strtoull(e, nullptr, 10) : (uint64_t(1) << 26);
+    if (c < 1) c = 1;
+    if (c > (uint64_t(1) << 27)) c = uint64_t(1) << 27;
+    return c;
+}
+
+// elements of one all-to-all-v element unit that divide every split of a buffer of
+// `w`-byte items (splits are item multiples)
+uint32_t unit_for(uint32_t w) { return (w % 8 == 0) ? 8 : (w % 4 == 0 ? 4 : 1); }
+
+}  // namespace
+
+extern "C" {
+
+uint64_t lmr_exchange_plan(uint32_t npes, uint32_t iw, uint32_t eb, const int64_t* sh, const int64_t* rh,
+                           uint64_t* idx_sb, uint64_t* idx_so, uint64_t* idx_rb, uint64_t* idx_ro,
+                           uint64_t* val_sb, uint64_t* val_so, uint64_t* val_rb, uint64_t* val_ro) {
+    uint64_t k = 0, a = 0, b = 0, c = 0, d = 0;
+    for (uint32_t p = 0; p < npes; p++) {
+        const int64_t* s = sh + uint64_t(p) * LMR_XHDR_WORDS;
+        const int64_t* r = rh + uint64_t(p) * LMR_XHDR_WORDS;
+        const uint64_t sc = uint64_t(s[0] > 0 ? s[0] : 0), rc = uint64_t(r[0] > 0 ? r[0] : 0);
+        idx_sb[p] = s[1] < 0 ? sc * iw : 0;            // MVSI senders name their index in the header
+        idx_rb[p] = r[1] < 0 ? rc * iw : 0;
+        val_sb[p] = s[2] ? 0 : sc * eb;                // one scalar value travels in the header
+        val_rb[p] = r[2] ? 0 : rc * eb;
+        idx_so[p] = a; a += idx_sb[p];
+        idx_ro[p] = b; b += idx_rb[p];
+        val_so[p] = c; c += val_sb[p];
+        val_ro[p] = d; d += val_rb[p];
+        if (r[4] > 0 && uint64_t(r[4]) > k) k = uint64_t(r[4]);
+    }
+    return k;
+}
+
+lmr_status_t lmr_rccl_unique_id(uint8_t id[128]) {
+    if (!id) return LMR_E_INVALID;
+    if (!rccl().ok) return LMR_E_UNSUPPORTED;
+    ncclUniqueId u;
+    if (rccl().get_unique_id(&u) != ncclSuccess) return LMR_E_HIP;
+    static_assert(sizeof(u) == 128, "ncclUniqueId is 128 bytes");
+    memcpy(id, &u, 128);
+    return LMR_OK;
+}
+
+lmr_status_t lmr_transport_rccl_create(const uint8_t id[128], uint32_t num_pes, uint32_t my_pe, int device,
+                                       lmr_transport_t** out) {
+    if (!id || !out || num_pes == 0 || my_pe >= num_pes) return LMR_E_INVALID;
+    *out = nullptr;
+    if (!rccl().ok) return LMR_E_UNSUPPORTED;
+    if (hipSetDevice(device) != hipSuccess) return LMR_E_HIP;
+    RcclTransport* t = new RcclTransport();
+    ncclUniqueId u;
+    memcpy(&u, id, 128);
+    if (rccl().comm_init_rank(&t->comm, int(num_pes), u, int(my_pe)) != ncclSuccess) {
+        delete t;
+        return LMR_E_HIP;
+    }
+    t->device = device;
+    t->tp.num_pes = num_pes;
+    t->tp.my_pe = my_pe;
+    t->tp.host_buffers = 0;
+    t->tp.self = t;
+    t->tp.alltoall = rccl_alltoall;
+    t->tp.alltoallv = rccl_alltoallv;
+    *out = &t->tp;
+    return LMR_OK;
+}
+
+lmr_status_t lmr_transport_rccl_destroy(lmr_transport_t* tp) {
+    if (!tp || tp->alltoall != rccl_alltoall) return LMR_E_INVALID;
+    RcclTransport* t = static_cast<RcclTransport*>(tp->self);
+    (void)hipSetDevice(t->device);
+    (void)hipDeviceSynchronize();
+    if (t->comm) rccl().comm_destroy(t->comm);
+    delete t;
+    return LMR_OK;
+}
+
+lmr_status_t lmr_batch_exchange(lmr_ctx_t* ctx, const lmr_transport_t* tp, const lmr_layout_t* layout,
+                                const lmr_apply_desc_t* desc, const uint64_t* d_gidx, uint64_t h_index,
+                                uint64_t i_len, const void* d_vals, const void* h_val, uint64_t v_len,
+                                void* d_results, uint8_t* d_ok, lmr_stream_t stream) {
+    if (!ctx || !tp || !valid_layout(layout) || !desc || tp->num_pes != layout->num_pes ||
+        tp->my_pe != layout->my_pe || layout->num_pes > uint32_t(kMaxPackPes))
+        return LMR_E_INVALID;
+    if (desc->dtype >= LMR_NUM_DTYPES || desc->op >= LMR_NUM_OPS) return LMR_E_INVALID;
+    if (!lmr_op_supported(desc->kind, desc->dtype, desc->op)) return LMR_E_UNSUPPORTED;
+    if (i_len > 1 && v_len > 1 && i_len != v_len) return LMR_E_LENGTH;
+    if ((i_len > 1 && !d_gidx) || (v_len > 1 && !d_vals) || (v_len == 1 && !h_val)) return LMR_E_INVALID;
+    const uint32_t npes = layout->num_pes;
+    const uint32_t eb = uint32_t(dtype_bytes(int(desc->dtype)));
+    const uint32_t iw = lmr_index_size(layout);
+    const uint32_t rk = lmr_op_ret_kind(desc->op);
+    // every PE of a returning op sends results back, even one whose own batch is empty
+    const bool returning = rk != LMR_RET_NONE;
+    const bool want_ok = rk == LMR_RET_RESULT;
+    const uint64_t n = (i_len == 0 || v_len == 0) ? 0 : std::max(i_len, v_len);
+    if (n > 0 && ((returning && !d_results) || (want_ok && !d_ok))) return LMR_E_INVALID;
+    const bool mvsi = i_len == 1 && v_len > 1;
+    const bool scalar = v_len == 1 && !mvsi;
+    uint64_t sbits = 0;
+    if (scalar) memcpy(&sbits, h_val, eb);
+    (void)hipSetDevice(ctx->device);
+    if (!ctx->xch) ctx->xch = new XState();
+    XState* x = ctx->xch;
+    if (xstate_init(x) != hipSuccess) return LMR_E_HIP;
+    hipStream_t s0 = reinterpret_cast<hipStream_t>(stream);
+    // --- shape on the sender side
+    int64_t mvsi_pe = -1, mvsi_off = 0;
+    const uint64_t* gidx = d_gidx;
+    const uint64_t m = mvsi ? 0 : n;                   // records that go through the pack
+    if (mvsi) {
+        uint64_t pe = 0, off = 0;
+        if (!lmr_pe_and_offset(layout, h_index, &pe, &off)) return LMR_E_OOB;   // unsafe/operations.rs:611-613
+        mvsi_pe = int64_t(pe);
+        mvsi_off = int64_t(off);
+    } else if (n > 0 && i_len == 1) {                  // one index (1 x 1): a one-record batch
+        if (x->one_idx.need(8) != hipSuccess) return LMR_E_HIP;
+        if (hipMemcpyAsync(x->one_idx.p, &h_index, 8, hipMemcpyHostToDevice, s0) != hipSuccess) return LMR_E_HIP;
+        gidx = x->one_idx.as<uint64_t>();
+    }
+    const uint64_t chunk = exchange_chunk();
+    const uint64_t my_k = mvsi ? 1 : std::max<uint64_t>(1, (m + chunk - 1) / chunk);
+    // --- buffers that do not depend on the chunk
+    if (x->hdr_send.need(size_t(npes) * LMR_XHDR_WORDS * 8) != hipSuccess ||
+        x->hdr_recv.need(size_t(npes) * LMR_XHDR_WORDS * 8) != hipSuccess ||
+        x->counts.need(size_t(npes) * 8) != hipSuccess || x->offsets.need(size_t(npes + 1) * 8) != hipSuccess ||
+        x->h_hdr.need(size_t(2 * npes) * LMR_XHDR_WORDS * 8) != hipSuccess)
+        return LMR_E_HIP;
+    const uint64_t cmax = std::min<uint64_t>(m, chunk);
+    if (x->send_idx.need(cmax * iw + 8) != hipSuccess || x->send_vals.need(cmax * eb + 8) != hipSuccess)
+        return LMR_E_HIP;
+    // --- both internal streams start after everything already on the caller's stream
+    if (hipEventRecord(x->ev_begin, s0) != hipSuccess || hipStreamWaitEvent(x->sp, x->ev_begin, 0) != hipSuccess ||
+        hipStreamWaitEvent(x->sa, x->ev_begin, 0) != hipSuccess)
+        return LMR_E_HIP;
+    x->recv_used[0] = x->recv_used[1] = false;
+    lmr_status_t st = lmr_stage_begin(ctx, desc);
+    if (st != LMR_OK) return st;
+    // a failed exchange closes the session (its staged records are dropped) so the
+    // context stays usable; the device work already enqueued drains first
+    struct SessionGuard {
+        lmr_ctx_t* c;
+        bool armed = true;
+        ~SessionGuard() {
+            if (!armed) return;
+            (void)hipDeviceSynchronize();
+            stage_abort(c->stage);
+        }
+    } guard{ctx};
+    struct ChunkRec {
+        std::vector<uint64_t> send_cnt, recv_cnt;
+        uint64_t lo, hi, total;
+    };
+    std::vector<ChunkRec> chunks;
+    std::vector<uint64_t> isb(npes), iso(npes), irb(npes), iro(npes), vsb(npes), vso(npes), vrb(npes), vro(npes);
+    const int64_t* h_send = static_cast<const int64_t*>(x->h_hdr.p);
+    const int64_t* h_recv = h_send + size_t(npes) * LMR_XHDR_WORDS;
+    uint64_t nchunks = my_k;
+    for (uint64_t j = 0; j < nchunks; j++) {
+        const uint64_t lo = std::min(m, j * chunk), hi = std::min(m, (j + 1) * chunk);
+        const uint64_t cnt = hi - lo;
+        if (returning && x->pos.size() <= j) x->pos.resize(j + 1);
+        // ---- pack this chunk by destination PE (pack stream)
+        const bool packed = !mvsi && j < my_k && cnt > 0;
+        if (packed) {
+            if (returning && x->pos[j].need(cnt * 4 + 8) != hipSuccess) return LMR_E_HIP;
+            st = lmr_pack_unordered(ctx, layout, gidx + lo, cnt, scalar ? nullptr : static_cast<const uint8_t*>(d_vals) + lo * eb,
+                                    desc->dtype, iw, x->send_idx.p, scalar ? nullptr : x->send_vals.p,
+                                    returning ? x->pos[j].as<uint32_t>() : nullptr, x->counts.as<uint64_t>(),
+                                    x->offsets.as<uint64_t>(), reinterpret_cast<lmr_stream_t>(x->sp));
+            if (st != LMR_OK) return st;
+        }
+        hipLaunchKernelGGL(k_xhdr, dim3((npes + 255) / 256), dim3(256), 0, x->sp, packed ? x->counts.as<uint64_t>() : nullptr,
+                           npes, mvsi && j == 0 ? mvsi_pe : -1, mvsi_off, int64_t(n), int64_t(scalar ? 1 : 0), sbits,
+                           int64_t(my_k), x->hdr_send.as<int64_t>());
+        if (hipGetLastError() != hipSuccess) return LMR_E_HIP;
+        st = tp_alltoall(tp, x, x->hdr_send.p, x->hdr_recv.p, LMR_XHDR_WORDS * 8, x->sp);
+        if (st != LMR_OK) return st;
+        // the host needs this chunk's counts (one wait per chunk): sent rows, then received rows
+        if (hipMemcpyAsync(x->h_hdr.p, x->hdr_send.p, size_t(npes) * LMR_XHDR_WORDS * 8, hipMemcpyDeviceToHost,
+                           x->sp) != hipSuccess)
+            return LMR_E_HIP;
+        if (hipMemcpyAsync(static_cast<int64_t*>(x->h_hdr.p) + size_t(npes) * LMR_XHDR_WORDS, x->hdr_recv.p,
+                           size_t(npes) * LMR_XHDR_WORDS * 8, hipMemcpyDeviceToHost, x->sp) != hipSuccess ||
+            hipEventRecord(x->ev_hdr, x->sp) != hipSuccess || hipEventSynchronize(x->ev_hdr) != hipSuccess)
+            return LMR_E_HIP;
+        const uint64_t k = lmr_exchange_plan(npes, iw, eb, h_send, h_recv, isb.data(), iso.data(), irb.data(),
+                                             iro.data(), vsb.data(), vso.data(), vrb.data(), vro.data());
+        if (j == 0) nchunks = std::max<uint64_t>(k, 1);
+        ChunkRec cr;
+        cr.lo = mvsi ? 0 : lo;
+        cr.hi = mvsi ? n : hi;
+        cr.send_cnt.resize(npes);
+        cr.recv_cnt.resize(npes);
+        cr.total = 0;
+        for (uint32_t p = 0; p < npes; p++) {
+            cr.send_cnt[p] = uint64_t(std::max<int64_t>(h_send[p * LMR_XHDR_WORDS], 0));
+            cr.recv_cnt[p] = uint64_t(std::max<int64_t>(h_recv[p * LMR_XHDR_WORDS], 0));
+            cr.total += cr.recv_cnt[p];
+        }
+        // ---- receive buffers of this chunk (double-buffered against the apply stream)
+        const int b = int(j & 1);
+        if (x->recv_used[b] && hipStreamWaitEvent(x->sp, x->ev_recv_free[b], 0) != hipSuccess) return LMR_E_HIP;
+        const uint64_t ib = iro[npes - 1] + irb[npes - 1], vb = vro[npes - 1] + vrb[npes - 1];
+        if (x->recv_idx[b].cap < ib + 8 || x->recv_vals[b].cap < vb + 8) {
+            // growing frees the old buffer: nothing may still use it
+            if (hipStreamSynchronize(x->sa) != hipSuccess) return LMR_E_HIP;
+            if (x->recv_idx[b].need(ib + 8) != hipSuccess || x->recv_vals[b].need(vb + 8) != hipSuccess)
+                return LMR_E_HIP;
+        }
+        const uint8_t* send_vals = mvsi ? static_cast<const uint8_t*>(d_vals) : x->send_vals.as<uint8_t>();
+        st = tp_alltoallv(tp, x, x->send_idx.p, isb.data(), iso.data(), x->recv_idx[b].p, irb.data(), iro.data(),
+                          unit_for(iw), x->sp);
+        if (st == LMR_OK)
+            st = tp_alltoallv(tp, x, send_vals, vsb.data(), vso.data(), x->recv_vals[b].p, vrb.data(), vro.data(),
+                              unit_for(eb), x->sp);
+        if (st != LMR_OK) return st;
+        if (hipEventRecord(x->ev_x, x->sp) != hipSuccess || hipStreamWaitEvent(x->sa, x->ev_x, 0) != hipSuccess)
+            return LMR_E_HIP;
+        // ---- owner side: stage every source's records (apply stream)
+        if (returning) {
+            if (x->res.size() <= j) { x->res.resize(j + 1); x->rok.resize(j + 1); }
+            if (x->res[j].need(cr.total * eb + 8) != hipSuccess) return LMR_E_HIP;
+            if (want_ok && x->rok[j].need(cr.total + 8) != hipSuccess) return LMR_E_HIP;
+        }
+        uint64_t io = 0, vo = 0, ro = 0;
+        lmr_stream_t sa = reinterpret_cast<lmr_stream_t>(x->sa);
+        for (uint32_t p = 0; p < npes;) {
+            const int64_t* r = h_recv + uint64_t(p) * LMR_XHDR_WORDS;
+            const uint64_t c = cr.recv_cnt[p];
+            if (c == 0) { p++; continue; }
+            void* res = returning ? x->res[j].as<uint8_t>() + ro * eb : nullptr;
+            uint8_t* okp = want_ok ? x->rok[j].as<uint8_t>() + ro : nullptr;
+            if (r[1] >= 0) {                            // MVSI: one atomic block at its index
+                lmr_apply_desc_t d = *desc;
+                st = lmr_apply_mvsi(ctx, &d, x->recv_vals[b].as<uint8_t>() + vo, c, uint64_t(r[1]), res, okp, sa);
+                if (st != LMR_OK) return st;
+                vo += c * eb;
+                ro += c;
+                p++;
+                continue;
+            }
+            // consecutive sources with the same value form go in one stream
+            const int64_t sc = r[2], bits = r[3];
+            uint32_t e = p;
+            uint64_t tot = 0;
+            while (e < npes) {
+                const int64_t* q = h_recv + uint64_t(e) * LMR_XHDR_WORDS;
+                if (cr.recv_cnt[e] == 0) { e++; continue; }
+                if (q[1] >= 0 || q[2] != sc || (sc && q[3] != bits)) break;
+                tot += cr.recv_cnt[e];
+                e++;
+            }
+            const uint64_t ubits = uint64_t(bits);
+            st = lmr_stage_soa(ctx, x->recv_idx[b].as<uint8_t>() + io, iw, sc ? nullptr : x->recv_vals[b].as<uint8_t>() + vo,
+                               sc ? &ubits : nullptr, tot, res, okp, sa);
+            if (st != LMR_OK) return st;
+            io += tot * iw;
+            if (!sc) vo += tot * eb;
+            ro += tot;
+            p = e;
+        }
+        if (hipEventRecord(x->ev_recv_free[b], x->sa) != hipSuccess) return LMR_E_HIP;
+        x->recv_used[b] = true;
+        chunks.push_back(std::move(cr));
+    }
+    // ---- one shard sweep, then results back to their senders
+    st = lmr_stage_finish(ctx, reinterpret_cast<lmr_stream_t>(x->sa));
+    if (st != LMR_OK) return st;
+    guard.armed = false;
+    if (returning) {
+        std::vector<uint64_t> sb(npes), so(npes), rb(npes), ro(npes), osb(npes), oso(npes), orb(npes), oro(npes);
+        for (uint64_t j = 0; j < chunks.size(); j++) {
+            const ChunkRec& cr = chunks[j];
+            uint64_t a = 0, bb = 0, nsent = 0;
+            for (uint32_t p = 0; p < npes; p++) {
+                sb[p] = cr.recv_cnt[p] * eb; so[p] = a; a += sb[p];
+                rb[p] = cr.send_cnt[p] * eb; ro[p] = bb; bb += rb[p];
+                osb[p] = cr.recv_cnt[p]; oso[p] = so[p] / eb;
+                orb[p] = cr.send_cnt[p]; oro[p] = ro[p] / eb;
+                nsent += cr.send_cnt[p];
+            }
+            if (x->back.cap < nsent * eb + 8 || (want_ok && x->back_ok.cap < nsent + 8)) {
+                if (hipStreamSynchronize(x->sa) != hipSuccess) return LMR_E_HIP;
+                if (x->back.need(nsent * eb + 8) != hipSuccess || (want_ok && x->back_ok.need(nsent + 8) != hipSuccess))
+                    return LMR_E_HIP;
+            }
+            st = tp_alltoallv(tp, x, x->res[j].p, sb.data(), so.data(), x->back.p, rb.data(), ro.data(), unit_for(eb),
+                              x->sa);
+            if (st == LMR_OK && want_ok)
+                st = tp_alltoallv(tp, x, x->rok[j].p, osb.data(), oso.data(), x->back_ok.p, orb.data(), oro.data(), 1,
+                                  x->sa);
+            if (st != LMR_OK) return st;
+            if (nsent == 0) continue;
+            if (mvsi) {                                 // results come back in value order
+                if (hipMemcpyAsync(d_results, x->back.p, nsent * eb, hipMemcpyDeviceToDevice, x->sa) != hipSuccess ||
+                    (want_ok && hipMemcpyAsync(d_ok, x->back_ok.p, nsent, hipMemcpyDeviceToDevice, x->sa) != hipSuccess))
+                    return LMR_E_HIP;
+            } else {
+                st = lmr_scatter_results(x->back.p, x->pos[j].as<uint32_t>(), nsent, eb,
+                                         static_cast<uint8_t*>(d_results) + cr.lo * eb, want_ok ? x->back_ok.as<uint8_t>() : nullptr,
+                                         want_ok ? d_ok + cr.lo : nullptr, reinterpret_cast<lmr_stream_t>(x->sa));
+                if (st != LMR_OK) return st;
+            }
+        }
+    }
+    // ---- the caller's stream continues after both internal streams
+    if (hipEventRecord(x->ev_pack_done, x->sp) != hipSuccess || hipEventRecord(x->ev_apply_done, x->sa) != hipSuccess ||
+        hipStreamWaitEvent(s0, x->ev_pack_done, 0) != hipSuccess || hipStreamWaitEvent(s0, x->ev_apply_done, 0) != hipSuccess)
+        return LMR_E_HIP;
+    return LMR_OK;
+}
+
+}  // extern "C"

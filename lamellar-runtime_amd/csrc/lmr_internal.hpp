@@ -9,7 +9,8 @@
 namespace lmr { struct Prof; }
 
 namespace lmr { struct HostStage; void host_stage_free(HostStage* h); }
-namespace lmr { struct StageState; void stage_state_free(StageState* s); }
+namespace lmr { struct StageState; void stage_state_free(StageState* s); void stage_abort(StageState* s); }
+namespace lmr { struct XState; void xstate_free(XState* x); }
 
 struct lmr_ctx {
     int device = 0;
@@ -22,6 +23,7 @@ struct lmr_ctx {
     lmr::Prof* prof = nullptr;     // stage timing (lmr_ctx_profile), null when off
     lmr::HostStage* host = nullptr;  // host-buffer ingestion staging (lmr_apply_mvmi_host), lazily made
     lmr::StageState* stage = nullptr;  // staged-apply session (lmr_stage_*), lazily made
+    lmr::XState* xch = nullptr;        // multi-PE exchange state (lmr_batch_exchange), lazily made
 };
 
 namespace lmr {

@@ -8,22 +8,17 @@ so the records go straight to the apply kernel: at one PE a global index *is*
 the local offset (Block, Cyclic and sub-arrays alike), bounds-checked on the
 device.
 
-N PEs (one per GPU): a collective step replaces the shmem lamellae:
-  lmr_pack_unordered (device, grouped by destination PE, IndexSize-narrowed offsets)
-  -> header all-to-all (per destination: count, MVSI index, scalar value)
-  -> all-to-all-v of indices and values (RCCL over xGMI)
-  -> apply of every received segment (device)
-  -> [fetch / result ops] reverse all-to-all-v of results + lmr_scatter_results
-     back into input order (operations/handle.rs:315-317).
-The step is cut into chunks and software-pipelined over a pack stream, the
-RCCL stream and an apply stream (_distributed).
+N PEs (one per GPU): one collective C-ABI call, lmr_batch_exchange, replaces
+the shmem lamellae (pack by owner PE -> header all-to-all -> all-to-all-v of
+indices and values over RCCL/xGMI -> staged apply at the owner -> reverse
+all-to-all-v of results -> scatter into input order,
+operations/handle.rs:315-317), chunked and pipelined inside the library.
 Every PE must issue the same sequence of batch calls (a PE with nothing to
 send passes an empty batch): the exchange is collective where the reference's
 AMs are one-sided.
 """
 from __future__ import annotations
 
-import contextlib
 import numbers
 import os
 
@@ -126,20 +121,16 @@ def run_batch(arr, op, index, val, current=None, eps=None) -> BatchResult:
     eps_bits = dt.to_bits(eps) if eps is not None else 0
     i_scalar, idx, i_len = index_input(k, index)
     v_scalar, vals, v_len = value_input(k, dt, val)
-    if i_len == 0 or v_len == 0:                        # "no vals no indices" :345-347
-        return BatchResult(k.empty(0, dt.torch) if ret else None,
-                           k.empty(0, torch.uint8) if ret == BatchReturnType.Result else None, dt, ret)
     if i_len > 1 and v_len > 1 and i_len != v_len:
         raise LamellarError(LmrStatus.LENGTH, f"{i_len} indices vs {v_len} values")
-    n = max(i_len, v_len)
+    n = 0 if (i_len == 0 or v_len == 0) else max(i_len, v_len)   # "no vals no indices" :345-347
     results = k.empty(n, dt.torch) if ret != BatchReturnType.None_ else None
     ok = k.empty(n, torch.uint8) if ret == BatchReturnType.Result else None
-    mvsi = (i_len == 1 and v_len > 1)
-    if team.num_pes() == 1 and not _FORCE_EXCHANGE:
-        _local(arr, k, dt, op, i_scalar, idx, v_scalar, vals, n, mvsi, results, ok, cmp_bits, eps_bits)
-    else:
-        _distributed(arr, k, dt, op, ret, i_scalar, idx, v_scalar, vals, n, mvsi, results, ok,
-                     cmp_bits, eps_bits)
+    if team.num_pes() > 1 or _FORCE_EXCHANGE:
+        _distributed(arr, k, dt, op, i_scalar, idx, i_len, v_scalar, vals, v_len, results, ok, cmp_bits, eps_bits)
+    elif n:
+        _local(arr, k, dt, op, i_scalar, idx, v_scalar, vals, n, i_len == 1 and v_len > 1, results, ok,
+               cmp_bits, eps_bits)
     return BatchResult(results, ok, dt, ret)
 
 
@@ -166,214 +157,19 @@ def _local(arr, k, dt, op, i_scalar, idx, v_scalar, vals, n, mvsi, results, ok, 
                 vals if v_scalar else 0, n, results, ok, cmp_bits, eps_bits)
 
 
-def _exchange_chunk() -> int:
-    """Records per exchange chunk (LAMELLAR_EXCHANGE_CHUNK, default 2^26), at most
-    2^27 so one chunk's value bytes stay below 2^31 per peer."""
-    return min(1 << 27, max(1, int(os.environ.get("LAMELLAR_EXCHANGE_CHUNK", str(1 << 26)))))
+def _distributed(arr, k, dt, op, i_scalar, idx, i_len, v_scalar, vals, v_len, results, ok, cmp_bits, eps_bits):
+    """One collective lmr_batch_exchange: pack by owner PE ->
+    header all-to-all -> all-to-all-v of indices and values -> the owner stages
+    every arriving stream and applies them in one shard sweep -> reverse
+    all-to-all-v of results -> scatter into input order, chunked and pipelined
+    inside the library (include/lamellar_gpu_ops.h, exchange section).
 
-
-class _Streams:
-    """Pack/exchange and apply streams of one batch on a device (no-ops on CPU)."""
-
-    def __init__(self, k):
-        self.dev = getattr(k, "is_device", True) and k.device.type == "cuda"
-        if self.dev:
-            self.main = torch.cuda.current_stream(k.device)
-            self.pack = torch.cuda.Stream(k.device)
-            self.apply = torch.cuda.Stream(k.device)
-            self.pack.wait_stream(self.main)
-            self.apply.wait_stream(self.main)
-
-    def on(self, which):
-        if not self.dev:
-            return contextlib.nullcontext()
-        return torch.cuda.stream(getattr(self, which))
-
-    def used_on(self, which, *tensors):
-        """Tell the caching allocator that `tensors` are read/written on stream `which`."""
-        if self.dev:
-            st = getattr(self, which)
-            for t in tensors:
-                if t is not None and t.is_cuda:
-                    t.record_stream(st)
-
-    def join(self):
-        if self.dev:
-            self.main.wait_stream(self.pack)
-            self.main.wait_stream(self.apply)
-
-
-def _distributed(arr, k, dt, op, ret, i_scalar, idx, v_scalar, vals, n, mvsi, results, ok,
-                 cmp_bits, eps_bits):
-    """Chunked, software-pipelined exchange.
-
-    The batch is cut into chunks of LAMELLAR_EXCHANGE_CHUNK records. Per chunk j:
-    pack (pack stream) -> header all-to-all (counts, MVSI index, scalar value)
-    -> async all-to-all-v of indices and values (RCCL stream) -> the apply
-    stream waits for the exchange and applies every source's records in one
-    call. Chunk j's exchange overlaps chunk j+1's pack and chunk j-1's apply;
-    returned values of chunk j travel back (async) after chunk j+1's exchange
-    has been issued, then lmr_scatter_results puts them in input order.
-
-    Owner side: every chunk's received records are partitioned into shard tiles
-    on arrival (lmr_stage_soa) and all chunks are applied in one sweep of the
-    shard after the last one (lmr_stage_finish), so the shard is read and
-    written once per batch, not once per chunk. Returned values of every chunk
-    travel back after that sweep.
-
-    Collective: every PE issues the same sequence. PEs agree on the chunk count
-    through the first header (column 4 = the sender's chunk count); a PE past
-    its own last chunk sends empty chunks.
-    """
+    Collective: every PE issues the same sequence of batch calls; a PE with an
+    empty batch still takes part (others may send it records)."""
     team = arr.team
-    npes = team.num_pes()
-    iw = arr.index_size()
-    eb = dt.bytes
-    returning = ret != BatchReturnType.None_
-    st = _Streams(k)
-    chunk = _exchange_chunk()
-    if mvsi:
-        my_k = 1
-        mvsi_pe, mvsi_off = _host_map(arr, idx)
-    else:
-        if i_scalar:
-            idx = torch.tensor([idx], dtype=torch.int64, device=k.device)
-        m = int(idx.numel())
-        my_k = max(1, -(-m // chunk))
-    sbits = (vals & 0xFFFFFFFFFFFFFFFF) if (v_scalar and not mvsi) else 0
-    shard, slen = arr.local_shard(), arr.num_elems_local()
-    empty_u8 = k.empty(0, torch.uint8)
-    # the owner expects about as many records as it sends (uniform streams); more
-    # than the workspace holds only costs an extra shard sweep
-    with st.on("apply"):
-        k.stage_begin(shard, slen, arr.kind, dt, op, cmp_bits, eps_bits,
-                      expect=0 if mvsi else (m + m // 8 + (1 << 16)))
-
-    def pack_chunk(j):
-        """-> (send_idx, send_vals, pos, counts (device or host), lo, hi)"""
-        if mvsi:
-            if j > 0:
-                return empty_u8, empty_u8, None, torch.zeros(npes, dtype=torch.int64), 0, 0
-            c = torch.zeros(npes, dtype=torch.int64)
-            c[mvsi_pe] = n
-            sv = vals.view(torch.uint8) if vals.dtype != torch.uint8 else vals
-            return empty_u8, sv, None, c, 0, n
-        lo, hi = min(m, j * chunk), min(m, (j + 1) * chunk)
-        with st.on("pack"):
-            si, sv, pos, counts = k.pack(arr.layout, idx[lo:hi], hi - lo,
-                                         None if v_scalar else vals[lo:hi], dt, iw,
-                                         stable=False, want_pos=returning)
-        return si, (sv if sv is not None else empty_u8), pos, counts, lo, hi
-
-    def send_back(p):
-        """Reverse exchange of a chunk's returned values + scatter into input order."""
-        r_res, r_ok, recv_counts, send_counts, pos, lo, hi = p
-        with st.on("apply"):
-            back, wb = team.alltoallv_async(r_res, [c * eb for c in recv_counts],
-                                            [c * eb for c in send_counts], eb)
-            back_ok, wo = (team.alltoallv_async(r_ok, recv_counts, send_counts)
-                           if r_ok is not None else (None, None))
-            wb.wait()
-            if wo is not None:
-                wo.wait()
-            st.used_on("apply", back, back_ok, pos)
-            nsent = int(sum(send_counts))
-            if mvsi:
-                results.view(torch.uint8)[:nsent * eb].copy_(back[:nsent * eb])
-                if ok is not None:
-                    ok[:nsent].copy_(back_ok[:nsent])
-            elif nsent:
-                k.scatter_results(back, pos, nsent, eb, results[lo:hi], back_ok,
-                                  ok[lo:hi] if ok is not None else None)
-
-    nchunks = my_k
-    nxt = pack_chunk(0)
-    pending = []
-    j = 0
-    while j < nchunks:
-        send_idx, send_vals, pos, counts, lo, hi = nxt
-        with st.on("pack"):
-            send_counts = counts.cpu() if counts.is_cuda else counts      # waits for this pack only
-        header = torch.zeros(npes, 5, dtype=torch.int64)
-        header[:, 0] = send_counts
-        header[:, 1] = -1
-        if mvsi and j == 0:
-            header[mvsi_pe, 1] = mvsi_off
-        if v_scalar and not mvsi:
-            header[:, 2] = 1
-            header[:, 3] = torch.tensor(np.array([sbits], dtype=np.uint64).view(np.int64))
-        header[:, 4] = my_k
-        with st.on("pack"):
-            rh = team.alltoall_header(header)
-        if j == 0:
-            nchunks = int(rh[:, 4].max())
-        send_counts = header[:, 0].tolist()
-        recv_counts = rh[:, 0].tolist()
-        idx_ss = [c * iw if header[p, 1] < 0 else 0 for p, c in enumerate(send_counts)]
-        idx_rs = [c * iw if rh[p, 1] < 0 else 0 for p, c in enumerate(recv_counts)]
-        val_ss = [0 if header[p, 2] else c * eb for p, c in enumerate(send_counts)]
-        val_rs = [0 if rh[p, 2] else c * eb for p, c in enumerate(recv_counts)]
-        with st.on("pack"):
-            r_idx, w_i = team.alltoallv_async(send_idx, idx_ss, idx_rs, iw)
-            r_vals, w_v = team.alltoallv_async(send_vals, val_ss, val_rs, eb)
-        # next chunk's pack runs while this chunk is on the wire
-        nxt = pack_chunk(j + 1) if j + 1 < nchunks else None
-        total = int(sum(recv_counts))
-        with st.on("apply"):
-            w_i.wait()
-            w_v.wait()
-            st.used_on("apply", r_idx, r_vals)
-            r_res = k.empty(total * eb, torch.uint8) if returning else None
-            r_ok = k.empty(total, torch.uint8) if ret == BatchReturnType.Result else None
-            _apply_received(k, arr, dt, op, shard, slen, rh, recv_counts, iw, eb, r_idx, r_vals,
-                            r_res, r_ok, cmp_bits, eps_bits)
-        if returning:
-            pending.append((r_res, r_ok, recv_counts, send_counts, pos, lo, hi))
-        j += 1
-    with st.on("apply"):
-        k.stage_finish()
-    for p in pending:
-        send_back(p)
-    st.join()
-
-
-def _apply_received(k, arr, dt, op, shard, slen, rh, recv_counts, iw, eb, r_idx, r_vals, r_res, r_ok,
-                    cmp_bits, eps_bits):
-    """Stage one chunk's received records into the open session: consecutive
-    sources with the same value form (array values / the same scalar) go in one
-    call; MVSI sources are applied at once, one by one (their block is applied
-    as one atomic unit)."""
-    npes = len(recv_counts)
-    io = vo = ro = 0
-    s = 0
-    while s < npes:
-        c = int(recv_counts[s])
-        if c == 0:
-            s += 1
-            continue
-        if rh[s, 1] >= 0:
-            k.apply_mvsi(shard, slen, arr.kind, dt, op, r_vals[vo:vo + c * eb], c, int(rh[s, 1]),
-                         r_res[ro * eb:(ro + c) * eb] if r_res is not None else None,
-                         r_ok[ro:ro + c] if r_ok is not None else None, cmp_bits, eps_bits)
-            vo += c * eb
-            ro += c
-            s += 1
-            continue
-        scalar, bits = int(rh[s, 2]), int(rh[s, 3])
-        e, cnt = s, 0
-        while e < npes and (int(recv_counts[e]) == 0 or
-                            (rh[e, 1] < 0 and int(rh[e, 2]) == scalar and (not scalar or int(rh[e, 3]) == bits))):
-            cnt += int(recv_counts[e])
-            e += 1
-        seg_idx = r_idx[io:io + cnt * iw]
-        seg_res = r_res[ro * eb:(ro + cnt) * eb] if r_res is not None else None
-        seg_ok = r_ok[ro:ro + cnt] if r_ok is not None else None
-        if scalar:
-            ubits = int(np.array([bits], dtype=np.int64).view(np.uint64)[0])
-            k.stage_soa(seg_idx, iw, None, ubits, cnt, seg_res, seg_ok)
-        else:
-            k.stage_soa(seg_idx, iw, r_vals[vo:vo + cnt * eb], 0, cnt, seg_res, seg_ok)
-            vo += cnt * eb
-        io += cnt * iw
-        ro += cnt
-        s = e
+    m = 0 if (i_len == 0 or v_len == 0) else max(i_len, v_len)
+    expect = 0 if (i_scalar and v_len > 1) else m + m // 8 + (1 << 16)   # about what this PE sends
+    k.batch_exchange(team.transport(), arr.layout, arr.local_shard(), arr.num_elems_local(), arr.kind, dt, op,
+                     None if i_scalar else idx, idx if i_scalar else 0, i_len,
+                     None if v_scalar else vals, vals if v_scalar else 0, v_len,
+                     results, ok, cmp_bits, eps_bits, expect=expect)

@@ -229,6 +229,23 @@ class DeviceKernels:
         h = out.cpu()
         return bool(h[1].item() & 0xFF), int(h[0].item()) & 0xFFFFFFFFFFFFFFFF
 
+    def batch_exchange(self, transport, layout, shard, shard_len, kind, dt, op, gidx, h_index, i_len, vals,
+                       h_val_bits, v_len, results=None, ok=None, cmp_bits=0, eps_bits=0, expect=0):
+        """lmr_batch_exchange: one batched op over every PE (collective). gidx: i_len
+        global indices (device) unless i_len == 1 (h_index); vals: v_len elements
+        (device) unless v_len == 1 (h_val_bits). `expect`: records this PE will likely
+        receive; the workspace grows to hold them before the call."""
+        if expect:
+            self._maybe_reserve(int(expect))
+        d = self._desc(shard, shard_len, kind, dt, op, cmp_bits, eps_bits)
+        hv = c_uint64(int(h_val_bits) & 0xFFFFFFFFFFFFFFFF)
+        st = self.lib.lmr_batch_exchange(self.ctx, transport.ptr, byref(layout), byref(d), _p(gidx),
+                                         int(h_index) & 0xFFFFFFFFFFFFFFFF, int(i_len), _p(vals),
+                                         ctypes.cast(byref(hv), c_void_p), int(v_len), _p(results), _p(ok),
+                                         self.stream())
+        transport.raise_pending()
+        check(st, "lmr_batch_exchange")
+
     def scatter_results(self, res_in, pos, n, eb, res_out, ok_in=None, ok_out=None):
         st = self.lib.lmr_scatter_results(_p(res_in), _p(pos), int(n), int(eb), _p(res_out),
                                           _p(ok_in), _p(ok_out), self.stream())

@@ -13,6 +13,7 @@ LAMELLAR_NUM_PES, lamellar_run.sh:31-40).
 """
 from __future__ import annotations
 
+import ctypes
 import os
 
 import torch
@@ -29,31 +30,111 @@ def _env_int(*names, default=None):
 
 _WIDE = {8: torch.int64, 4: torch.int32, 2: torch.int16, 1: torch.uint8}
 _MAX_SPLIT = (1 << 31) - 1
+_LMR_E_HIP = 6
+
+
+def _host_view(addr, nbytes):
+    """uint8 tensor over nbytes of host memory at addr (no copy)."""
+    if nbytes == 0:
+        return torch.empty(0, dtype=torch.uint8)
+    return torch.frombuffer((ctypes.c_uint8 * nbytes).from_address(addr), dtype=torch.uint8)
+
+
+class HostTransport:
+    """lmr_transport_t whose collectives run on a host (gloo) process group.
+
+    host_buffers = 1: lmr_batch_exchange stages device data through pinned host
+    memory around each callback, so the callbacks see host pointers. Used where
+    the process group cannot carry device memory (LAMELLAR_COMM_BACKEND=gloo,
+    CPU rehearsals). A callback that raises returns LMR_E_HIP to the library and
+    the exception is re-raised by `raise_pending` after the C call returns."""
+
+    def __init__(self, num_pes, my_pe, group):
+        from . import _capi
+        self.num_pes, self.my_pe, self.group = num_pes, my_pe, group
+        self.error = None
+        self._a2a = _capi.ALLTOALL_FN(self._alltoall)       # keep the thunks alive
+        self._a2av = _capi.ALLTOALLV_FN(self._alltoallv)
+        self.t = _capi.lmr_transport_t(num_pes, my_pe, 1, 0, None, self._a2a, self._a2av)
+
+    @property
+    def ptr(self):
+        return ctypes.c_void_p(ctypes.addressof(self.t))
+
+    def raise_pending(self):
+        if self.error is not None:
+            e, self.error = self.error, None
+            raise e
+
+    def _alltoall(self, _self, send, recv, nbytes, _stream):
+        try:
+            tot = int(nbytes) * self.num_pes
+            s, r = _host_view(send, tot), _host_view(recv, tot)
+            if tot:
+                dist.all_to_all_single(r, s, group=self.group)
+            return 0
+        except Exception as e:  # noqa: BLE001 - handed back to the caller of the C entry point
+            self.error = e
+            return _LMR_E_HIP
+
+    def _alltoallv(self, _self, send, sb, so, recv, rb, ro, unit, _stream):
+        try:
+            n = self.num_pes
+            sb, so, rb, ro = ([int(a[p]) for p in range(n)] for a in (sb, so, rb, ro))
+            # the library's splits are back to back (offsets are prefix sums)
+            if any(so[p] != sum(sb[:p]) for p in range(n)) or any(ro[p] != sum(rb[:p]) for p in range(n)):
+                raise ValueError("alltoallv splits are not contiguous")
+            s, r = _host_view(send, sum(sb)), _host_view(recv, sum(rb))
+            sw, rw, ss, rs = _widen(s, r, sb, rb, int(unit))
+            dist.all_to_all_single(rw, sw, output_split_sizes=rs, input_split_sizes=ss, group=self.group)
+            return 0
+        except Exception as e:  # noqa: BLE001
+            self.error = e
+            return _LMR_E_HIP
+
+
+class RcclTransport:
+    """lmr_transport_rccl_create: RCCL grouped send/recv over xGMI on the library's
+    streams. PE 0 makes the unique id and the process group broadcasts it."""
+
+    def __init__(self, num_pes, my_pe, device, group):
+        from . import _capi
+        from .kernels import check
+        lib = _capi.lib()
+        uid = (ctypes.c_uint8 * 128)()
+        if my_pe == 0:
+            check(lib.lmr_rccl_unique_id(uid), "lmr_rccl_unique_id")
+        obj = [bytes(uid)]
+        dist.broadcast_object_list(obj, src=0, group=group)
+        uid = (ctypes.c_uint8 * 128).from_buffer_copy(obj[0])
+        self.ptr = ctypes.c_void_p()
+        check(lib.lmr_transport_rccl_create(uid, num_pes, my_pe, device.index or 0, ctypes.byref(self.ptr)),
+              "lmr_transport_rccl_create")
+
+    def raise_pending(self):
+        pass
+
+    def close(self):
+        from . import _capi
+        if self.ptr:
+            _capi.lib().lmr_transport_rccl_destroy(self.ptr)
+            self.ptr = ctypes.c_void_p()
 
 
 def _widen(send, recv, send_splits, recv_splits, unit):
-    """View 1-D uint8 buffers as `unit`-byte integers (unit 4 or 8: the record
-    field width, the same on every PE, so all ranks agree on the element type)
-    so per-peer element counts stay below 2^31 (RCCL/NCCL all-to-all-v counts
-    are signed 32-bit); split sizes converted to elements."""
+    """View 1-D uint8 buffers as `unit`-byte integers (the record field width,
+    the same on every PE, so all ranks agree on the element type) so per-peer
+    element counts stay below 2^31 (all-to-all-v counts are signed 32-bit);
+    split sizes converted to elements."""
     ss = [int(x) for x in send_splits]
     rs = [int(x) for x in recv_splits]
-    if unit in (4, 8) and send.dtype == torch.uint8 and recv.dtype == torch.uint8:
-        if send.storage_offset() % unit:
-            send = send.clone()
+    if unit in (4, 8):                 # gloo has no 16-bit integer type; 2-byte splits stay bytes
         send, recv = send.view(_WIDE[unit]), recv.view(_WIDE[unit])
         ss, rs = [x // unit for x in ss], [x // unit for x in rs]
     if max(ss + rs + [0]) > _MAX_SPLIT:
         raise ValueError("exchange split of %d elements exceeds 2^31 - 1; lower LAMELLAR_EXCHANGE_CHUNK"
                          % max(ss + rs))
     return send, recv, ss, rs
-
-
-class _Done:
-    """Work handle of an exchange that has already completed."""
-
-    def wait(self):
-        return True
 
 
 class LamellarTeam:
@@ -63,8 +144,7 @@ class LamellarTeam:
         self.device = device
         self.kernels = kernels
         self.group = group
-        self.comm_device = device if (dist.is_initialized() and dist.get_backend(group) == "nccl") \
-            else torch.device("cpu")
+        self._transport = None
 
     def num_pes(self):
         return self._num_pes
@@ -80,47 +160,17 @@ class LamellarTeam:
                 dist.barrier(group=self.group)
 
     # ---- exchange step (collective) ----
-    def alltoall_header(self, send: torch.Tensor) -> torch.Tensor:
-        """send: int64 [num_pes, k] (row p goes to PE p) -> recv int64 [num_pes, k]."""
-        if not self._collective():
-            return send.clone()
-        s = send.to(self.comm_device).contiguous()
-        r = torch.empty_like(s)
-        dist.all_to_all_single(r, s, group=self.group)
-        return r.cpu()
-
-    def alltoallv(self, send: torch.Tensor, send_splits, recv_splits, unit=1) -> torch.Tensor:
-        """Byte / element all-to-all-v of a 1-D tensor with per-PE split sizes."""
-        total = int(sum(recv_splits))
-        if not self._collective():
-            return send[:total].clone()
-        dev = send.device
-        s = send.to(self.comm_device).contiguous()
-        r = torch.empty(total, dtype=send.dtype, device=self.comm_device)
-        sw, rw, ss, rs = _widen(s, r, send_splits, recv_splits, unit)
-        dist.all_to_all_single(rw, sw, output_split_sizes=rs, input_split_sizes=ss, group=self.group)
-        return r.to(dev)
-
-    def alltoallv_async(self, send: torch.Tensor, send_splits, recv_splits, unit=1):
-        """Asynchronous alltoallv -> (recv tensor, work). work.wait() orders the
-        caller's current stream after the transfer (RCCL) or blocks until it is
-        done (gloo). The recv tensor lives on the comm device."""
-        total = int(sum(recv_splits))
-        if not self._collective():
-            return send[:total].clone(), _Done()
-        if send.device != self.comm_device:
-            # host-side backend (gloo) with device tensors: synchronous round trip
-            return self.alltoallv(send, send_splits, recv_splits, unit), _Done()
-        r = torch.empty(total, dtype=send.dtype, device=self.comm_device)
-        sw, rw, ss, rs = _widen(send.contiguous(), r, send_splits, recv_splits, unit)
-        w = dist.all_to_all_single(rw, sw, output_split_sizes=rs, input_split_sizes=ss, group=self.group,
-                                   async_op=True)
-        return r, w
-
-    def _collective(self):
-        # a 1-PE world still goes through the collective when a process group
-        # exists (LAMELLAR_FORCE_EXCHANGE rehearsal of the RCCL calls)
-        return self._num_pes > 1 or (dist.is_available() and dist.is_initialized())
+    def transport(self):
+        """The lmr_transport_t of lmr_batch_exchange (made on first use, collective):
+        RCCL when the process group is "nccl", host callbacks over the group otherwise."""
+        if self._transport is None:
+            if self.group is None:
+                raise RuntimeError("the exchange needs a process group (num_pes > 1 or LAMELLAR_FORCE_EXCHANGE=1)")
+            if dist.get_backend(self.group) == "nccl":
+                self._transport = RcclTransport(self._num_pes, self._my_pe, self.device, self.group)
+            else:
+                self._transport = HostTransport(self._num_pes, self._my_pe, self.group)
+        return self._transport
 
     def all_gather_object(self, obj):
         if self._num_pes == 1:

@@ -1,10 +1,15 @@
-"""N > 1 exchange orchestration rehearsed on CPU: world_size 2, gloo backend.
+"""N > 1 on CPU: world_size 2, gloo backend.
 
-The product exchange (engine._distributed: lmr_pack -> header all-to-all ->
-all-to-all-v of indices/values -> apply -> reverse all-to-all-v -> result
-scatter) runs unchanged; only the device kernels are replaced by the small
-CPU test double below (no GPU here). Results are checked against the oracle
-simulating both PEs.
+The product exchange is one C-ABI call (lmr_batch_exchange, device code). Here,
+without a GPU, the parts of it that are host code run for real:
+* the host-buffer transport (world.HostTransport) called through the
+  lmr_transport_t function pointers exactly as the library calls them, over a
+  2-rank gloo group, with ragged splits and every element unit;
+* lmr_exchange_plan, the library's per-chunk host planning;
+* the array API over 2 PEs (team transport selection, reductions, to_numpy)
+  with a CPU test double of DeviceKernels whose batch_exchange is a one-chunk
+  restatement of lmr_batch_exchange built on those two. Results are checked
+  against the oracle simulating both PEs.
 """
 import ctypes
 import os
@@ -123,6 +128,99 @@ class CpuTestKernels:
         idx = torch.from_numpy(np.full(n, index, dtype=np.uint64).view(np.uint8))
         self.apply_soa(shard, shard_len, kind, dt, op, idx, 8, vals, 0, n, results, ok, cmp_bits, eps_bits)
 
+    def batch_exchange(self, transport, layout, shard, shard_len, kind, dt, op, gidx, h_index, i_len, vals,
+                       h_val_bits, v_len, results=None, ok=None, cmp_bits=0, eps_bits=0, expect=0):
+        """One-chunk restatement of lmr_batch_exchange over the real transport
+        callbacks and the real lmr_exchange_plan."""
+        lib = self.capi.lib()
+        npes = layout.num_pes
+        iw, eb = lib.lmr_index_size(ctypes.byref(layout)), dt.bytes
+        n = 0 if (i_len == 0 or v_len == 0) else max(i_len, v_len)
+        mvsi, scalar = i_len == 1 and v_len > 1, v_len == 1 and not (i_len == 1 and v_len > 1)
+        t = transport.t
+        hdr = np.zeros((npes, 5), np.int64)
+        hdr[:, 1], hdr[:, 4] = -1, 1
+        pos = None
+        if mvsi:
+            pe, off = ctypes.c_uint64(), ctypes.c_uint64()
+            assert lib.lmr_pe_and_offset(ctypes.byref(layout), int(h_index), ctypes.byref(pe), ctypes.byref(off))
+            hdr[pe.value, 0], hdr[pe.value, 1] = n, off.value
+            s_idx, s_vals = np.zeros(8, np.uint8), vals.numpy().view(np.uint8).copy()
+        else:
+            g = gidx if i_len != 1 else torch.tensor([int(h_index)], dtype=torch.int64)
+            si, sv, pos, counts = self.pack(layout, g, n, None if scalar else vals, dt, iw)
+            hdr[:, 0] = counts.numpy()
+            s_idx = np.concatenate([si.numpy(), np.zeros(8, np.uint8)])
+            s_vals = np.concatenate([sv.numpy() if sv is not None else np.zeros(0, np.uint8), np.zeros(8, np.uint8)])
+        if scalar:
+            hdr[:, 2], hdr[:, 3] = 1, np.array([h_val_bits], np.uint64).view(np.int64)[0]
+        rh = np.zeros_like(hdr)
+        assert t.alltoall(t.self, hdr.ctypes.data, rh.ctypes.data, 40, None) == 0
+        plan = [np.zeros(npes, np.uint64) for _ in range(8)]
+        assert lib.lmr_exchange_plan(npes, iw, eb, hdr.ctypes.data, rh.ctypes.data, *[a.ctypes.data for a in plan]) == 1
+        isb, iso, irb, iro, vsb, vso, vrb, vro = plan
+        u64p = lambda a: a.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64))
+        r_idx = np.zeros(int(irb.sum()) + 8, np.uint8)
+        r_vals = np.zeros(int(vrb.sum()) + 8, np.uint8)
+        st = t.alltoallv(t.self, s_idx.ctypes.data, u64p(isb), u64p(iso), r_idx.ctypes.data, u64p(irb), u64p(iro),
+                         iw, None)
+        transport.raise_pending()
+        assert st == 0
+        assert t.alltoallv(t.self, s_vals.ctypes.data, u64p(vsb), u64p(vso), r_vals.ctypes.data, u64p(vrb),
+                           u64p(vro), eb, None) == 0
+        rcnt = np.maximum(rh[:, 0], 0)
+        tot = int(rcnt.sum())
+        r_res = torch.zeros(tot * eb, dtype=torch.uint8)
+        r_ok = torch.zeros(tot, dtype=torch.uint8)
+        io = vo = ro = 0
+        for p in range(npes):
+            c = int(rcnt[p])
+            if c == 0:
+                continue
+            res_seg, ok_seg = r_res[ro * eb:(ro + c) * eb], r_ok[ro:ro + c]
+            if rh[p, 1] >= 0:
+                self.apply_mvsi(shard, shard_len, kind, dt, op, torch.from_numpy(r_vals[vo:vo + c * eb].copy()), c,
+                                int(rh[p, 1]), res_seg, ok_seg, cmp_bits, eps_bits)
+                vo += c * eb
+            else:
+                ii = torch.from_numpy(r_idx[io:io + c * iw].copy())
+                if rh[p, 2]:
+                    self.apply_soa(shard, shard_len, kind, dt, op, ii, iw, None,
+                                   int(np.array([rh[p, 3]], np.int64).view(np.uint64)[0]), c, res_seg, ok_seg,
+                                   cmp_bits, eps_bits)
+                else:
+                    self.apply_soa(shard, shard_len, kind, dt, op, ii, iw,
+                                   torch.from_numpy(r_vals[vo:vo + c * eb].copy()), 0, c, res_seg, ok_seg,
+                                   cmp_bits, eps_bits)
+                    vo += c * eb
+                io += c * iw
+            ro += c
+        if results is None and not self.capi.lib().lmr_op_ret_kind(op):
+            return
+        scnt = np.maximum(hdr[:, 0], 0).astype(np.uint64)
+        sb, rb = rcnt.astype(np.uint64) * np.uint64(eb), scnt * np.uint64(eb)
+        so, ro_ = np.concatenate([[0], np.cumsum(sb)[:-1]]).astype(np.uint64), \
+            np.concatenate([[0], np.cumsum(rb)[:-1]]).astype(np.uint64)
+        back = np.zeros(int(rb.sum()) + 8, np.uint8)
+        src = np.concatenate([r_res.numpy(), np.zeros(8, np.uint8)])
+        assert t.alltoallv(t.self, src.ctypes.data, u64p(sb), u64p(so), back.ctypes.data, u64p(rb), u64p(ro_),
+                           eb, None) == 0
+        okb = np.zeros(int(scnt.sum()) + 8, np.uint8)
+        oks = np.concatenate([r_ok.numpy(), np.zeros(8, np.uint8)])
+        sbo, rbo = rcnt.astype(np.uint64), scnt
+        assert t.alltoallv(t.self, oks.ctypes.data, u64p(sbo), u64p(so // np.uint64(eb)), okb.ctypes.data,
+                           u64p(rbo), u64p(ro_ // np.uint64(eb)), 1, None) == 0
+        if n == 0 or results is None:
+            return
+        nb = torch.from_numpy(back[:n * eb].copy())
+        nok = torch.from_numpy(okb[:n].copy())
+        if mvsi:
+            results.view(torch.uint8)[:n * eb] = nb
+            if ok is not None:
+                ok[:n] = nok
+        else:
+            self.scatter_results(nb, pos, n, eb, results, nok if ok is not None else None, ok)
+
     def reduce(self, data, n, dt, op):
         a = data.numpy().view(dt.np)[:n]
         if n == 0:
@@ -149,13 +247,11 @@ class CpuTestKernels:
             ok_out.numpy()[p] = ok_in.numpy()[:n]
 
 
-def _worker(rank, ws, port, outdir, dist_kind, chunk=None, ragged=False):
+def _worker(rank, ws, port, outdir, dist_kind, ragged=False):
     sys.path.insert(0, ROOT)
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
                       WORLD_SIZE=str(ws), LOCAL_RANK=str(rank))
-    if chunk:
-        os.environ["LAMELLAR_EXCHANGE_CHUNK"] = str(chunk)
     from _lamellar_bootstrap import load_package
     lam = load_package()
     from test_dist_gloo import CpuTestKernels
@@ -192,9 +288,14 @@ def _worker(rank, ws, port, outdir, dist_kind, chunk=None, ragged=False):
             arr.batch_add(np.array([1, 2, 3], dtype=np.uint64), np.array([100, 200, 300], dtype=np.uint64)).block()
         world.barrier()
         res["after_mixed"] = arr.to_numpy()
+        # a fetch op where PE 1's batch is empty: it still takes part in the exchange
+        ei = np.array([9, 10, 11], dtype=np.uint64) if me == 0 else np.zeros(0, np.uint64)
+        eo = arr.batch_fetch_add(ei, 2).block()
+        world.barrier()
+        res["empty_olds"], res["after_empty"] = eo.numpy().view(np.uint64), arr.to_numpy()
     # compare_exchange on PE-owned indices: all succeed
     ci = np.arange(me, n_len, ws, dtype=np.uint64)
-    cur = res["after_mvsi"][ci]
+    cur = arr.to_numpy()[ci]
     r = arr.batch_compare_exchange(ci, 0, 1).block()  # current 0: only zero elements succeed
     vals, ok = r.numpy()
     res["cas_idx"], res["cas_vals"], res["cas_ok"], res["cas_cur"] = ci, vals, ok, cur
@@ -206,17 +307,15 @@ def _worker(rank, ws, port, outdir, dist_kind, chunk=None, ragged=False):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("dist_kind,chunk,ragged", [(0, None, False), (1, None, False), (0, 700, True),
-                                                     (1, 256, True)],
-                         ids=["Block", "Cyclic", "Block-chunked-ragged", "Cyclic-chunked-ragged"])
-def test_two_pe_exchange_gloo(orc, dist_kind, chunk, ragged):
-    """chunk: LAMELLAR_EXCHANGE_CHUNK (several pipelined chunks per batch); ragged:
-    PEs with different batch lengths (different chunk counts) and a call where one
-    PE passes an MVSI shape and the other an MVMI one."""
+@pytest.mark.parametrize("dist_kind,ragged", [(0, False), (1, False), (0, True), (1, True)],
+                         ids=["Block", "Cyclic", "Block-ragged", "Cyclic-ragged"])
+def test_two_pe_exchange_gloo(orc, dist_kind, ragged):
+    """ragged: PEs with different batch lengths, an empty batch on one PE, and a
+    call where one PE passes an MVSI shape and the other an MVMI one."""
     ws = 2
     port = 29600 + dist_kind * 7 + (13 if ragged else 0) + (os.getpid() % 200)
     with tempfile.TemporaryDirectory() as d:
-        mp.spawn(_worker, args=(ws, port, d, dist_kind, chunk, ragged), nprocs=ws, join=True)
+        mp.spawn(_worker, args=(ws, port, d, dist_kind, ragged), nprocs=ws, join=True)
         pe = [dict(np.load(os.path.join(d, f"pe{r}.npz"))) for r in range(ws)]
     # oracle: both PEs' batch_add applied (order-independent wrapping add)
     from simworld import SimArray
@@ -255,5 +354,110 @@ def test_two_pe_exchange_gloo(orc, dist_kind, chunk, ragged):
         exp4[[1, 2, 3]] += np.array([100, 200, 300], dtype=np.uint64)
         for r in range(ws):
             assert np.array_equal(pe[r]["after_mixed"], exp4)
+        assert np.array_equal(pe[0]["empty_olds"], exp4[[9, 10, 11]]) and pe[1]["empty_olds"].size == 0
+        exp4[[9, 10, 11]] += np.uint64(2)
+        for r in range(ws):
+            assert np.array_equal(pe[r]["after_empty"], exp4)
     for r in range(ws):
         assert np.array_equal(pe[r]["cas_ok"].astype(bool), pe[r]["cas_cur"] == 0)
+
+
+# ---------------------------------------------------------------- lmr_exchange_plan
+def _plan(_capi, npes, iw, eb, sh, rh):
+    out = [np.zeros(npes, np.uint64) for _ in range(8)]
+    sh, rh = np.ascontiguousarray(sh, np.int64), np.ascontiguousarray(rh, np.int64)
+    k = _capi.lmr_exchange_plan(npes, iw, eb, sh.ctypes.data, rh.ctypes.data, *[a.ctypes.data for a in out])
+    return k, out
+
+
+def test_exchange_plan_array_values(capi):
+    sh = np.array([[3, -1, 0, 0, 2], [0, -1, 0, 0, 2], [5, -1, 0, 0, 2]])
+    rh = np.array([[4, -1, 0, 0, 1], [2, -1, 0, 0, 7], [0, -1, 0, 0, 3]])
+    k, (isb, iso, irb, iro, vsb, vso, vrb, vro) = _plan(capi, 3, 4, 8, sh, rh)
+    assert k == 7                                          # the largest chunk count any PE announced
+    assert list(isb) == [12, 0, 20] and list(iso) == [0, 12, 12]
+    assert list(irb) == [16, 8, 0] and list(iro) == [0, 16, 24]
+    assert list(vsb) == [24, 0, 40] and list(vso) == [0, 24, 24]
+    assert list(vrb) == [32, 16, 0] and list(vro) == [0, 32, 48]
+
+
+def test_exchange_plan_mvsi_and_scalar(capi):
+    """MVSI senders send values but no index (it travels in the header); scalar
+    senders send indices but no values."""
+    sh = np.array([[0, -1, 0, 0, 1], [6, 17, 0, 0, 1]])          # this PE: MVSI block of 6 for PE 1
+    rh = np.array([[9, -1, 1, 42, 1], [6, 3, 0, 0, 1]])          # from PE 0: 9 scalar; from PE 1: MVSI
+    k, (isb, iso, irb, iro, vsb, vso, vrb, vro) = _plan(capi, 2, 2, 4, sh, rh)
+    assert k == 1
+    assert list(isb) == [0, 0] and list(vsb) == [0, 24] and list(vso) == [0, 0]
+    assert list(irb) == [18, 0] and list(vrb) == [0, 24] and list(vro) == [0, 0]
+
+
+def test_exchange_plan_empty_and_negative_counts(capi):
+    sh = np.zeros((4, 5), np.int64)
+    sh[:, 1] = -1
+    rh = sh.copy()
+    rh[2, 0] = -5                                           # never trusted as a size
+    k, out = _plan(capi, 4, 8, 8, sh, rh)
+    assert k == 0 and all(int(a.sum()) == 0 for a in out)
+
+
+# ---------------------------------------------------------------- host transport over gloo
+def _transport_worker(rank, ws, port, outdir):
+    sys.path.insert(0, ROOT)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch.distributed as dist
+    dist.init_process_group("gloo", rank=rank, world_size=ws)
+    from _lamellar_bootstrap import load_package
+    lam = load_package()
+    from lamellar_runtime_amd.world import HostTransport
+    tp = HostTransport(ws, rank, dist.group.WORLD)
+    t = tp.t
+    assert (t.num_pes, t.my_pe, t.host_buffers) == (ws, rank, 1)
+    out = {}
+    # all-to-all: 40-byte rows (one exchange header row per PE)
+    send = np.arange(ws * 5, dtype=np.int64) + 1000 * rank
+    recv = np.zeros_like(send)
+    assert t.alltoall(t.self, send.ctypes.data, recv.ctypes.data, 40, None) == 0
+    out["a2a"] = recv
+    u64p = lambda a: a.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64))
+    for unit in (1, 2, 4, 8):
+        # PE r sends (r + 1) * (p + 2) elements to PE p; element = (src, dst, j) encoded
+        cnt_s = np.array([(rank + 1) * (p + 2) for p in range(ws)], np.uint64)
+        cnt_r = np.array([(p + 1) * (rank + 2) for p in range(ws)], np.uint64)
+        sb, rb = cnt_s * np.uint64(unit), cnt_r * np.uint64(unit)
+        so = np.concatenate([[0], np.cumsum(sb)[:-1]]).astype(np.uint64)
+        ro = np.concatenate([[0], np.cumsum(rb)[:-1]]).astype(np.uint64)
+        it = {1: np.uint8, 2: np.uint16, 4: np.uint32, 8: np.uint64}[unit]
+        sv = np.concatenate([(np.arange(int(cnt_s[p])) + 16 * rank + 4 * p) % 251 for p in range(ws)]).astype(it)
+        rv = np.zeros(int(cnt_r.sum()), it)
+        assert t.alltoallv(t.self, sv.ctypes.data, u64p(sb), u64p(so), rv.ctypes.data, u64p(rb), u64p(ro),
+                           unit, None) == 0
+        out[f"v{unit}"] = rv
+    # a failing callback returns an error status (not LMR_OK) and keeps the exception
+    bad = np.array([1, 0], np.uint64)
+    st = t.alltoallv(t.self, send.ctypes.data, u64p(bad), u64p(bad), recv.ctypes.data, u64p(bad), u64p(bad), 1,
+                     None)
+    out["bad_status"] = np.array([st])
+    try:
+        tp.raise_pending()
+        out["raised"] = np.array([0])
+    except ValueError:
+        out["raised"] = np.array([1])
+    np.savez(os.path.join(outdir, f"t{rank}.npz"), **out)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_host_transport_callbacks_gloo():
+    ws = 2
+    port = 29650 + (os.getpid() % 200)
+    with tempfile.TemporaryDirectory() as d:
+        mp.spawn(_transport_worker, args=(ws, port, d), nprocs=ws, join=True)
+        pe = [dict(np.load(os.path.join(d, f"t{r}.npz"))) for r in range(ws)]
+    for r in range(ws):
+        exp = np.concatenate([np.arange(r * 5, r * 5 + 5) + 1000 * p for p in range(ws)])
+        assert np.array_equal(pe[r]["a2a"], exp)
+        for unit in (1, 2, 4, 8):
+            exp = np.concatenate([(np.arange((p + 1) * (r + 2)) + 16 * p + 4 * r) % 251 for p in range(ws)])
+            assert np.array_equal(pe[r][f"v{unit}"].astype(np.int64), exp)
+        assert pe[r]["bad_status"][0] != 0 and pe[r]["raised"][0] == 1
