@@ -80,6 +80,7 @@ def stage_bytes_per_op(stage, iw, vb, eb, n, shard_len, fetch):
         "pack": 8 + 8 + vb + iw + vb + 4,
         "scatter_results": 4 + 2 * eb,
         "mvsi": vb + res,
+        "window": 2 * iw + vb + 4 + vb + pos,           # count (idx) + scatter (idx, val in; u32 idx, val, pos out)
     }.get(stage, 0.0)
 
 
@@ -481,7 +482,7 @@ def main():
             row["frac"] = row["achieved_GBps"] * 1e9 / HBM_PEAK
         stage_rows[st] = row
     apply_stages = [st for st in ("direct", "mvsi", "bin_count", "scan", "bin_scatter", "fine_scatter",
-                                  "tile_apply", "unpartition", "pack", "scatter_results") if st in per]
+                                  "tile_apply", "unpartition", "pack", "scatter_results", "window") if st in per]
     apply_ms = sum(per[st][0] * per[st][1] for st in apply_stages)
 
     out = {

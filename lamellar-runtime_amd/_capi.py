@@ -130,7 +130,7 @@ SIGNATURES = {
 }
 
 STAGES = ["direct", "mvsi", "bin_count", "scan", "bin_scatter", "tile_apply", "pack",
-          "scatter_results", "fine_scatter", "unpartition"]
+          "scatter_results", "fine_scatter", "unpartition", "window"]
 
 _lib = None
 

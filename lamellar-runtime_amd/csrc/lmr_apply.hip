@@ -1101,6 +1101,8 @@ static int tile_shift_for(int dtype) {
     return sh;
 }
 
+int tile_shift(int dtype) { return tile_shift_for(dtype); }
+
 bool tiled_supported(int dtype, uint64_t shard_len) {
     uint64_t tiles = (shard_len + (uint64_t(1) << tile_shift_for(dtype)) - 1) >> tile_shift_for(dtype);
     return tiles >= 1 && tiles <= uint64_t(kMaxTiles);

@@ -228,11 +228,18 @@ lmr_status_t run_apply(lmr_ctx* ctx, const lmr_apply_desc_t* d, ApplyArgs a, int
     bool tiled = false;
     if (d->strategy == LMR_STRATEGY_TILED) {
         if (!ctx->ws || ctx->rec_cap == 0) return LMR_E_WORKSPACE;
-        if (!tiled_supported(int(d->dtype), d->shard_len)) return LMR_E_UNSUPPORTED;
         tiled = true;
     } else if (d->strategy == LMR_STRATEGY_AUTO) {
-        tiled = ctx->ws && ctx->rec_cap > 0 && a.n >= 65536 &&
-                tiled_supported(int(d->dtype), d->shard_len);
+        tiled = ctx->ws && ctx->rec_cap > 0 && a.n >= 65536;
+    }
+    if (tiled && !tiled_supported(int(d->dtype), d->shard_len)) {
+        // shard above one tiled window: records by window, each window tiled
+        const hipError_t e = apply_windowed(ctx, d, a, iw, s, [ctx](const lmr_apply_desc_t* dw, const ApplyArgs& b,
+                                                                    hipStream_t st) {
+            return run_apply(ctx, dw, b, 4, st) == LMR_OK ? hipSuccess : hipErrorUnknown;
+        });
+        if (e == hipErrorNotSupported) return hip_status(launch_apply_direct(int(d->dtype), iw, a, s));
+        return hip_status(e);
     }
     if (!tiled) return hip_status(launch_apply_direct(int(d->dtype), iw, a, s));
     if (const uint64_t split = staged_mode_split(int(d->dtype), a.op, a.ret, d->shard_len,
@@ -304,6 +311,7 @@ lmr_status_t lmr_ctx_destroy(lmr_ctx_t* ctx) {
     host_stage_free(ctx->host);
     stage_state_free(ctx->stage);
     xstate_free(ctx->xch);
+    win_state_free(ctx->win);
     if (ctx->ws) (void)hipFree(ctx->ws);
     if (ctx->d_err) (void)hipFree(ctx->d_err);
     if (ctx->prof) {

@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stddef.h>
+#include <functional>
 #include "../../include/lamellar_gpu_ops.h"
 
 namespace lmr { struct Prof; }
@@ -11,6 +12,7 @@ namespace lmr { struct Prof; }
 namespace lmr { struct HostStage; void host_stage_free(HostStage* h); }
 namespace lmr { struct StageState; void stage_state_free(StageState* s); void stage_abort(StageState* s); }
 namespace lmr { struct XState; void xstate_free(XState* x); }
+namespace lmr { struct WinState; void win_state_free(WinState* w); }
 
 struct lmr_ctx {
     int device = 0;
@@ -24,6 +26,7 @@ struct lmr_ctx {
     lmr::HostStage* host = nullptr;  // host-buffer ingestion staging (lmr_apply_mvmi_host), lazily made
     lmr::StageState* stage = nullptr;  // staged-apply session (lmr_stage_*), lazily made
     lmr::XState* xch = nullptr;        // multi-PE exchange state (lmr_batch_exchange), lazily made
+    lmr::WinState* win = nullptr;      // window partition of shards above one tiled window, lazily made
 };
 
 namespace lmr {
@@ -35,6 +38,7 @@ constexpr int kBinBlock = 1024;           // threads per bin/scatter block
 constexpr int kMaxBinBlocks = 1024;       // G: blocks of the bin passes
 constexpr int kScanItems = 4096;          // elements per scan block (1024 threads x 4)
 constexpr int kMaxPackPes = 512;
+constexpr int kMaxWindows = 256;          // tiled windows per shard (lmr_window.hip)
 constexpr int kMaxRegions = 32;           // staged-apply regions per session
 constexpr int kStageInfoWords = 512;      // staged-apply piece table + per-region totals (u32)
 constexpr uint64_t kStageMaxRegion = uint64_t(1) << 30;   // records per staged region
@@ -117,6 +121,14 @@ hipError_t launch_apply_mvsi(int dtype, const ApplyArgs& a, uint64_t index, hipS
 hipError_t launch_apply_tiled(int dtype, int index_size, const ApplyArgs& a, const TiledWs& w,
                               hipStream_t s);
 bool tiled_supported(int dtype, uint64_t shard_len);
+// log2 of the elements of one 64 KiB shard tile
+int tile_shift(int dtype);
+// elements of one tiled window (kMaxTiles tiles)
+uint64_t tiled_window_len(int dtype);
+// Shards above one window: partition the records by window, apply each window's
+// records with apply_one (its slice of the shard as desc; u32 window-local offsets),
+// then results back to input order. Host waits once per piece for the window counts.
+using WindowApplyFn = std::function<hipError_t(const lmr_apply_desc_t*, const ApplyArgs&, hipStream_t)>;
 // true when the two-level partition's per-(bucket, producer block) segments of an
 // n-record piece would be short (< 8192 records) and fixed-size pieces pay
 bool piece_partition_pays(int dtype, uint64_t shard_len, uint64_t n);
@@ -175,6 +187,8 @@ hipError_t launch_reduce(int dtype, int op, const void* x, uint64_t n, uint64_t*
 hipError_t launch_scatter_results(const uint8_t* in, const uint32_t* pos, uint64_t n,
                                   uint32_t elem_bytes, uint8_t* out, const uint8_t* ok_in,
                                   uint8_t* ok_out, Prof* prof, hipStream_t s);
+hipError_t apply_windowed(lmr_ctx* ctx, const lmr_apply_desc_t* d, const ApplyArgs& a, int iw, hipStream_t s,
+                          const WindowApplyFn& apply_one);
 
 inline int dtype_bytes(int d) {
     switch (d) {

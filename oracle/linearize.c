@@ -14,9 +14,13 @@
  *
  * Method: a depth-first search over serial orders. At state s the candidates are
  * the unused records whose step from s (orc_elem_step, the oracle's own per-record
- * semantics) returns their recorded value and Ok flag. A candidate that leaves the
- * state unchanged is taken at once and never branched on (it can be moved to any
- * other point where the state is s). Among state-changing candidates only one per
+ * semantics) returns their recorded value and Ok flag. A record that returns the
+ * state it ran at fits at that one state only; if it leaves it unchanged it is taken
+ * at once and never branched on. Other records (compare_exchange_epsilon successes,
+ * ops returning nothing) may fit at several states, as a no-op at one and a change at
+ * another, so they are only branched on as changes; any left over when the final
+ * value is reached must fit as a no-op at some visited state. Among state-changing
+ * candidates only one per
  * distinct value is tried. Records are found through a hash of their returned
  * value; the search gives up after `max_nodes` branch steps (reported apart).
  * When every record of an element returns the state it ran at (fetch_*, swap,
@@ -141,6 +145,21 @@ static int euler(const Ctx* c, uint64_t init, uint64_t final_bits, uint64_t* key
 
 typedef struct { uint64_t state; uint32_t trail_len; uint32_t tried_len; } Frame;
 
+/* every record the trail has not used leaves some visited state unchanged there
+   (so it can be inserted at that point of the order) */
+static int placeable_rest(const Ctx* c, const Frame* stack, uint32_t sp, uint64_t s, uint32_t tl) {
+    if (tl == c->m) return 1;
+    for (uint32_t j = 0; j < c->m; j++) {
+        if (c->used[j]) continue;
+        uint64_t ns;
+        int ok = fits(c, j, s, &ns) && ns == s;
+        for (uint32_t f = 0; !ok && f < sp; f++)
+            ok = fits(c, j, stack[f].state, &ns) && ns == stack[f].state;
+        if (!ok) return 0;
+    }
+    return 1;
+}
+
 /* Iterative DFS; each level owns the range [tried_len, tr) of values it has tried.
  * 1 = linearisable, 0 = not, -1 = gave up (node budget). */
 static int search(Ctx* c, uint64_t init, uint64_t final_bits, uint32_t* trail, uint32_t* tried,
@@ -160,14 +179,12 @@ static int search(Ctx* c, uint64_t init, uint64_t final_bits, uint32_t* trail, u
                         continue;
                     c->used[j] = 1; trail[tl++] = (uint32_t)j; progress = 1;
                 }
-                for (uint32_t q = 0; q < c->nother; q++) {
-                    const int32_t j = c->other[q];
-                    uint64_t ns;
-                    if (c->used[j] || !fits(c, (uint32_t)j, s, &ns) || ns != s) continue;
-                    c->used[j] = 1; trail[tl++] = (uint32_t)j; progress = 1;
-                }
             }
-            if (tl == c->m && s == (final_bits & mk)) return 1;
+            /* records of the `other` list are not absorbed on the way: one that is a no-op
+               here may be needed elsewhere as a state change (compare_exchange_epsilon with
+               |new - current| < eps fits both at `current` and at `new`). Any of them left
+               unused at the end is placed as a no-op at a visited state, if one fits. */
+            if (s == (final_bits & mk) && placeable_rest(c, stack, sp, s, tl)) return 1;
             stack[sp].state = s;
             stack[sp].trail_len = tl;
             stack[sp].tried_len = tr;

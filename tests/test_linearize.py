@@ -137,6 +137,29 @@ def test_known_small_cases(orc):
     assert orc.check_linearizable(3, c, u64, CAS_EPS, [6], [9], idx[:1], [9], [6], [1], **eps)[0] == 1
 
 
+def test_cas_eps_record_that_is_a_noop_at_one_state_and_a_change_at_another(orc):
+    """NativeAtomic compare_exchange_epsilon(current = 3, eps = 2) of new = 4 returns
+    4 both at state 3 (exact match: Ok(new), 3 -> 4) and at state 4 (|4 - 3| < 2:
+    Ok(old), no change). From 4: C = cas_eps(new = 3) moves 4 -> 3 returning Ok(4),
+    then A = cas_eps(new = 4) moves 3 -> 4 returning Ok(4). Taking A as a no-op at the
+    initial 4 would strand the search at 3; the only order is C, A."""
+    u8 = np.uint8
+    c = CODE["u8"]
+    idx = np.zeros(2, dtype=np.uint64)
+    eps = dict(current=u8(3), eps=u8(2))
+    # records: A (new 4, Ok(4)), C (new 3, Ok(4)); 4 -> 3 -> 4
+    assert orc.check_linearizable(1, c, u8, CAS_EPS, np.array([4], u8), np.array([4], u8), idx,
+                                  np.array([4, 3], u8), np.array([4, 4], u8), np.array([1, 1], np.uint8),
+                                  **eps)[0] == 0
+    # ... they may also end at 3 (A as a no-op at 4, then C), never at 5
+    assert orc.check_linearizable(1, c, u8, CAS_EPS, np.array([4], u8), np.array([3], u8), idx,
+                                  np.array([4, 3], u8), np.array([4, 4], u8), np.array([1, 1], np.uint8),
+                                  **eps)[0] == 0
+    assert orc.check_linearizable(1, c, u8, CAS_EPS, np.array([4], u8), np.array([5], u8), idx,
+                                  np.array([4, 3], u8), np.array([4, 4], u8), np.array([1, 1], np.uint8),
+                                  **eps)[0] == 1
+
+
 @pytest.mark.parametrize("dt,op", [("u16", FETCH_ADD), ("u8", FETCH_XOR), ("i16", FETCH_SUB), ("u8", SWAP),
                                    ("u16", CAS)])
 def test_small_type_hot_element_revisits_states(orc, dt, op):
