@@ -76,6 +76,40 @@ class lmr_transport_t(Structure):
 
 XHDR_WORDS = 5     # LMR_XHDR_WORDS
 
+
+# ---- AM wire format (include/lamellar_gpu_ops.h, "AM wire format")
+class lmr_net_darc_t(Structure):
+    _fields_ = [("inner_addr", c_uint64), ("backend", c_uint32), ("reserved_", c_uint32),
+                ("orig_world_pe", c_uint64), ("orig_team_pe", c_uint64)]
+
+
+class lmr_am_view_t(Structure):
+    _fields_ = [("shape", c_uint32), ("kind", c_uint32), ("dtype", c_uint32), ("op", c_uint32),
+                ("cmp_bits", c_uint64), ("eps_bits", c_uint64),
+                ("data", lmr_net_darc_t), ("lock", lmr_net_darc_t),
+                ("native_type", c_uint32), ("distribution", c_uint32),
+                ("orig_elem_per_pe", c_uint64), ("orig_remaining_elems", c_uint64), ("elem_size", c_uint64),
+                ("offset", c_uint64), ("size", c_uint64),
+                ("sub", c_uint32), ("index_size", c_uint32),
+                ("val_bits", c_uint64), ("index", c_uint64),
+                ("recs_offset", c_uint64), ("recs_bytes", c_uint64), ("body_bytes", c_uint64)]
+
+
+class lmr_msg_entry_t(Structure):
+    _fields_ = [("cmd", c_uint32), ("src", c_uint32), ("am_id", ctypes.c_int32),
+                ("shape", c_uint32), ("kind", c_uint32), ("dtype", c_uint32),
+                ("team_addr", c_uint64), ("req_id", c_uint64), ("req_sub_id", c_uint64),
+                ("body_offset", c_uint64), ("body_bytes", c_uint64)]
+
+
+class lmr_shard_t(Structure):
+    _fields_ = [("shard", c_void_p), ("shard_len", c_uint64), ("strategy", c_uint32), ("reserved_", c_uint32)]
+
+
+AM_RESOLVER_FN = ctypes.CFUNCTYPE(c_int, c_void_p, ctypes.c_int32, POINTER(c_uint32), POINTER(c_uint32),
+                                  POINTER(c_uint32))
+SHARD_RESOLVER_FN = ctypes.CFUNCTYPE(c_int, c_void_p, POINTER(lmr_am_view_t), POINTER(lmr_shard_t))
+
 # name -> (restype, argtypes). Every symbol of include/lamellar_gpu_ops.h.
 SIGNATURES = {
     "lmr_abi_version": (c_uint32, []),
@@ -127,6 +161,15 @@ SIGNATURES = {
                                    c_void_p, c_uint64, c_uint64, c_void_p, c_void_p, c_uint64, c_void_p,
                                    c_void_p, c_void_p]),
     "lmr_exchange_plan": (c_uint64, [c_uint32, c_uint32, c_uint32, c_void_p, c_void_p] + [c_void_p] * 8),
+    "lmr_am_decode": (c_int, [c_void_p, c_uint64, c_uint32, c_uint32, c_uint32, POINTER(lmr_am_view_t)]),
+    "lmr_am_encode": (c_int, [POINTER(lmr_am_view_t), c_void_p, c_void_p, c_uint64, POINTER(c_uint64)]),
+    "lmr_msg_parse": (c_int, [c_void_p, c_uint64, AM_RESOLVER_FN, c_void_p, POINTER(lmr_msg_entry_t), c_uint32,
+                              POINTER(c_uint32)]),
+    "lmr_reply_bytes": (c_uint64, [c_uint32, c_uint32, c_uint64]),
+    "lmr_reply_encode": (c_int, [c_uint32, c_uint32, c_uint64, c_void_p, c_void_p, c_void_p, c_uint64]),
+    "lmr_apply_msg": (c_int, [c_void_p, c_void_p, c_uint64, AM_RESOLVER_FN, SHARD_RESOLVER_FN, c_void_p, c_void_p,
+                              c_uint64, POINTER(c_uint64), POINTER(c_uint64), c_uint32, POINTER(c_uint32),
+                              c_void_p]),
 }
 
 STAGES = ["direct", "mvsi", "bin_count", "scan", "bin_scatter", "tile_apply", "pack",

@@ -312,6 +312,7 @@ lmr_status_t lmr_ctx_destroy(lmr_ctx_t* ctx) {
     stage_state_free(ctx->stage);
     xstate_free(ctx->xch);
     win_state_free(ctx->win);
+    wire_bufs_free(ctx->wire);
     if (ctx->ws) (void)hipFree(ctx->ws);
     if (ctx->d_err) (void)hipFree(ctx->d_err);
     if (ctx->prof) {

@@ -13,6 +13,7 @@ namespace lmr { struct HostStage; void host_stage_free(HostStage* h); }
 namespace lmr { struct StageState; void stage_state_free(StageState* s); void stage_abort(StageState* s); }
 namespace lmr { struct XState; void xstate_free(XState* x); }
 namespace lmr { struct WinState; void win_state_free(WinState* w); }
+namespace lmr { struct WireBufs; void wire_bufs_free(WireBufs* b); }
 
 struct lmr_ctx {
     int device = 0;
@@ -27,6 +28,7 @@ struct lmr_ctx {
     lmr::StageState* stage = nullptr;  // staged-apply session (lmr_stage_*), lazily made
     lmr::XState* xch = nullptr;        // multi-PE exchange state (lmr_batch_exchange), lazily made
     lmr::WinState* win = nullptr;      // window partition of shards above one tiled window, lazily made
+    lmr::WireBufs* wire = nullptr;     // staging of lmr_apply_msg (AM wire format), lazily made
 };
 
 namespace lmr {

@@ -246,6 +246,55 @@ class DeviceKernels:
         transport.raise_pending()
         check(st, "lmr_batch_exchange")
 
+    def apply_msg(self, msg: bytes, resolve, shard_of, max_entries=1 << 16):
+        """lmr_apply_msg over one lamellae message (single AM or batched) in host memory.
+        resolve(am_id) -> (shape, kind, dtype code) of a registered op AM, or None;
+        shard_of(view) -> (device tensor, shard_len, strategy) for a decoded AM, or None
+        to skip it. Returns {entry index: reply bytes} for the returning AMs."""
+        errs = []
+
+        def res_cb(_user, am_id, shape, kind, dtype):
+            try:
+                r = resolve(int(am_id))
+            except Exception as e:  # noqa: BLE001 - reported after the C call
+                errs.append(e)
+                return 1
+            if r is None:
+                return 1
+            shape[0], kind[0], dtype[0] = (int(x) for x in r)
+            return 0
+
+        keep = []
+
+        def shard_cb(_user, view, out):
+            try:
+                r = shard_of(view.contents)
+            except Exception as e:  # noqa: BLE001
+                errs.append(e)
+                return 1
+            if r is None:
+                return 1
+            t, slen, strategy = r
+            keep.append(t)
+            out[0].shard = t.data_ptr()
+            out[0].shard_len = int(slen)
+            out[0].strategy = int(strategy)
+            return 0
+
+        rfn, sfn = _capi.AM_RESOLVER_FN(res_cb), _capi.SHARD_RESOLVER_FN(shard_cb)
+        raw = (ctypes.c_uint8 * max(len(msg), 1)).from_buffer_copy(msg if msg else b"\0")
+        cap = 16 * len(msg) + 4096
+        replies = (ctypes.c_uint8 * cap)()
+        offs = (c_uint64 * max_entries)()
+        lens = (c_uint64 * max_entries)()
+        n = c_uint32()
+        st = self.lib.lmr_apply_msg(self.ctx, raw, len(msg), rfn, sfn, None, replies, cap, offs, lens, max_entries,
+                                    byref(n), self.stream())
+        if errs:
+            raise errs[0]
+        check(st, "lmr_apply_msg")
+        return {e: bytes(replies[int(offs[e]):int(offs[e]) + int(lens[e])]) for e in range(n.value) if lens[e]}
+
     def scatter_results(self, res_in, pos, n, eb, res_out, ok_in=None, ok_out=None):
         st = self.lib.lmr_scatter_results(_p(res_in), _p(pos), int(n), int(eb), _p(res_out),
                                           _p(ok_in), _p(ok_out), self.stream())

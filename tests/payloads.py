@@ -19,8 +19,9 @@ reference's Cargo.toml (so tests/rem.rs and tests/fetch_rem.rs cannot launch the
 """
 import numpy as np
 
-from opgen import (ADD, CAS, CAS_EPS, DIV, FETCH_ADD, FETCH_AND, FETCH_DIV, FETCH_MUL, FETCH_OR,
-                   FETCH_REM, FETCH_SUB, LOAD, NP, REM, STORE)
+from opgen import (ADD, AND, CAS, CAS_EPS, DIV, FETCH_ADD, FETCH_AND, FETCH_DIV, FETCH_MUL, FETCH_OR,
+                   FETCH_REM, FETCH_SHL, FETCH_SHR, FETCH_SUB, FETCH_XOR, LOAD, MUL, NP, OR, REM, SHL, SHR,
+                   STORE, SUB, XOR)
 
 INT_TYPES = ["u8", "u16", "u32", "u64", "i8", "i16", "i32", "i64"]
 ALL_TYPES = INT_TYPES + ["f32", "f64"]
@@ -318,3 +319,129 @@ def index_containers(local_data_of=None):
     if local_data_of is not None:
         out.append(("&UnsafeArray<T>", local_data_of))
     return out
+
+
+# ---------------------------------------------------------------- examples/array_examples/array_ops.rs
+def _step(op, dt, x, v):
+    """One record on a register copy (the reference's per-op semantics, array_ops.rs:327-458)."""
+    t = NP[dt]
+    with np.errstate(over="ignore"):
+        x, v = t(x), t(v)
+        if op in (ADD, FETCH_ADD):
+            return t(x + v)
+        if op in (SUB, FETCH_SUB):
+            return t(x - v)
+        if op in (MUL, FETCH_MUL):
+            return t(x * v)
+        if op in (DIV, FETCH_DIV):
+            return t(x / v) if dt.startswith("f") else t(x // v)
+        if op in (REM, FETCH_REM):
+            return t(np.fmod(x, v)) if dt.startswith("f") else t(x % v)
+        if op in (AND, FETCH_AND):
+            return t(x & v)
+        if op in (OR, FETCH_OR):
+            return t(x | v)
+        if op in (XOR, FETCH_XOR):
+            return t(x ^ v)
+        bits = 8 * t(0).itemsize
+        if op in (SHL, FETCH_SHL):
+            return t((int(x) << (int(v) & (bits - 1))) & ((1 << bits) - 1))
+        return t(int(x) >> (int(v) & (bits - 1)))
+
+
+def _reachable(op, dt, x0, vals):
+    """Every value an element can hold after some subset of `vals` in some order (the
+    olds one PE's fetch may return while the other PEs' records run concurrently)."""
+    states = {NP[dt](x0).tobytes(): NP[dt](x0)}
+    frontier = [(NP[dt](x0), tuple(range(len(vals))))]
+    while frontier:
+        nxt = []
+        for x, rest in frontier:
+            for j in rest:
+                y = _step(op, dt, x, vals[j])
+                r = tuple(q for q in rest if q != j)
+                if y.tobytes() not in states or r:
+                    states[y.tobytes()] = y
+                    nxt.append((y, r))
+        frontier = nxt
+    return set(states)
+
+
+ARRAY_OPS_EXAMPLE = {
+    # dt: [(op, fetch op, init, per-PE value (pe, npes) -> v, reset before the fetch phase,
+    #       trailing single op at index 3 or 1 (index, value(npes)) or None)]
+    "u8": [(ADD, FETCH_ADD, 0, lambda pe, n: 1, False, (3, lambda n: 1)),
+           (SUB, FETCH_SUB, 10, lambda pe, n: 1, False, (3, lambda n: 1)),
+           (MUL, FETCH_MUL, 1, lambda pe, n: 2, False, None),
+           (DIV, FETCH_DIV, 255, lambda pe, n: 2, False, None),
+           (REM, FETCH_REM, 255, lambda pe, n: 2, False, None),
+           (AND, FETCH_AND, 255, lambda pe, n: 1 << pe, True, (3, lambda n: 1 << n)),
+           (OR, FETCH_OR, 0, lambda pe, n: 1 << pe, True, (3, lambda n: 1 << n)),
+           (XOR, FETCH_XOR, 0, lambda pe, n: 1 << pe, True, (3, lambda n: 1 << n)),
+           (SHL, FETCH_SHL, 1, lambda pe, n: 3, False, (1, lambda n: 3)),
+           (SHR, FETCH_SHR, 255, lambda pe, n: 3, False, (1, lambda n: 3))],
+    "f64": [(ADD, FETCH_ADD, 0.0, lambda pe, n: 1.0, False, (3, lambda n: 1.0)),
+            (SUB, FETCH_SUB, 10.0, lambda pe, n: 1.0, False, None),
+            (MUL, FETCH_MUL, 1.0, lambda pe, n: 2.5, False, None),
+            (DIV, FETCH_DIV, 1000.0, lambda pe, n: 2.5, False, None),
+            (REM, FETCH_REM, 1000.0, lambda pe, n: 2.5, False, None)],
+}
+
+
+def array_ops_example_payload(W, dt):
+    """examples/array_examples/array_ops.rs:474-830 on AtomicArray<u8> and AtomicArray<f64>
+    (num_pes * 10 elements, Block): each test_<op> (:80-458) stores init, every PE issues
+    <op>(i, val) for every index i, then fetch_<op>(i, val) for every i (test_and / test_or /
+    test_xor store init again first), and main follows some tests with one more <op> at
+    index 3 (or 1 for shl / shr) from every PE. The example only prints; its answers follow
+    from the ops: after the first phase every element holds init with every PE's value
+    applied, the fetch olds a PE gets are init' with some subset of the other PEs' values
+    applied (_reachable), and the final value has every value applied again. Also
+    test_store_load (:360-392): PE p stores p on i = p (mod num_pes), every load(i) reads
+    i % num_pes. Shl / shr here are the batched path's (array_ops.rs:420-458); the element
+    wrapper's ShlAssign / ShrAssign (native_atomic.rs:90-111) shift the wrong way on a CAS
+    retry (shl) or on the first try (shr) -- not on this path, not reproduced."""
+    npes = W.npes
+    n = 10 * npes
+    t = NP[dt]
+    a = W.array("AtomicArray", n, 0, dt)
+    idx = np.arange(n, dtype=np.uint64)
+    for op, fop, init, val, reset, trail in ARRAY_OPS_EXAMPLE[dt]:
+        vals = [t(val(pe, npes)) for pe in range(npes)]
+        a.fill(t(init))
+        for pe in range(npes):
+            a.op(op, idx, vals[pe], pe=pe)
+        x1 = t(init)
+        for v in vals:
+            x1 = _step(op, dt, x1, v)
+        got = a.to_numpy()
+        assert np.array_equal(got, np.full(n, x1, dtype=t)), ("phase 1", dt, op, npes, got[:4], x1)
+        if reset:
+            a.fill(t(init))
+            x1 = t(init)
+        for pe in range(npes):
+            res, _ = a.op(fop, idx, vals[pe], pe=pe)
+            others = [vals[q] for q in range(npes) if q != pe]
+            ok = _reachable(op, dt, x1, others)
+            assert all(t(r).tobytes() in ok for r in res), ("fetch olds", dt, fop, npes, pe)
+        x2 = x1
+        for v in vals:
+            x2 = _step(op, dt, x2, v)
+        assert np.array_equal(a.to_numpy(), np.full(n, x2, dtype=t)), ("phase 2", dt, fop, npes)
+        if trail is not None:
+            i, tv = trail
+            for pe in range(npes):
+                a.op(op, np.array([i], dtype=np.uint64), t(tv(npes)), pe=pe)
+            x3 = x2
+            for _ in range(npes):
+                x3 = _step(op, dt, x3, t(tv(npes)))
+            want = np.full(n, x2, dtype=t)
+            want[i] = x3
+            assert np.array_equal(a.to_numpy(), want), ("trailing", dt, op, npes)
+    # test_store_load
+    a.fill(t(0))
+    for pe in range(npes):
+        a.op(STORE, np.arange(pe, n, npes, dtype=np.uint64), t(pe), pe=pe)
+    for pe in range(npes):
+        res, _ = a.op(LOAD, idx, t(0), pe=pe)
+        assert np.array_equal(res, (np.arange(n) % npes).astype(t)), ("load", dt, npes)

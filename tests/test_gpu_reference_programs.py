@@ -176,13 +176,16 @@ def test_reference_add_program_c1(world, lam):
 import payloads as P  # noqa: E402
 import torch  # noqa: E402
 
-from opgen import (ADD, CAS, CAS_EPS, FETCH_ADD, FETCH_AND, FETCH_DIV, FETCH_MUL, FETCH_OR,  # noqa: E402
-                   FETCH_REM, FETCH_SUB, LOAD, REM, STORE)
+from opgen import (ADD, AND, CAS, CAS_EPS, DIV, FETCH_ADD, FETCH_AND, FETCH_DIV, FETCH_MUL,  # noqa: E402
+                   FETCH_OR, FETCH_REM, FETCH_SHL, FETCH_SHR, FETCH_SUB, FETCH_XOR, LOAD, MUL, OR, REM,
+                   SHL, SHR, STORE, SUB, XOR)
 
 _METHOD = {ADD: "batch_add", FETCH_ADD: "batch_fetch_add", FETCH_SUB: "batch_fetch_sub",
            FETCH_MUL: "batch_fetch_mul", FETCH_DIV: "batch_fetch_div", REM: "batch_rem",
            FETCH_REM: "batch_fetch_rem", FETCH_AND: "batch_fetch_bit_and", FETCH_OR: "batch_fetch_bit_or",
-           STORE: "batch_store"}
+           STORE: "batch_store", SUB: "batch_sub", MUL: "batch_mul", DIV: "batch_div", AND: "batch_bit_and",
+           OR: "batch_bit_or", XOR: "batch_bit_xor", FETCH_XOR: "batch_fetch_bit_xor", SHL: "batch_shl",
+           FETCH_SHL: "batch_fetch_shl", SHR: "batch_shr", FETCH_SHR: "batch_fetch_shr"}
 
 
 class _DevArr:
@@ -293,3 +296,9 @@ def test_reference_input_payloads(world, lam, kind):
             P.fetch_add_input_payload(W, kind, n, dist, cont)
             if kind != "UnsafeArray":
                 P.cas_input_payload(W, kind, n, dist)
+
+
+@pytest.mark.parametrize("dt", ["u8", "f64"])
+def test_reference_array_ops_example(world, lam, dt):
+    """examples/array_examples/array_ops.rs (u8 and f64 halves, incl. shl / shr) on the device."""
+    P.array_ops_example_payload(DevWorld(lam, world), dt)

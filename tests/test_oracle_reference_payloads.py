@@ -133,3 +133,10 @@ def test_add_and_fetch_add_input_payloads(orc, npes, dist):
         for n in (4, 100, 2000):
             P.add_input_payload(SimWorld(orc, npes), kind, n, dist, cont)
             P.fetch_add_input_payload(SimWorld(orc, npes), kind, n, dist, cont)
+
+
+@pytest.mark.parametrize("npes", PES)
+@pytest.mark.parametrize("dt", ["u8", "f64"])
+def test_array_ops_example_payload(orc, dt, npes):
+    """examples/array_examples/array_ops.rs (u8 and f64 halves, incl. shl / shr)."""
+    P.array_ops_example_payload(SimWorld(orc, npes), dt)
