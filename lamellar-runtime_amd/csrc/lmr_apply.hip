@@ -982,7 +982,7 @@ __global__ __launch_bounds__(1024) void k_tile_delta(TileArgs a) {
 // dst[k] = src[map[k]] over block-contiguous ranges of k (the forward pass's
 // chunks), so each block's reads stay within the runs its chunk produced and
 // hit L2; map[k] == ~0 marks an out-of-bounds record (left unwritten).
-template <int VB>
+template <int VB, int U>
 __global__ __launch_bounds__(1024) void k_unpartition(const uint32_t* __restrict__ map, uint64_t n,
                                                       const uint32_t* n_dev, uint64_t chunk,
                                                       const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
@@ -993,44 +993,24 @@ __global__ __launch_bounds__(1024) void k_unpartition(const uint32_t* __restrict
     const uint64_t hi = min(lo + chunk, m);
     const V* s = reinterpret_cast<const V*>(src);
     V* d = reinterpret_cast<V*>(dst);
-    // 8-byte values: 4 records per thread, each gathered and stored in turn; values of
-    // <= 4 bytes: 16 gathers in flight per thread before the stores (C5's u32 swap / CAS
-    // olds: 0.96 -> 0.83 ms per step same box; the same for C3's f64 olds: 0.71 -> 0.85 ms)
-    if constexpr (VB >= 8) {
-        for (uint64_t k0 = lo + threadIdx.x; k0 < hi; k0 += 4 * 1024) {
-            uint32_t p[4];
+    const uint32_t nt = blockDim.x;
+    // U records per thread per iteration: all U map loads, then all U gathers, then the stores
+    for (uint64_t k0 = lo + threadIdx.x; k0 < hi; k0 += uint64_t(U) * nt) {
+        uint32_t p[U];
 #pragma unroll
-            for (int j = 0; j < 4; j++) {
-                const uint64_t k = k0 + uint64_t(j) * 1024;
-                p[j] = k < hi ? map[k] : 0xFFFFFFFFu;
-            }
-#pragma unroll
-            for (int j = 0; j < 4; j++) {
-                if (p[j] == 0xFFFFFFFFu) continue;
-                const uint64_t k = k0 + uint64_t(j) * 1024;
-                d[k] = s[p[j]];
-                if (ok_src) ok_dst[k] = ok_src[p[j]];
-            }
+        for (int j = 0; j < U; j++) {
+            const uint64_t k = k0 + uint64_t(j) * nt;
+            p[j] = k < hi ? map[k] : 0xFFFFFFFFu;
         }
-    } else {
-        constexpr int U = 16;
-        for (uint64_t k0 = lo + threadIdx.x; k0 < hi; k0 += U * 1024) {
-            uint32_t p[U];
+        V v[U];
 #pragma unroll
-            for (int j = 0; j < U; j++) {
-                const uint64_t k = k0 + uint64_t(j) * 1024;
-                p[j] = k < hi ? map[k] : 0xFFFFFFFFu;
-            }
-            V v[U];
+        for (int j = 0; j < U; j++) v[j] = (p[j] != 0xFFFFFFFFu) ? s[p[j]] : V(0);
 #pragma unroll
-            for (int j = 0; j < U; j++) v[j] = (p[j] != 0xFFFFFFFFu) ? s[p[j]] : V(0);
-#pragma unroll
-            for (int j = 0; j < U; j++) {
-                if (p[j] == 0xFFFFFFFFu) continue;
-                const uint64_t k = k0 + uint64_t(j) * 1024;
-                d[k] = v[j];
-                if (ok_src) ok_dst[k] = ok_src[p[j]];
-            }
+        for (int j = 0; j < U; j++) {
+            if (p[j] == 0xFFFFFFFFu) continue;
+            const uint64_t k = k0 + uint64_t(j) * nt;
+            d[k] = v[j];
+            if (ok_src) ok_dst[k] = ok_src[p[j]];
         }
     }
 }
@@ -1244,6 +1224,45 @@ static void dispatch_vb_rpt(int vb, int rpt, F&& f) {
 static int fine_blocks_cap() {
     static int v = env_int("LMR_FINE_BLOCKS", 512, 1, 1 << 20);
     return v;
+}
+
+// dst[k] = src[map[k]] over G block-contiguous ranges of `chunk` records, each split into
+// `split` sub-ranges (LMR_UNPART_SPLIT overrides); LMR_UNPART_NT threads per block,
+// LMR_UNPART_U gathers in flight per thread (defaults 1024, and 4 for 8-byte values, 16 for
+// narrower ones). The one-shot path's ranges are the forward pass's chunks, one per CU
+// (split 1); the staged regions' are 64K-record ranges, about 1.6 per CU at C5's size,
+// and 8 sub-ranges per range balance them: C5 un-partition 0.84 -> 0.62 ms (same box).
+// Measured and not kept: 256 / 512-thread blocks, 2 or 8 gathers per thread for 8-byte
+// values (C3 0.81 -> 0.82-0.90 ms), and (value, ok) packed into one u64 for Result ops
+// on narrow types (C5: un-partition -0.01 ms, tile sweep +0.02 ms)
+static hipError_t launch_unpartition(int vb, const uint32_t* map, uint64_t n, const uint32_t* n_dev, uint64_t chunk,
+                                     uint64_t G, const uint8_t* src, uint8_t* dst, const uint8_t* oks, uint8_t* okd,
+                                     hipStream_t s, int dflt_split = 1) {
+    static const int split_env = env_int("LMR_UNPART_SPLIT", 0, 0, 64);
+    static const int nt = env_int("LMR_UNPART_NT", 1024, 64, 1024);
+    static const int uq = env_int("LMR_UNPART_U", 0, 0, 16);
+    const int split = split_env ? split_env : dflt_split;
+    const uint64_t c2 = (chunk + split - 1) / split;
+    const unsigned grid = unsigned(std::max<uint64_t>(1, G * uint64_t(split)));
+    const int u = uq ? uq : (vb >= 8 ? 4 : 16);
+    auto go = [&](auto vbt) {
+        constexpr int VB = decltype(vbt)::value;
+        auto with_u = [&](auto ut) {
+            constexpr int UU = decltype(ut)::value;
+            hipLaunchKernelGGL((k_unpartition<VB, UU>), dim3(grid), dim3(nt), 0, s, map, n, n_dev, c2, src, dst, oks, okd);
+        };
+        if (u >= 16) with_u(std::integral_constant<int, 16>{});
+        else if (u >= 8) with_u(std::integral_constant<int, 8>{});
+        else if (u >= 4) with_u(std::integral_constant<int, 4>{});
+        else with_u(std::integral_constant<int, 2>{});
+    };
+    switch (vb) {
+    case 1: go(std::integral_constant<int, 1>{}); break;
+    case 2: go(std::integral_constant<int, 2>{}); break;
+    case 4: go(std::integral_constant<int, 4>{}); break;
+    default: go(std::integral_constant<int, 8>{}); break;
+    }
+    return hipGetLastError();
 }
 
 // Count-free partition (k_coarse_free / k_fine_free): order-insensitive ops with
@@ -1500,12 +1519,7 @@ hipError_t launch_apply_tiled(int dtype, int index_size, const ApplyArgs& a, con
     const uint8_t* ok_src = (a.ret == LMR_RET_RESULT) ? ok_bin : nullptr;
     auto gather = [&](const uint32_t* map, const uint32_t* n_dev, const uint8_t* src, uint8_t* dst,
                       const uint8_t* oks, uint8_t* okd) {
-        switch (vb) {
-        case 1: hipLaunchKernelGGL((k_unpartition<1>), dim3(unsigned(G)), dim3(1024), 0, s, map, a.n, n_dev, b.chunk, src, dst, oks, okd); break;
-        case 2: hipLaunchKernelGGL((k_unpartition<2>), dim3(unsigned(G)), dim3(1024), 0, s, map, a.n, n_dev, b.chunk, src, dst, oks, okd); break;
-        case 4: hipLaunchKernelGGL((k_unpartition<4>), dim3(unsigned(G)), dim3(1024), 0, s, map, a.n, n_dev, b.chunk, src, dst, oks, okd); break;
-        default: hipLaunchKernelGGL((k_unpartition<8>), dim3(unsigned(G)), dim3(1024), 0, s, map, a.n, n_dev, b.chunk, src, dst, oks, okd); break;
-        }
+        (void)launch_unpartition(vb, map, a.n, n_dev, b.chunk, G, src, dst, oks, okd, s);
     };
     if (num_tiles > uint64_t(kFine)) {
         uint8_t* ok_tmp = ok_src ? reinterpret_cast<uint8_t*>(w.bin_lidx) : nullptr;
@@ -1999,12 +2013,7 @@ hipError_t launch_stage_finish(const TiledWs& w, StageSession& s, hipStream_t st
             if (Gu > 1024) Gu = 1024;
             if (Gu < 1) Gu = 1;
             const uint64_t chunk = (n + Gu - 1) / Gu;
-            switch (vb) {
-            case 1: hipLaunchKernelGGL((k_unpartition<1>), dim3(unsigned(Gu)), dim3(1024), 0, st, map, n, n_dev, chunk, src, dst, oks, okd); break;
-            case 2: hipLaunchKernelGGL((k_unpartition<2>), dim3(unsigned(Gu)), dim3(1024), 0, st, map, n, n_dev, chunk, src, dst, oks, okd); break;
-            case 4: hipLaunchKernelGGL((k_unpartition<4>), dim3(unsigned(Gu)), dim3(1024), 0, st, map, n, n_dev, chunk, src, dst, oks, okd); break;
-            default: hipLaunchKernelGGL((k_unpartition<8>), dim3(unsigned(Gu)), dim3(1024), 0, st, map, n, n_dev, chunk, src, dst, oks, okd); break;
-            }
+            (void)launch_unpartition(vb, map, n, n_dev, chunk, Gu, src, dst, oks, okd, st, 8);
         };
         for (int r = 0; r < s.nreg; r++) {
             const StageRegion& g = s.reg[r];

@@ -7,7 +7,7 @@ out=gpurun_out/$tag
 mkdir -p $out
 for cfg in "$@"; do
   timeout -k 10 300 python -u bench.py --config $cfg --steps 20 --warmup 5 --no-cpu-baseline > $out/bench_$cfg.json 2> $out/bench_$cfg.err || exit $?
-  timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $out/prof_$cfg -o run -- python3 bench.py --config $cfg --steps 10 --warmup 3 --no-cpu-baseline --no-verify > $out/prof_$cfg.log 2>&1 || exit $?
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats -f csv -d $out/prof_$cfg -o run -- python3 bench.py --config $cfg --steps 10 --warmup 3 --no-cpu-baseline --no-verify > $out/prof_$cfg.log 2>&1 || exit $?
 done
 for cfg in "$@"; do
   python3 - "$out/bench_$cfg.json" <<'PY'
