@@ -429,24 +429,26 @@ __global__ __launch_bounds__(1024) void k_fine_scatter(PartArgs p) {
         for (uint32_t r0 = lo; r0 < hi; r0 += kRound) {
             for (uint32_t f = threadIdx.x; f < nf; f += blockDim.x) hist[f] = 0;
             __syncthreads();
-            uint32_t m_rank[RPT], m_f[RPT];
-            bool m_ok[RPT];
+            // (tile, validity) recomputed from m_idx and the position: no per-record arrays
+            // beyond the ranks (51 -> 3 spilled VGPRs for 8-byte values; fine pass
+            // 0.546 -> 0.522 ms on C3, same box)
+            uint32_t m_rank[RPT];
 #pragma unroll
-            for (int j = 0; j < RPT; j++) {
-                m_ok[j] = r0 + uint32_t(j) * 1024 + threadIdx.x < hi;
-                m_f[j] = m_ok[j] ? (m_idx[j] >> p.tile_shift) - t0 : 0u;
-                if (m_ok[j]) m_rank[j] = atomicAdd(&hist[m_f[j]], 1u);
-            }
+            for (int j = 0; j < RPT; j++)
+                m_rank[j] = (r0 + uint32_t(j) * 1024 + threadIdx.x < hi)
+                                ? atomicAdd(&hist[(m_idx[j] >> p.tile_shift) - t0], 1u) : 0u;
             __syncthreads();
             small_excl_scan(hist, base, nf, &tot);
             __syncthreads();
 #pragma unroll
             for (int j = 0; j < RPT; j++) {
-                if (!m_ok[j]) continue;
-                const uint32_t q = base[m_f[j]] + m_rank[j];
+                const uint32_t k = r0 + uint32_t(j) * 1024 + threadIdx.x;
+                if (k >= hi) continue;
+                const uint32_t f = (m_idx[j] >> p.tile_shift) - t0;
+                const uint32_t q = base[f] + m_rank[j];
                 s_l[q] = uint16_t(m_idx[j] & lmask);
                 s_val[q] = m_val[j];
-                if (p.rpos) p.rpos[r0 + uint32_t(j) * 1024 + threadIdx.x] = cursor[m_f[j]] + m_rank[j];
+                if (p.rpos) p.rpos[k] = cursor[f] + m_rank[j];
             }
             if (r0 + kRound < hi) {
                 load_round(r0 + kRound, hi);
@@ -664,8 +666,8 @@ __global__ __launch_bounds__(NT) void k_fine_free(PartArgs p) {
             uint32_t m_rank[RPT];
 #pragma unroll
             for (int j = 0; j < RPT; j++)
-                if (r0 + uint32_t(j) * NT + threadIdx.x < hi)
-                    m_rank[j] = atomicAdd(&hist[(m_idx[j] >> p.tile_shift) - t0], 1u);
+                m_rank[j] = (r0 + uint32_t(j) * NT + threadIdx.x < hi)
+                                ? atomicAdd(&hist[(m_idx[j] >> p.tile_shift) - t0], 1u) : 0u;
             __syncthreads();
             small_excl_scan(hist, base, nf, &tot);
             __syncthreads();
