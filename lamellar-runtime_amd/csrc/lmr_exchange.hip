@@ -79,12 +79,18 @@ struct HostBuf {
 }  // namespace
 
 // Exchange state of a context: internal streams, events, grow-only buffers.
+// Streams: sp packs, sx runs every forward collective, sa stages and applies. Send and
+// receive buffers are double-buffered, so chunk j+1's pack overlaps chunk j's all-to-all-v
+// and chunk j-1's staging.
 struct XState {
-    hipStream_t sp = nullptr, sa = nullptr;
-    hipEvent_t ev_begin = nullptr, ev_hdr = nullptr, ev_x = nullptr, ev_pack_done = nullptr, ev_apply_done = nullptr;
-    hipEvent_t ev_recv_free[2] = {nullptr, nullptr};
-    bool recv_used[2] = {false, false};
-    DevBuf hdr_send, hdr_recv, counts, offsets, one_idx, send_idx, send_vals;
+    hipStream_t sp = nullptr, sx = nullptr, sa = nullptr;
+    hipEvent_t ev_begin = nullptr, ev_hdr = nullptr, ev_x = nullptr, ev_pack_done = nullptr, ev_apply_done = nullptr,
+               ev_x_done = nullptr;
+    hipEvent_t ev_recv_free[2] = {nullptr, nullptr}, ev_send_free[2] = {nullptr, nullptr},
+               ev_packed[2] = {nullptr, nullptr};
+    bool recv_used[2] = {false, false}, send_used[2] = {false, false};
+    DevBuf hdr_recv, counts, offsets, one_idx;
+    DevBuf hdr_send[2], send_idx[2], send_vals[2];
     DevBuf recv_idx[2], recv_vals[2];
     std::vector<DevBuf> pos, res, rok;   // per chunk (returning ops)
     DevBuf back, back_ok;
@@ -95,18 +101,21 @@ struct XState {
 void xstate_free(XState* x) {
     if (!x) return;
     (void)hipDeviceSynchronize();
-    for (DevBuf* b : {&x->hdr_send, &x->hdr_recv, &x->counts, &x->offsets, &x->one_idx, &x->send_idx, &x->send_vals,
-                      &x->recv_idx[0], &x->recv_idx[1], &x->recv_vals[0], &x->recv_vals[1], &x->back, &x->back_ok})
+    for (DevBuf* b : {&x->hdr_send[0], &x->hdr_send[1], &x->hdr_recv, &x->counts, &x->offsets, &x->one_idx,
+                      &x->send_idx[0], &x->send_idx[1], &x->send_vals[0], &x->send_vals[1], &x->recv_idx[0],
+                      &x->recv_idx[1], &x->recv_vals[0], &x->recv_vals[1], &x->back, &x->back_ok})
         b->release();
     for (auto* v : {&x->pos, &x->res, &x->rok})
         for (DevBuf& b : *v) b.release();
     x->h_hdr.release();
     x->h_send.release();
     x->h_recv.release();
-    for (hipEvent_t e : {x->ev_begin, x->ev_hdr, x->ev_x, x->ev_pack_done, x->ev_apply_done, x->ev_recv_free[0],
-                         x->ev_recv_free[1]})
+    for (hipEvent_t e : {x->ev_begin, x->ev_hdr, x->ev_x, x->ev_pack_done, x->ev_apply_done, x->ev_x_done,
+                         x->ev_recv_free[0], x->ev_recv_free[1], x->ev_send_free[0], x->ev_send_free[1],
+                         x->ev_packed[0], x->ev_packed[1]})
         if (e) (void)hipEventDestroy(e);
     if (x->sp) (void)hipStreamDestroy(x->sp);
+    if (x->sx) (void)hipStreamDestroy(x->sx);
     if (x->sa) (void)hipStreamDestroy(x->sa);
     delete x;
 }
@@ -114,9 +123,11 @@ void xstate_free(XState* x) {
 static hipError_t xstate_init(XState* x) {
     if (x->sp) return hipSuccess;
     hipError_t e = hipStreamCreateWithFlags(&x->sp, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&x->sx, hipStreamNonBlocking);
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&x->sa, hipStreamNonBlocking);
-    for (hipEvent_t* ev : {&x->ev_begin, &x->ev_hdr, &x->ev_x, &x->ev_pack_done, &x->ev_apply_done,
-                           &x->ev_recv_free[0], &x->ev_recv_free[1]})
+    for (hipEvent_t* ev : {&x->ev_begin, &x->ev_hdr, &x->ev_x, &x->ev_pack_done, &x->ev_apply_done, &x->ev_x_done,
+                           &x->ev_recv_free[0], &x->ev_recv_free[1], &x->ev_send_free[0], &x->ev_send_free[1],
+                           &x->ev_packed[0], &x->ev_packed[1]})
         if (e == hipSuccess) e = hipEventCreateWithFlags(ev, hipEventDisableTiming);
     return e;
 }
@@ -386,19 +397,22 @@ lmr_status_t lmr_batch_exchange(lmr_ctx_t* ctx, const lmr_transport_t* tp, const
     const uint64_t chunk = exchange_chunk();
     const uint64_t my_k = mvsi ? 1 : std::max<uint64_t>(1, (m + chunk - 1) / chunk);
     // --- buffers that do not depend on the chunk
-    if (x->hdr_send.need(size_t(npes) * LMR_XHDR_WORDS * 8) != hipSuccess ||
+    if (x->hdr_send[0].need(size_t(npes) * LMR_XHDR_WORDS * 8) != hipSuccess ||
+        x->hdr_send[1].need(size_t(npes) * LMR_XHDR_WORDS * 8) != hipSuccess ||
         x->hdr_recv.need(size_t(npes) * LMR_XHDR_WORDS * 8) != hipSuccess ||
         x->counts.need(size_t(npes) * 8) != hipSuccess || x->offsets.need(size_t(npes + 1) * 8) != hipSuccess ||
         x->h_hdr.need(size_t(2 * npes) * LMR_XHDR_WORDS * 8) != hipSuccess)
         return LMR_E_HIP;
     const uint64_t cmax = std::min<uint64_t>(m, chunk);
-    if (x->send_idx.need(cmax * iw + 8) != hipSuccess || x->send_vals.need(cmax * eb + 8) != hipSuccess)
-        return LMR_E_HIP;
+    for (int b = 0; b < 2; b++)
+        if (x->send_idx[b].need(cmax * iw + 8) != hipSuccess || x->send_vals[b].need(cmax * eb + 8) != hipSuccess)
+            return LMR_E_HIP;
     // --- both internal streams start after everything already on the caller's stream
     if (hipEventRecord(x->ev_begin, s0) != hipSuccess || hipStreamWaitEvent(x->sp, x->ev_begin, 0) != hipSuccess ||
-        hipStreamWaitEvent(x->sa, x->ev_begin, 0) != hipSuccess)
+        hipStreamWaitEvent(x->sx, x->ev_begin, 0) != hipSuccess || hipStreamWaitEvent(x->sa, x->ev_begin, 0) != hipSuccess)
         return LMR_E_HIP;
     x->recv_used[0] = x->recv_used[1] = false;
+    x->send_used[0] = x->send_used[1] = false;
     lmr_status_t st = lmr_stage_begin(ctx, desc);
     if (st != LMR_OK) return st;
     // a failed exchange closes the session (its staged records are dropped) so the
@@ -425,29 +439,36 @@ lmr_status_t lmr_batch_exchange(lmr_ctx_t* ctx, const lmr_transport_t* tp, const
         const uint64_t lo = std::min(m, j * chunk), hi = std::min(m, (j + 1) * chunk);
         const uint64_t cnt = hi - lo;
         if (returning && x->pos.size() <= j) x->pos.resize(j + 1);
-        // ---- pack this chunk by destination PE (pack stream)
+        const int b = int(j & 1);
+        // ---- pack this chunk by destination PE (pack stream) into send buffer b, once the
+        // all-to-all-v of chunk j-2 has read it
         const bool packed = !mvsi && j < my_k && cnt > 0;
+        if (x->send_used[b] && hipStreamWaitEvent(x->sp, x->ev_send_free[b], 0) != hipSuccess) return LMR_E_HIP;
         if (packed) {
             if (returning && x->pos[j].need(cnt * 4 + 8) != hipSuccess) return LMR_E_HIP;
             st = lmr_pack_unordered(ctx, layout, gidx + lo, cnt, scalar ? nullptr : static_cast<const uint8_t*>(d_vals) + lo * eb,
-                                    desc->dtype, iw, x->send_idx.p, scalar ? nullptr : x->send_vals.p,
+                                    desc->dtype, iw, x->send_idx[b].p, scalar ? nullptr : x->send_vals[b].p,
                                     returning ? x->pos[j].as<uint32_t>() : nullptr, x->counts.as<uint64_t>(),
                                     x->offsets.as<uint64_t>(), reinterpret_cast<lmr_stream_t>(x->sp));
             if (st != LMR_OK) return st;
         }
         hipLaunchKernelGGL(k_xhdr, dim3((npes + 255) / 256), dim3(256), 0, x->sp, packed ? x->counts.as<uint64_t>() : nullptr,
                            npes, mvsi && j == 0 ? mvsi_pe : -1, mvsi_off, int64_t(n), int64_t(scalar ? 1 : 0), sbits,
-                           int64_t(my_k), x->hdr_send.as<int64_t>());
+                           int64_t(my_k), x->hdr_send[b].as<int64_t>());
         if (hipGetLastError() != hipSuccess) return LMR_E_HIP;
-        st = tp_alltoall(tp, x, x->hdr_send.p, x->hdr_recv.p, LMR_XHDR_WORDS * 8, x->sp);
+        if (hipEventRecord(x->ev_packed[b], x->sp) != hipSuccess || hipStreamWaitEvent(x->sx, x->ev_packed[b], 0) != hipSuccess)
+            return LMR_E_HIP;
+        // ---- the exchange stream: header all-to-all, then the host reads this chunk's counts
+        // (one wait per chunk; the next chunk's pack is not enqueued yet, the previous
+        // chunk's staging runs meanwhile): sent rows, then received rows
+        st = tp_alltoall(tp, x, x->hdr_send[b].p, x->hdr_recv.p, LMR_XHDR_WORDS * 8, x->sx);
         if (st != LMR_OK) return st;
-        // the host needs this chunk's counts (one wait per chunk): sent rows, then received rows
-        if (hipMemcpyAsync(x->h_hdr.p, x->hdr_send.p, size_t(npes) * LMR_XHDR_WORDS * 8, hipMemcpyDeviceToHost,
-                           x->sp) != hipSuccess)
+        if (hipMemcpyAsync(x->h_hdr.p, x->hdr_send[b].p, size_t(npes) * LMR_XHDR_WORDS * 8, hipMemcpyDeviceToHost,
+                           x->sx) != hipSuccess)
             return LMR_E_HIP;
         if (hipMemcpyAsync(static_cast<int64_t*>(x->h_hdr.p) + size_t(npes) * LMR_XHDR_WORDS, x->hdr_recv.p,
-                           size_t(npes) * LMR_XHDR_WORDS * 8, hipMemcpyDeviceToHost, x->sp) != hipSuccess ||
-            hipEventRecord(x->ev_hdr, x->sp) != hipSuccess || hipEventSynchronize(x->ev_hdr) != hipSuccess)
+                           size_t(npes) * LMR_XHDR_WORDS * 8, hipMemcpyDeviceToHost, x->sx) != hipSuccess ||
+            hipEventRecord(x->ev_hdr, x->sx) != hipSuccess || hipEventSynchronize(x->ev_hdr) != hipSuccess)
             return LMR_E_HIP;
         const uint64_t k = lmr_exchange_plan(npes, iw, eb, h_send, h_recv, isb.data(), iso.data(), irb.data(),
                                              iro.data(), vsb.data(), vso.data(), vrb.data(), vro.data());
@@ -464,8 +485,7 @@ lmr_status_t lmr_batch_exchange(lmr_ctx_t* ctx, const lmr_transport_t* tp, const
             cr.total += cr.recv_cnt[p];
         }
         // ---- receive buffers of this chunk (double-buffered against the apply stream)
-        const int b = int(j & 1);
-        if (x->recv_used[b] && hipStreamWaitEvent(x->sp, x->ev_recv_free[b], 0) != hipSuccess) return LMR_E_HIP;
+        if (x->recv_used[b] && hipStreamWaitEvent(x->sx, x->ev_recv_free[b], 0) != hipSuccess) return LMR_E_HIP;
         const uint64_t ib = iro[npes - 1] + irb[npes - 1], vb = vro[npes - 1] + vrb[npes - 1];
         if (x->recv_idx[b].cap < ib + 8 || x->recv_vals[b].cap < vb + 8) {
             // growing frees the old buffer: nothing may still use it
@@ -473,14 +493,16 @@ lmr_status_t lmr_batch_exchange(lmr_ctx_t* ctx, const lmr_transport_t* tp, const
             if (x->recv_idx[b].need(ib + 8) != hipSuccess || x->recv_vals[b].need(vb + 8) != hipSuccess)
                 return LMR_E_HIP;
         }
-        const uint8_t* send_vals = mvsi ? static_cast<const uint8_t*>(d_vals) : x->send_vals.as<uint8_t>();
-        st = tp_alltoallv(tp, x, x->send_idx.p, isb.data(), iso.data(), x->recv_idx[b].p, irb.data(), iro.data(),
-                          unit_for(iw), x->sp);
+        const uint8_t* send_vals = mvsi ? static_cast<const uint8_t*>(d_vals) : x->send_vals[b].as<uint8_t>();
+        st = tp_alltoallv(tp, x, x->send_idx[b].p, isb.data(), iso.data(), x->recv_idx[b].p, irb.data(), iro.data(),
+                          unit_for(iw), x->sx);
         if (st == LMR_OK)
             st = tp_alltoallv(tp, x, send_vals, vsb.data(), vso.data(), x->recv_vals[b].p, vrb.data(), vro.data(),
-                              unit_for(eb), x->sp);
+                              unit_for(eb), x->sx);
         if (st != LMR_OK) return st;
-        if (hipEventRecord(x->ev_x, x->sp) != hipSuccess || hipStreamWaitEvent(x->sa, x->ev_x, 0) != hipSuccess)
+        if (hipEventRecord(x->ev_send_free[b], x->sx) != hipSuccess) return LMR_E_HIP;
+        x->send_used[b] = true;
+        if (hipEventRecord(x->ev_x, x->sx) != hipSuccess || hipStreamWaitEvent(x->sa, x->ev_x, 0) != hipSuccess)
             return LMR_E_HIP;
         // ---- owner side: stage every source's records (apply stream)
         if (returning) {
@@ -569,9 +591,11 @@ lmr_status_t lmr_batch_exchange(lmr_ctx_t* ctx, const lmr_transport_t* tp, const
             }
         }
     }
-    // ---- the caller's stream continues after both internal streams
-    if (hipEventRecord(x->ev_pack_done, x->sp) != hipSuccess || hipEventRecord(x->ev_apply_done, x->sa) != hipSuccess ||
-        hipStreamWaitEvent(s0, x->ev_pack_done, 0) != hipSuccess || hipStreamWaitEvent(s0, x->ev_apply_done, 0) != hipSuccess)
+    // ---- the caller's stream continues after the three internal streams
+    if (hipEventRecord(x->ev_pack_done, x->sp) != hipSuccess || hipEventRecord(x->ev_x_done, x->sx) != hipSuccess ||
+        hipEventRecord(x->ev_apply_done, x->sa) != hipSuccess ||
+        hipStreamWaitEvent(s0, x->ev_pack_done, 0) != hipSuccess || hipStreamWaitEvent(s0, x->ev_x_done, 0) != hipSuccess ||
+        hipStreamWaitEvent(s0, x->ev_apply_done, 0) != hipSuccess)
         return LMR_E_HIP;
     return LMR_OK;
 }

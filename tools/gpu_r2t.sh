@@ -1,0 +1,7 @@
+#!/bin/bash
+cd $GRAFT_REPO_ROOT
+mkdir -p gpurun_out
+export PYTHONUNBUFFERED=1
+timeout -k 10 600 python -u -m pytest tests/test_gpu_dist.py -x -q --timeout 300 --timeout-method thread > gpurun_out/r2t.log 2>&1 || { tail -30 gpurun_out/r2t.log; exit 1; }
+tail -1 gpurun_out/r2t.log
+timeout -k 10 600 bash tools/ab_mix.sh c4 2 "tools/abl/base.so|" "cur|"
