@@ -89,7 +89,7 @@ struct XState {
     hipEvent_t ev_recv_free[2] = {nullptr, nullptr}, ev_send_free[2] = {nullptr, nullptr},
                ev_packed[2] = {nullptr, nullptr};
     bool recv_used[2] = {false, false}, send_used[2] = {false, false};
-    DevBuf hdr_recv, counts, offsets, one_idx;
+    DevBuf hdr_recv, counts, offsets, one_idx, fill;
     DevBuf hdr_send[2], send_idx[2], send_vals[2];
     DevBuf recv_idx[2], recv_vals[2];
     std::vector<DevBuf> pos, res, rok;   // per chunk (returning ops)
@@ -101,7 +101,7 @@ struct XState {
 void xstate_free(XState* x) {
     if (!x) return;
     (void)hipDeviceSynchronize();
-    for (DevBuf* b : {&x->hdr_send[0], &x->hdr_send[1], &x->hdr_recv, &x->counts, &x->offsets, &x->one_idx,
+    for (DevBuf* b : {&x->hdr_send[0], &x->hdr_send[1], &x->hdr_recv, &x->counts, &x->offsets, &x->one_idx, &x->fill,
                       &x->send_idx[0], &x->send_idx[1], &x->send_vals[0], &x->send_vals[1], &x->recv_idx[0],
                       &x->recv_idx[1], &x->recv_vals[0], &x->recv_vals[1], &x->back, &x->back_ok})
         b->release();
@@ -173,15 +173,22 @@ lmr_status_t tp_alltoallv(const lmr_transport_t* tp, XState* x, const void* send
                           hipStream_t s) {
     if (!tp->host_buffers)
         return tp->alltoallv(tp->self, send, sb, so, recv, rb, ro, unit, reinterpret_cast<lmr_stream_t>(s));
+    // send segments are packed back to back into the host staging (a count-free pack leaves
+    // them in fixed regions); the callbacks see prefix offsets on both sides
+    std::vector<uint64_t> cso(tp->num_pes);
     uint64_t st_end = 0, rt_end = 0;
     for (uint32_t p = 0; p < tp->num_pes; p++) {
-        st_end = std::max(st_end, so[p] + sb[p]);
+        cso[p] = st_end;
+        st_end += sb[p];
         rt_end = std::max(rt_end, ro[p] + rb[p]);
     }
     if (x->h_send.need(st_end + 8) != hipSuccess || x->h_recv.need(rt_end + 8) != hipSuccess) return LMR_E_HIP;
-    if (st_end && hipMemcpyAsync(x->h_send.p, send, st_end, hipMemcpyDeviceToHost, s) != hipSuccess) return LMR_E_HIP;
+    for (uint32_t p = 0; p < tp->num_pes; p++)
+        if (sb[p] && hipMemcpyAsync(static_cast<uint8_t*>(x->h_send.p) + cso[p], static_cast<const uint8_t*>(send) + so[p],
+                                    sb[p], hipMemcpyDeviceToHost, s) != hipSuccess)
+            return LMR_E_HIP;
     if (hipStreamSynchronize(s) != hipSuccess) return LMR_E_HIP;
-    lmr_status_t st = tp->alltoallv(tp->self, x->h_send.p, sb, so, x->h_recv.p, rb, ro, unit,
+    lmr_status_t st = tp->alltoallv(tp->self, x->h_send.p, sb, cso.data(), x->h_recv.p, rb, ro, unit,
                                     reinterpret_cast<lmr_stream_t>(s));
     if (st != LMR_OK) return st;
     if (rt_end) return hs(hipMemcpyAsync(recv, x->h_recv.p, rt_end, hipMemcpyHostToDevice, s));
@@ -268,6 +275,11 @@ lmr_status_t rccl_alltoallv(void* self, const void* send, const uint64_t* sb, co
 
 bool valid_layout(const lmr_layout_t* L) {
     return L && L->num_pes > 0 && L->my_pe < L->num_pes && L->distribution <= 1 && L->orig_elem_per_pe > 0;
+}
+
+bool free_pack_enabled() {
+    const char* e = getenv("LAMELLAR_FREE_PACK");
+    return !(e && e[0] == '0');
 }
 
 uint64_t exchange_chunk() {
@@ -404,8 +416,17 @@ lmr_status_t lmr_batch_exchange(lmr_ctx_t* ctx, const lmr_transport_t* tp, const
         x->h_hdr.need(size_t(2 * npes) * LMR_XHDR_WORDS * 8) != hipSuccess)
         return LMR_E_HIP;
     const uint64_t cmax = std::min<uint64_t>(m, chunk);
+    // nothing returned: the count-free pack (fixed per-PE regions, no count pass); a chunk
+    // whose records overflow a region is packed again with the counted pack
+    const bool free_pack = !returning && npes <= 512 && free_pack_enabled();
+    auto region_cap = [&](uint64_t c) -> uint64_t {
+        const uint64_t q = (c + npes - 1) / npes;
+        return q + q / 8 + 4096;
+    };
+    const uint64_t send_recs = free_pack ? std::max<uint64_t>(cmax, uint64_t(npes) * region_cap(cmax)) : cmax;
+    if (free_pack && (send_recs > 0xFFFFFFFFull || x->fill.need(size_t(npes) * 4 + 8) != hipSuccess)) return LMR_E_HIP;
     for (int b = 0; b < 2; b++)
-        if (x->send_idx[b].need(cmax * iw + 8) != hipSuccess || x->send_vals[b].need(cmax * eb + 8) != hipSuccess)
+        if (x->send_idx[b].need(send_recs * iw + 8) != hipSuccess || x->send_vals[b].need(send_recs * eb + 8) != hipSuccess)
             return LMR_E_HIP;
     // --- both internal streams start after everything already on the caller's stream
     if (hipEventRecord(x->ev_begin, s0) != hipSuccess || hipStreamWaitEvent(x->sp, x->ev_begin, 0) != hipSuccess ||
@@ -444,13 +465,36 @@ lmr_status_t lmr_batch_exchange(lmr_ctx_t* ctx, const lmr_transport_t* tp, const
         // all-to-all-v of chunk j-2 has read it
         const bool packed = !mvsi && j < my_k && cnt > 0;
         if (x->send_used[b] && hipStreamWaitEvent(x->sp, x->ev_send_free[b], 0) != hipSuccess) return LMR_E_HIP;
+        const uint32_t cap = uint32_t(free_pack ? region_cap(cnt) : 0);
+        auto counted_pack = [&]() -> lmr_status_t {
+            return lmr_pack_unordered(ctx, layout, gidx + lo, cnt, scalar ? nullptr : static_cast<const uint8_t*>(d_vals) + lo * eb,
+                                      desc->dtype, iw, x->send_idx[b].p, scalar ? nullptr : x->send_vals[b].p,
+                                      returning ? x->pos[j].as<uint32_t>() : nullptr, x->counts.as<uint64_t>(),
+                                      x->offsets.as<uint64_t>(), reinterpret_cast<lmr_stream_t>(x->sp));
+        };
         if (packed) {
             if (returning && x->pos[j].need(cnt * 4 + 8) != hipSuccess) return LMR_E_HIP;
-            st = lmr_pack_unordered(ctx, layout, gidx + lo, cnt, scalar ? nullptr : static_cast<const uint8_t*>(d_vals) + lo * eb,
-                                    desc->dtype, iw, x->send_idx[b].p, scalar ? nullptr : x->send_vals[b].p,
-                                    returning ? x->pos[j].as<uint32_t>() : nullptr, x->counts.as<uint64_t>(),
-                                    x->offsets.as<uint64_t>(), reinterpret_cast<lmr_stream_t>(x->sp));
-            if (st != LMR_OK) return st;
+            if (free_pack) {
+                PackArgs pa;
+                pa.layout = *layout;
+                pa.gidx = gidx + lo;
+                pa.vals = scalar ? nullptr : static_cast<const uint8_t*>(d_vals) + lo * eb;
+                pa.val_bytes = eb;
+                pa.n = cnt;
+                pa.index_size = iw;
+                pa.out_idx = x->send_idx[b].as<uint8_t>();
+                pa.out_vals = scalar ? nullptr : x->send_vals[b].as<uint8_t>();
+                pa.out_pos = nullptr;
+                pa.dest_counts = x->counts.as<uint64_t>();
+                pa.dest_offsets = nullptr;
+                pa.err = ctx->d_err;
+                pa.prof = ctx->prof;
+                pa.stable = false;
+                if (launch_pack_free(pa, x->fill.as<uint32_t>(), cap, x->sp) != hipSuccess) return LMR_E_HIP;
+            } else {
+                st = counted_pack();
+                if (st != LMR_OK) return st;
+            }
         }
         hipLaunchKernelGGL(k_xhdr, dim3((npes + 255) / 256), dim3(256), 0, x->sp, packed ? x->counts.as<uint64_t>() : nullptr,
                            npes, mvsi && j == 0 ? mvsi_pe : -1, mvsi_off, int64_t(n), int64_t(scalar ? 1 : 0), sbits,
@@ -473,6 +517,22 @@ lmr_status_t lmr_batch_exchange(lmr_ctx_t* ctx, const lmr_transport_t* tp, const
         const uint64_t k = lmr_exchange_plan(npes, iw, eb, h_send, h_recv, isb.data(), iso.data(), irb.data(),
                                              iro.data(), vsb.data(), vso.data(), vrb.data(), vro.data());
         if (j == 0) nchunks = std::max<uint64_t>(k, 1);
+        if (packed && free_pack) {
+            bool over = false;
+            for (uint32_t p = 0; p < npes; p++) over = over || h_send[p * LMR_XHDR_WORDS] > int64_t(cap);
+            if (over) {                                 // same counts, contiguous layout: the plan's offsets
+                st = counted_pack();
+                if (st != LMR_OK) return st;
+                if (hipEventRecord(x->ev_packed[b], x->sp) != hipSuccess ||
+                    hipStreamWaitEvent(x->sx, x->ev_packed[b], 0) != hipSuccess)
+                    return LMR_E_HIP;
+            } else {                                    // sends start at each PE's region
+                for (uint32_t p = 0; p < npes; p++) {
+                    iso[p] = uint64_t(p) * cap * iw;
+                    vso[p] = uint64_t(p) * cap * eb;
+                }
+            }
+        }
         ChunkRec cr;
         cr.lo = mvsi ? 0 : lo;
         cr.hi = mvsi ? n : hi;

@@ -183,6 +183,9 @@ struct PackArgs {
 };
 hipError_t launch_pack(const PackArgs& a, uint32_t* counts, uint32_t* partials, uint32_t* total,
                        hipStream_t s);
+// count-free unordered pack into fixed per-destination regions of `cap` records (nothing
+// returned; dest_counts[i] > cap: region i overflowed, pack again with launch_pack)
+hipError_t launch_pack_free(const PackArgs& a, uint32_t* fill, uint32_t cap, hipStream_t s);
 constexpr int kReduceBlocks = 1024;
 hipError_t launch_reduce(int dtype, int op, const void* x, uint64_t n, uint64_t* out, uint8_t* has,
                          void* part, uint8_t* part_has, hipStream_t s);

@@ -38,6 +38,8 @@ struct PackK {
     uint8_t* out_vals;
     uint32_t* out_pos;
     uint32_t* err;
+    uint32_t* fill;         // count-free pack: records reserved in each destination's region
+    uint32_t cap;           // count-free pack: records per destination region
 };
 
 // Wave-aggregated LDS counting: one atomic per distinct key in the wave instead
@@ -227,7 +229,11 @@ __device__ __forceinline__ void stage_scan(const uint32_t* hist, uint32_t* base,
     if (t < m) base[t] = inc - x + wsum[w];
 }
 
-template <int IW, int VB, int RPT, int MODE>
+// FREE: no count pass. Destination i owns the region [i * cap, (i + 1) * cap) of the output;
+// each round reserves its run per destination with one atomicAdd on fill[i]. A round that
+// would overflow a region writes nothing (fill[i] still counts every record, so the caller
+// sees a count above cap and packs the chunk again with the counted pack).
+template <int IW, int VB, int RPT, int MODE, bool FREE>
 __global__ __launch_bounds__(1024) void k_pack_stage(PackK p) {
     using I = typename idx_t<IW>::I;
     using V = typename idx_t<VB>::I;
@@ -238,7 +244,9 @@ __global__ __launch_bounds__(1024) void k_pack_stage(PackK p) {
     __shared__ uint32_t s_pos[kRound];
     const uint32_t np = p.npes;
     const int bits = key_bits(np);
-    for (uint32_t i = threadIdx.x; i < np; i += blockDim.x) cursor[i] = p.counts[uint64_t(i) * p.G + blockIdx.x];
+    __shared__ uint32_t s_over;
+    if constexpr (!FREE)
+        for (uint32_t i = threadIdx.x; i < np; i += blockDim.x) cursor[i] = p.counts[uint64_t(i) * p.G + blockIdx.x];
     const uint64_t lo = uint64_t(blockIdx.x) * p.chunk;
     const uint64_t hi = min(lo + p.chunk, p.n);
     const V* vals = reinterpret_cast<const V*>(p.vals);
@@ -256,6 +264,7 @@ __global__ __launch_bounds__(1024) void k_pack_stage(PackK p) {
     load_round(lo);
     for (uint64_t r0 = lo; r0 < hi; r0 += kRound) {
         for (uint32_t i = threadIdx.x; i < np; i += blockDim.x) hist[i] = 0;
+        if (FREE && threadIdx.x == 0) s_over = 0;
         __syncthreads();
         uint32_t m_rank[RPT], m_pe[RPT];
         uint64_t m_off[RPT];
@@ -269,6 +278,14 @@ __global__ __launch_bounds__(1024) void k_pack_stage(PackK p) {
         }
         __syncthreads();
         stage_scan(hist, base, np);
+        if constexpr (FREE) {
+            for (uint32_t i = threadIdx.x; i < np; i += blockDim.x) {
+                const uint32_t h = hist[i];
+                const uint32_t r = h ? atomicAdd(&p.fill[i], h) : 0u;
+                if (uint64_t(r) + h > p.cap) s_over = 1;
+                cursor[i] = i * p.cap + r;
+            }
+        }
         __syncthreads();
 #pragma unroll
         for (int j = 0; j < RPT; j++) {
@@ -280,14 +297,21 @@ __global__ __launch_bounds__(1024) void k_pack_stage(PackK p) {
         }
         if (r0 + kRound < hi) load_round(r0 + kRound);
         __syncthreads();
-        bucket_writeout(hist, base, cursor, np, [&](uint32_t q, uint32_t dst) {
-            reinterpret_cast<I*>(p.out_idx)[dst] = s_off[q];
-            if (vals) reinterpret_cast<V*>(p.out_vals)[dst] = s_val[q];
-            if (p.out_pos) p.out_pos[dst] = s_pos[q];
-        });
+        if (!FREE || !s_over)
+            bucket_writeout(hist, base, cursor, np, [&](uint32_t q, uint32_t dst) {
+                reinterpret_cast<I*>(p.out_idx)[dst] = s_off[q];
+                if (vals) reinterpret_cast<V*>(p.out_vals)[dst] = s_val[q];
+                if (p.out_pos) p.out_pos[dst] = s_pos[q];
+            });
         __syncthreads();
-        for (uint32_t i = threadIdx.x; i < np; i += blockDim.x) cursor[i] += hist[i];
+        if constexpr (!FREE)
+            for (uint32_t i = threadIdx.x; i < np; i += blockDim.x) cursor[i] += hist[i];
     }
+}
+
+__global__ void k_fill_counts(const uint32_t* fill, uint32_t npes, uint64_t* dest_counts) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < npes) dest_counts[i] = fill[i];
 }
 
 __global__ void k_dest_offsets(const uint32_t* counts, uint32_t npes, uint32_t G, const uint32_t* total,
@@ -360,7 +384,7 @@ hipError_t launch_pack(const PackArgs& a, uint32_t* counts, uint32_t* partials, 
                 by_mode([&](auto m) {
                     constexpr int IWc = decltype(iw)::value, VBc = decltype(vb)::value;
                     constexpr int RP = (IWc + VBc + 4) * 8 <= 150 ? 8 : 4;      // rounds of RP * 1024 records in LDS
-                    hipLaunchKernelGGL((k_pack_stage<IWc, VBc, RP, decltype(m)::value>),
+                    hipLaunchKernelGGL((k_pack_stage<IWc, VBc, RP, decltype(m)::value, false>),
                                        dim3(unsigned(G)), dim3(1024), 0, s, p);
                 });
             });
@@ -373,6 +397,43 @@ hipError_t launch_pack(const PackArgs& a, uint32_t* counts, uint32_t* partials, 
     }
     hipLaunchKernelGGL(k_dest_offsets, dim3((npes + 1 + 255) / 256), dim3(256),
                        0, s, counts, npes, uint32_t(G), total, a.dest_offsets, a.dest_counts);
+    return hipGetLastError();
+}
+
+// Count-free unordered pack (nothing returned): destination i's records land in
+// [i * cap, i * cap + dest_counts[i]) of out_idx / out_vals. dest_counts[i] > cap means
+// the region overflowed and the output is incomplete (pack again with launch_pack).
+hipError_t launch_pack_free(const PackArgs& a, uint32_t* fill, uint32_t cap, hipStream_t s) {
+    const uint32_t npes = a.layout.num_pes;
+    if (npes == 0 || npes > kStageMaxPes || a.out_pos || a.stable) return hipErrorInvalidValue;
+    uint64_t G = (a.n + 65535) / 65536;
+    if (G > uint64_t(kMaxBinBlocks)) G = kMaxBinBlocks;
+    if (G < 1) G = 1;
+    PackK p;
+    p.L = a.layout; p.F = make_fast_layout(a.layout); p.gidx = a.gidx; p.vals = a.vals; p.vb = a.val_bytes; p.n = a.n;
+    p.iw = a.index_size; p.chunk = (a.n + G - 1) / G; if (p.chunk == 0) p.chunk = 1;
+    p.G = uint32_t(G); p.npes = npes; p.counts = nullptr;
+    p.out_idx = a.out_idx; p.out_vals = a.out_vals; p.out_pos = nullptr; p.err = a.err;
+    p.fill = fill; p.cap = cap;
+    ProfScope ps(a.prof, LMR_STAGE_PACK, s, a.n);
+    hipError_t e = hipMemsetAsync(fill, 0, size_t(npes) * 4, s);
+    if (e != hipSuccess) return e;
+    if (a.n > 0) {
+        const int mode = layout_map_mode(a.layout);
+        const int vbk = a.vals ? int(a.val_bytes) : 1;
+        dispatch_pack_stage(int(a.index_size), vbk, [&](auto iw, auto vb) {
+            constexpr int IWc = decltype(iw)::value, VBc = decltype(vb)::value;
+            constexpr int RP = (IWc + VBc + 4) * 8 <= 150 ? 8 : 4;
+            if (mode == LMR_MAP_BLOCK)
+                hipLaunchKernelGGL((k_pack_stage<IWc, VBc, RP, LMR_MAP_BLOCK, true>), dim3(unsigned(G)), dim3(1024), 0, s, p);
+            else if (mode == LMR_MAP_CYCLIC)
+                hipLaunchKernelGGL((k_pack_stage<IWc, VBc, RP, LMR_MAP_CYCLIC, true>), dim3(unsigned(G)), dim3(1024), 0, s, p);
+            else
+                hipLaunchKernelGGL((k_pack_stage<IWc, VBc, RP, LMR_MAP_GENERIC, true>), dim3(unsigned(G)), dim3(1024), 0, s,
+                                   p);
+        });
+    }
+    hipLaunchKernelGGL(k_fill_counts, dim3((npes + 255) / 256), dim3(256), 0, s, fill, npes, a.dest_counts);
     return hipGetLastError();
 }
 

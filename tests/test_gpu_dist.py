@@ -34,6 +34,12 @@ gi = rng.integers(0, n_len, 200000).astype(np.uint64)
 gv = rng.integers(0, 2**40, gi.size).astype(np.uint64)
 arr.batch_add(gi, gv).block(); world.barrier()
 out["after_add"] = arr.to_numpy()
+# skewed: every record to the first quarter of the array (one PE under Block): the
+# count-free pack's per-PE region overflows and the chunk is packed again, counted
+si = rng.integers(0, n_len // 4, 150000).astype(np.uint64)
+arr.batch_add(si, 3).block(); world.barrier()
+arr.batch_sub(si, 3).block(); world.barrier()
+out["after_skew"] = arr.to_numpy()
 fi = rng.permutation(n_len)[:20000].astype(np.uint64)
 olds = arr.batch_fetch_add(fi, 7).block(); world.barrier()
 out["fetch_olds"] = olds.cpu().numpy().view(np.uint64)
@@ -72,6 +78,7 @@ def _check(orc, outdir, ws, dist_kind):
     exp = a.to_numpy()
     for r in range(ws):
         assert np.array_equal(pe[r]["after_add"], exp)
+        assert np.array_equal(pe[r]["after_skew"], exp)       # +3 then -3 per skewed record
     cnt = np.zeros(exp.size, np.uint64)
     for r in range(ws):
         cnt[pe[r]["fi"].astype(np.int64)] += np.uint64(1)
