@@ -53,7 +53,7 @@ def parse():
     p.add_argument("--elems-log2", type=int, default=None)
     p.add_argument("--strategy", default=os.environ.get("LAMELLAR_OP_STRATEGY", "auto"))
     p.add_argument("--cpu-threads", type=int, default=0, help="0: every core this process may run on")
-    p.add_argument("--cpu-sample-log2", type=int, default=24)
+    p.add_argument("--cpu-sample-log2", type=int, default=25)
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-verify", action="store_true")
     p.add_argument("--e2e", action="store_true",
