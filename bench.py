@@ -426,6 +426,7 @@ def main():
     t0 = time.perf_counter()
     for _ in range(args.steps):
         W.step()
+    world.wait_all()              # every issued batch applied (deferred ones included)
     torch.cuda.synchronize(dev)
     world.barrier()
     t1 = time.perf_counter()

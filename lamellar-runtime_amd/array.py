@@ -245,7 +245,14 @@ class LamellarArray:
         return int(_capi.lib().lmr_index_size(ctypes.byref(self.layout)))
 
     def local_shard(self):
-        """Device tensor of this PE's local slice (UnsafeArray::local_as_mut_slice)."""
+        """Device tensor of this PE's local slice (UnsafeArray::local_as_mut_slice), with every
+        batch issued so far applied (stream-ordered)."""
+        flush = getattr(self.team.kernels, "flush", None)
+        if flush is not None:
+            flush()
+        return self._shard_view()
+
+    def _shard_view(self):
         start = int(_capi.lib().lmr_local_slice_start(ctypes.byref(self.layout), self.team.my_pe()))
         n = self.num_elems_local()
         if n == 0:

@@ -718,6 +718,12 @@ constexpr uint32_t kSplit = 16 * 1024;     // records per delta item (16 per thr
 
 struct TileItem { uint32_t tile, lo, hi, mode; };
 
+// a mixed staged session's per-region op (k_tile_owner applies region rg's records with rop[rg])
+struct RegionOp {
+    int32_t op, ret;
+    uint64_t cmp_bits, eps_bits;
+};
+
 __global__ void k_tile_plan_count(const uint32_t* tile_start, uint32_t num_tiles, uint32_t thresh,
                                   int combinable, uint32_t* tile_items) {
     const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
@@ -774,6 +780,10 @@ struct TileArgs {
     const uint32_t* rts;
     uint32_t nreg;
     uint32_t rstride;
+    // mixed session (regions of different ops / operands): region rg applied with rop[rg], every
+    // region of the tile after the previous one (staging order per element)
+    int mixed;
+    RegionOp rop[kMaxRegions];
 };
 
 __host__ __device__ constexpr bool op_combines(int op) {
@@ -833,10 +843,10 @@ __global__ __launch_bounds__(1024, 8) void k_tile_owner(TileArgs a) {
     if (w.mode != 0) return;
     const uint16_t* bin_lidx = a.bin_lidx;
     const T* bin_val = reinterpret_cast<const T*>(a.bin_val);
-    const int op = OPT >= 0 ? OPT : a.op;
-    const T cmp = from_bits<T>(U(a.cmp_bits)), eps = from_bits<T>(U(a.eps_bits));
+    int op = OPT >= 0 ? OPT : a.op;
+    T cmp = from_bits<T>(U(a.cmp_bits)), eps = from_bits<T>(U(a.eps_bits));
     const T sv = from_bits<T>(U(a.val_bits));
-    const int ret = a.ret;
+    int ret = a.ret;
     const uint64_t base = uint64_t(w.tile) << a.tile_shift;
     const uint32_t len = uint32_t(min(uint64_t(1) << a.tile_shift, a.shard_len - base));
     T* shard = reinterpret_cast<T*>(a.shard) + base;
@@ -865,6 +875,13 @@ __global__ __launch_bounds__(1024, 8) void k_tile_owner(TileArgs a) {
         lo = a.rts[uint64_t(rg) * a.rstride + w.tile];
         hi = a.rts[uint64_t(rg) * a.rstride + w.tile + 1];
     }
+    if (OPT < 0 && a.mixed) {          // the region's op; its records after every earlier region's
+        op = a.rop[rg].op;
+        ret = a.rop[rg].ret;
+        cmp = from_bits<T>(U(a.rop[rg].cmp_bits));
+        eps = from_bits<T>(U(a.rop[rg].eps_bits));
+        if (rg) __syncthreads();
+    }
     for (uint32_t r0 = lo + threadIdx.x; r0 < hi; r0 += kOwnUnroll * 1024u) {
         uint32_t l[kOwnUnroll];
         T v[kOwnUnroll];
@@ -891,7 +908,7 @@ __global__ __launch_bounds__(1024, 8) void k_tile_owner(TileArgs a) {
     }
     }
     __syncthreads();
-    if (!op_is_read(op)) {
+    if (!op_is_read(op) || (OPT < 0 && a.mixed)) {
         if constexpr (sizeof(T) >= 4) {
             if (vec) {
                 constexpr uint32_t per = 16 / sizeof(T);
@@ -1385,7 +1402,7 @@ static hipError_t launch_tile_sweep(int dtype, const ApplyArgs& a, const TiledWs
     t.num_tiles = T;
     t.bin_lidx = w.bin_lidx; t.bin_val = w.bin_val;
     t.results = res_bin; t.ok = ok_bin; t.err = a.err;
-    t.rts = nullptr; t.nreg = 0; t.rstride = 0;
+    t.rts = nullptr; t.nreg = 0; t.rstride = 0; t.mixed = 0;
     const bool delta = op_combines(a.op) && n > thresh;
     const unsigned dgrid = unsigned(std::min<uint64_t>(2 * ((n + kSplit - 1) / kSplit), uint64_t(tile_grid_cap())));
     return dispatch_dtype(dtype, [&](auto tag) {
@@ -1847,7 +1864,7 @@ static hipError_t stage_region_free(int dtype, int index_size, const ApplyArgs& 
         e = launch_coarse_free(index_size, vb, frpt, q, st);
     }
     if (e != hipSuccess) return e;
-    s.reg[s.nreg] = StageRegion{0, a.n, nullptr, nullptr};
+    s.reg[s.nreg] = StageRegion{0, a.n, nullptr, nullptr, a.op, LMR_RET_NONE, a.cmp_bits, a.eps_bits};
     s.nreg += 1;
     s.staged += a.n;
     return hipSuccess;
@@ -1879,7 +1896,7 @@ hipError_t launch_stage_region(int dtype, int index_size, const ApplyArgs& a, co
     const int vb = dtype_bytes(dtype);
     const int r = s.nreg;
     const uint32_t R = uint32_t(s.staged);
-    const bool has_res = s.a.ret != LMR_RET_NONE;
+    const bool has_res = a.ret != LMR_RET_NONE;
     uint64_t G = (a.n + 65535) / 65536;
     if (G > uint64_t(bin_blocks_cap(vb))) G = bin_blocks_cap(vb);
     if (G < 1) G = 1;
@@ -1945,7 +1962,7 @@ hipError_t launch_stage_region(int dtype, int index_size, const ApplyArgs& a, co
         e = hipGetLastError();
     }
     if (e != hipSuccess) return e;
-    s.reg[r] = StageRegion{uint64_t(R), a.n, a.results, a.ok};
+    s.reg[r] = StageRegion{uint64_t(R), a.n, a.results, a.ok, a.op, a.ret, a.cmp_bits, a.eps_bits};
     s.nreg = r + 1;
     s.staged += a.n;
     return hipSuccess;
@@ -1954,7 +1971,15 @@ hipError_t launch_stage_region(int dtype, int index_size, const ApplyArgs& a, co
 hipError_t launch_stage_finish(const TiledWs& w, StageSession& s, hipStream_t st) {
     if (s.nreg == 0) return hipSuccess;
     if (s.free) return stage_finish_free(w, s, st);
-    const ApplyArgs& a = s.a;
+    // the regions' op: every region's, or per region (mixed: op phases in staging order)
+    ApplyArgs a = s.a;
+    a.op = s.reg[0].op; a.ret = s.reg[0].ret; a.cmp_bits = s.reg[0].cmp_bits; a.eps_bits = s.reg[0].eps_bits;
+    bool mixed = false;
+    for (int r = 1; r < s.nreg; r++)
+        mixed = mixed || s.reg[r].op != a.op || s.reg[r].cmp_bits != a.cmp_bits || s.reg[r].eps_bits != a.eps_bits;
+    for (int r = 1; r < s.nreg; r++)
+        if (s.reg[r].ret != LMR_RET_NONE && (a.ret == LMR_RET_NONE || s.reg[r].ret == LMR_RET_RESULT))
+            a.ret = s.reg[r].ret;                                 // maps kept if any region returns
     const int dtype = s.dtype;
     const int shift = tile_shift_for(dtype);
     const uint32_t T = uint32_t((a.shard_len + (uint64_t(1) << shift) - 1) >> shift);
@@ -1970,7 +1995,7 @@ hipError_t launch_stage_finish(const TiledWs& w, StageSession& s, hipStream_t st
         const uint32_t thresh = uint32_t(std::min<uint64_t>(0xFFFFFFFFull, std::max<uint64_t>(4 * avg, 65536)));
         const unsigned pg = unsigned((T + 255) / 256);
         hipLaunchKernelGGL(k_stage_plan_count, dim3(pg), dim3(256), 0, st, w.rts, uint32_t(s.nreg), stride, T,
-                           thresh, op_combines(a.op) ? 1 : 0, w.tile_items);
+                           thresh, (!mixed && op_combines(a.op)) ? 1 : 0, w.tile_items);
         hipLaunchKernelGGL(k_tile_plan_extra, dim3(pg), dim3(256), 0, st, w.tile_items, T, w.tile_items2);
         e = scan_exclusive_u32(w.tile_items2, T, w.plan_partials, w.item_count, st);
         if (e != hipSuccess) return e;
@@ -1987,7 +2012,11 @@ hipError_t launch_stage_finish(const TiledWs& w, StageSession& s, hipStream_t st
         t.bin_lidx = w.bin_lidx; t.bin_val = w.bin_val;
         t.results = res_bin; t.ok = ok_bin; t.err = a.err;
         t.rts = w.rts; t.nreg = uint32_t(s.nreg); t.rstride = stride;
-        const bool delta = op_combines(a.op) && s.staged > thresh;
+        t.mixed = mixed ? 1 : 0;
+        for (int r = 0; r < s.nreg; r++)
+            t.rop[r] = RegionOp{s.reg[r].op, s.reg[r].ret, s.reg[r].cmp_bits, s.reg[r].eps_bits};
+        // delta mode needs one combinable op; a mixed session's hot tiles stay with their owner
+        const bool delta = !mixed && op_combines(a.op) && s.staged > thresh;
         const unsigned dgrid = unsigned(std::min<uint64_t>(2 * ((s.staged + kSplit - 1) / kSplit) + 2 * uint64_t(s.nreg),
                                                            uint64_t(tile_grid_cap())));
         e = dispatch_dtype(dtype, [&](auto tag) {
@@ -1997,8 +2026,8 @@ hipError_t launch_stage_finish(const TiledWs& w, StageSession& s, hipStream_t st
                 hipLaunchKernelGGL((k_tile_owner<Ty, OPT>), dim3(T), dim3(1024), size_t(kTileBytes), st, t);
                 if (delta) hipLaunchKernelGGL((k_tile_delta<Ty, OPT>), dim3(dgrid), dim3(1024), size_t(kTileBytes), st, t);
             };
-            if (a.op == LMR_OP_ADD) go(std::integral_constant<int, LMR_OP_ADD>{});
-            else if (a.op == LMR_OP_FETCH_ADD) go(std::integral_constant<int, LMR_OP_FETCH_ADD>{});
+            if (!mixed && a.op == LMR_OP_ADD) go(std::integral_constant<int, LMR_OP_ADD>{});
+            else if (!mixed && a.op == LMR_OP_FETCH_ADD) go(std::integral_constant<int, LMR_OP_FETCH_ADD>{});
             else go(std::integral_constant<int, -1>{});
             return hipGetLastError();
         });
@@ -2007,8 +2036,8 @@ hipError_t launch_stage_finish(const TiledWs& w, StageSession& s, hipStream_t st
         // binned -> temp slot (in-bounds slots of each region) -> arrival order
         ProfScope pu(a.prof, LMR_STAGE_UNPARTITION, st, s.staged);
         uint8_t* tmpres = w.bin_val;                              // bins are free after the tile sweep
-        uint8_t* ok_tmp = (a.ret == LMR_RET_RESULT) ? reinterpret_cast<uint8_t*>(w.bin_lidx) : nullptr;
-        const uint8_t* ok_src = (a.ret == LMR_RET_RESULT) ? ok_bin : nullptr;
+        uint8_t* ok_tmp_all = (a.ret == LMR_RET_RESULT) ? reinterpret_cast<uint8_t*>(w.bin_lidx) : nullptr;
+        const uint8_t* ok_src_all = (a.ret == LMR_RET_RESULT) ? ok_bin : nullptr;
         auto gather = [&](const uint32_t* map, uint64_t n, const uint32_t* n_dev, const uint8_t* src, uint8_t* dst,
                           const uint8_t* oks, uint8_t* okd) {
             uint64_t Gu = (n + 65535) / 65536;
@@ -2019,7 +2048,9 @@ hipError_t launch_stage_finish(const TiledWs& w, StageSession& s, hipStream_t st
         };
         for (int r = 0; r < s.nreg; r++) {
             const StageRegion& g = s.reg[r];
-            if (!g.results) continue;
+            if (!g.results || g.ret == LMR_RET_NONE) continue;
+            uint8_t* ok_tmp = g.ret == LMR_RET_RESULT ? ok_tmp_all : nullptr;
+            const uint8_t* ok_src = g.ret == LMR_RET_RESULT ? ok_src_all : nullptr;
             gather(w.rpos + g.base, g.n, w.sinfo + kStageInb + r, res_bin, tmpres + g.base * vb, ok_src,
                    ok_tmp ? ok_tmp + g.base : nullptr);
             const bool want_ok = ok_tmp && g.ok;

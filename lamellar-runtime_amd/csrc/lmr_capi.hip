@@ -52,6 +52,11 @@ void stage_abort(StageState* s) {
     s->open = false;
     s->s = StageSession();
 }
+bool stage_pending_other_op(const StageSession& s, const ApplyArgs& a) {
+    for (int r = 0; r < s.nreg; r++)
+        if (s.reg[r].op != a.op || s.reg[r].cmp_bits != a.cmp_bits || s.reg[r].eps_bits != a.eps_bits) return true;
+    return false;
+}
 }  // namespace lmr
 
 using namespace lmr;
@@ -669,9 +674,45 @@ lmr_status_t lmr_stage_soa(lmr_ctx_t* ctx, const void* d_indices, uint32_t index
     const bool tiled = ctx->ws && ctx->rec_cap > 0 && d->strategy != LMR_STRATEGY_DIRECT &&
                        tiled_supported(int(d->dtype), d->shard_len) &&
                        !(d->strategy == LMR_STRATEGY_AUTO && n < 65536);
-    if (!tiled) return run_apply(ctx, d, a, int(index_size), s);      // small stream: applied now
+    if (!tiled) {                                                     // small stream: applied now,
+        if (S->s.nreg > 0 && stage_pending_other_op(S->s, a)) {      // after earlier op phases
+            const hipError_t e = launch_stage_finish(carve_tiled_ws(ctx->ws, ctx->rec_cap), S->s, s);
+            if (e != hipSuccess) return hip_status(e);
+        }
+        return run_apply(ctx, d, a, int(index_size), s);
+    }
     a.ret = S->s.a.ret;
     return hip_status(stage_records(ctx, S->s, a, int(d->dtype), int(index_size), 1, s));
+}
+
+lmr_status_t lmr_stage_op(lmr_ctx_t* ctx, uint32_t op, uint64_t cmp_bits, uint64_t eps_bits, lmr_stream_t stream) {
+    if (!ctx || !ctx->stage || !ctx->stage->open) return LMR_E_INVALID;
+    StageState* S = ctx->stage;
+    lmr_apply_desc_t d = S->desc;
+    d.op = op;
+    d.cmp_bits = cmp_bits;
+    d.eps_bits = eps_bits;
+    lmr_status_t st = check_desc(&d);
+    if (st != LMR_OK) return st;
+    const lmr_apply_desc_t& c = S->desc;
+    if (c.op == op && c.cmp_bits == cmp_bits && c.eps_bits == eps_bits) return LMR_OK;
+    if (S->s.nreg > 0) {
+        // count-free regions share their bucket regions: apply them before the next op phase
+        if (S->s.free) {
+            const hipError_t e = launch_stage_finish(carve_tiled_ws(ctx->ws, ctx->rec_cap), S->s,
+                                                     reinterpret_cast<hipStream_t>(stream));
+            if (e != hipSuccess) return hip_status(e);
+        }
+        S->s.switched = true;
+    }
+    S->desc = d;
+    S->s.a = base_args(ctx, &d, nullptr, nullptr);
+    S->s.a.ret = int(lmr_op_ret_kind(op));
+    // count-free only while the session has had one op: a mixed session's later phases are
+    // counted regions, so one sweep applies them all
+    S->s.free = !S->s.switched && S->s.nreg == 0 && ctx->rec_cap > 0 &&
+                stage_free_applies(int(d.dtype), int(op), S->s.a.ret, d.shard_len, ctx->rec_cap);
+    return LMR_OK;
 }
 
 lmr_status_t lmr_stage_finish(lmr_ctx_t* ctx, lmr_stream_t stream) {

@@ -145,16 +145,23 @@ struct StageRegion {
     uint64_t n;          // records (slots) of the region
     void* results;       // caller's per-record results (arrival order), may be null
     uint8_t* ok;         // caller's per-record Ok flags, may be null
+    int op;              // the region's op and operands (mixed sessions: one op phase per run of
+    int ret;             // regions with equal op / operands, applied in staging order)
+    uint64_t cmp_bits;
+    uint64_t eps_bits;
 };
 struct StageSession {
-    ApplyArgs a;         // op / kind / shard / ret of the session (record fields unused)
+    ApplyArgs a;         // op / kind / shard / ret of the session's current op (record fields unused)
     int dtype = 0;
     int nreg = 0;
     uint64_t staged = 0; // workspace slots in use
     bool free = false;   // count-free regions (stage_free_applies): shared bucket regions, one fine pass
     bool free_armed = false;
+    bool switched = false;  // the op changed with records staged (lmr_stage_op): later phases counted
     StageRegion reg[kMaxRegions];
 };
+// true when a region staged under a different op / operands than `a`'s is pending
+bool stage_pending_other_op(const StageSession& s, const ApplyArgs& a);
 // true when a staged session of this op takes the count-free regions
 bool stage_free_applies(int dtype, int op, int ret, uint64_t shard_len, uint64_t cap);
 // partition the records of `a` into the next region (caller checks capacity:

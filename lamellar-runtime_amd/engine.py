@@ -33,6 +33,12 @@ from .types import RET_KIND, BatchReturnType, DType, LmrStatus, op_supported
 # the multi-GPU path on a one-GPU box); off by default.
 _FORCE_EXCHANGE = os.environ.get("LAMELLAR_FORCE_EXCHANGE", "0") == "1"
 
+# Large 1-PE batches are deferred: staged into the context's open session and applied with the
+# batches issued after them in one shard sweep, at the next flush point (a handle's block(),
+# wait_all, reading the array, any other device call). LAMELLAR_DEFER=0 applies each at once.
+_DEFER = os.environ.get("LAMELLAR_DEFER", "1") != "0"
+_DEFER_MIN = 65536
+
 
 class BatchResult:
     """Results of a fetch / result batch: values (and Ok flags) in input order."""
@@ -146,15 +152,18 @@ def _host_map(arr, g):
 
 
 def _local(arr, k, dt, op, i_scalar, idx, v_scalar, vals, n, mvsi, results, ok, cmp_bits, eps_bits):
-    shard, slen = arr.local_shard(), arr.num_elems_local()
+    shard, slen = arr._shard_view(), arr.num_elems_local()
     if mvsi:
         _, off = _host_map(arr, idx)
         k.apply_mvsi(shard, slen, arr.kind, dt, op, vals, n, off, results, ok, cmp_bits, eps_bits)
         return
     if i_scalar:
         idx = torch.tensor([idx], dtype=torch.int64, device=k.device)
-    k.apply_soa(shard, slen, arr.kind, dt, op, idx, 8, None if v_scalar else vals,
-                vals if v_scalar else 0, n, results, ok, cmp_bits, eps_bits)
+    apply = k.apply_soa
+    if _DEFER and n >= _DEFER_MIN and getattr(k, "defer_soa", None) is not None:
+        apply = k.defer_soa
+    apply(shard, slen, arr.kind, dt, op, idx, 8, None if v_scalar else vals,
+          vals if v_scalar else 0, n, results, ok, cmp_bits, eps_bits)
 
 
 def _distributed(arr, k, dt, op, i_scalar, idx, i_len, v_scalar, vals, v_len, results, ok, cmp_bits, eps_bits):

@@ -62,6 +62,9 @@ class DeviceKernels:
         self.strategy = int(strategy)
         self.max_ws_records = int(max_ws_records)
         self.reserved = 0
+        # the open deferred session of asynchronous batches (defer_soa): [shard key, (op, cmp, eps),
+        # tensors its kernels still write or read]; applied by flush()
+        self._deferred = None
 
     # ---------------------------------------------------------------- infra
     def stream(self):
@@ -71,6 +74,7 @@ class DeviceKernels:
         """Grow the tiled-apply workspace (allocation: call outside timed regions)."""
         n = min(int(n), self.max_ws_records)
         if n > self.reserved:
+            self.flush()
             torch.cuda.synchronize(self.device)     # the workspace may be in use on any stream
             check(self.lib.lmr_ctx_reserve(self.ctx, n), "lmr_ctx_reserve")
             self.reserved = n
@@ -80,6 +84,7 @@ class DeviceKernels:
             self.reserve(max(n, 1 << 20))
 
     def errors(self, clear=True) -> int:
+        self.flush()
         bits = c_uint32(0)
         self.lib.lmr_ctx_error(self.ctx, self.stream(), byref(bits), 1 if clear else 0)
         return bits.value
@@ -96,6 +101,7 @@ class DeviceKernels:
 
     def profile_read(self, reset=True):
         """{stage: (total_ms, launches, records)} accumulated since the last reset."""
+        self.flush()
         n = len(_capi.STAGES)
         ms = (ctypes.c_double * n)()
         cnt = (c_uint64 * n)()
@@ -105,7 +111,53 @@ class DeviceKernels:
         return {name: (ms[i], cnt[i], rec[i]) for i, name in enumerate(_capi.STAGES)}
 
     def synchronize(self):
+        self.flush()
         torch.cuda.current_stream(self.device).synchronize()
+
+    # ---------------------------------------------------------------- deferred batches
+    # The op-builder API's batches are asynchronous (the reference applies batches in
+    # flight together in no particular order). Consecutive batches on one shard are staged
+    # into one mixed session (lmr_stage_begin / lmr_stage_op / lmr_stage_soa) and applied
+    # together, in issue order per element, by flush(): one shard sweep for many batches.
+    # flush() runs before anything else touches the device state this context manages
+    # (every other call here, synchronize, error reads, the arrays' local data).
+    def defer_soa(self, shard, shard_len, kind, dt, op, idx, iw, vals, scalar_bits, n,
+                  results=None, ok=None, cmp_bits=0, eps_bits=0):
+        """Stage n records for a later flush(); their results / Ok flags are valid after it."""
+        key = (shard.data_ptr(), int(shard_len), int(kind), int(dt.code))
+        if self._deferred is not None and self._deferred[0] != key:
+            self.flush()
+        if self.strategy != Strategy.Direct and n >= 65536 and self.reserved < min(n, self.max_ws_records):
+            self.flush()                      # the workspace grows only with nothing staged
+            self._maybe_reserve(n)
+        opk = (int(op), int(cmp_bits), int(eps_bits))
+        if self._deferred is None:
+            d = self._desc(shard, shard_len, kind, dt, op, cmp_bits, eps_bits)
+            check(self.lib.lmr_stage_begin(self.ctx, byref(d)), "lmr_stage_begin")
+            self._deferred = [key, opk, []]
+        elif self._deferred[1] != opk:
+            check(self.lib.lmr_stage_op(self.ctx, opk[0], c_uint64(opk[1]), c_uint64(opk[2]), self.stream()),
+                  "lmr_stage_op")
+            self._deferred[1] = opk
+        self._deferred[2].append((shard, idx, vals, results, ok))
+        sv = c_uint64(int(scalar_bits) & 0xFFFFFFFFFFFFFFFF)
+        st = self.lib.lmr_stage_soa(self.ctx, _p(idx), int(iw), _p(vals),
+                                    None if vals is not None else ctypes.cast(byref(sv), c_void_p),
+                                    int(n), _p(results), _p(ok), self.stream())
+        if st:
+            self._deferred = None
+            self.lib.lmr_stage_finish(self.ctx, self.stream())
+            check(st, "lmr_stage_soa")
+
+    def flush(self):
+        """Apply the deferred batches (one sweep) on this stream."""
+        d = self._deferred
+        if d is None:
+            return
+        self._deferred = None
+        # the tensors in d[2] are released after the finish is enqueued: the caching allocator
+        # reuses their memory only for work ordered after it on this stream
+        check(self.lib.lmr_stage_finish(self.ctx, self.stream()), "lmr_stage_finish")
 
     def empty(self, n, torch_dtype):
         return torch.empty(max(int(n), 0), dtype=torch_dtype, device=self.device)
@@ -129,6 +181,7 @@ class DeviceKernels:
     def apply_soa(self, shard, shard_len, kind, dt, op, idx, iw, vals, scalar_bits, n,
                   results=None, ok=None, cmp_bits=0, eps_bits=0):
         """Apply n records (idx: iw-byte local offsets; vals tensor or scalar bits)."""
+        self.flush()
         self._maybe_reserve(n)
         d = self._desc(shard, shard_len, kind, dt, op, cmp_bits, eps_bits)
         sv = c_uint64(int(scalar_bits) & 0xFFFFFFFFFFFFFFFF)
@@ -142,6 +195,7 @@ class DeviceKernels:
         """Open a staged session for one op on one shard. `expect`: records the
         session will likely stage; the workspace grows to hold them now, before
         anything is staged (lmr_ctx_reserve is refused while records are staged)."""
+        self.flush()
         if expect:
             self._maybe_reserve(int(expect))
         d = self._desc(shard, shard_len, kind, dt, op, cmp_bits, eps_bits)
@@ -156,6 +210,12 @@ class DeviceKernels:
                                     int(n), _p(results), _p(ok), self.stream())
         check(st, "lmr_stage_soa")
 
+    def stage_op(self, op, cmp_bits=0, eps_bits=0):
+        """Later stage_soa calls stage under `op` (a mixed session: op phases applied in
+        staging order per element, lmr_stage_op)."""
+        check(self.lib.lmr_stage_op(self.ctx, int(op), c_uint64(int(cmp_bits) & 0xFFFFFFFFFFFFFFFF),
+                                    c_uint64(int(eps_bits) & 0xFFFFFFFFFFFFFFFF), self.stream()), "lmr_stage_op")
+
     def stage_finish(self):
         """Apply every staged record in one sweep of the shard and close the session."""
         check(self.lib.lmr_stage_finish(self.ctx, self.stream()), "lmr_stage_finish")
@@ -163,6 +223,7 @@ class DeviceKernels:
     def apply_mvmi(self, shard, shard_len, kind, dt, op, idx_vals_bytes, nbytes, iw,
                    results=None, ok=None, cmp_bits=0, eps_bits=0):
         """Apply a reference wire-format op buffer (packed IdxVal<I,T> records)."""
+        self.flush()
         self._maybe_reserve(nbytes // max(1, self.lib.lmr_record_bytes(iw, dt.code)))
         d = self._desc(shard, shard_len, kind, dt, op, cmp_bits, eps_bits)
         st = self.lib.lmr_apply_mvmi(self.ctx, byref(d), _p(idx_vals_bytes), int(nbytes), int(iw),
@@ -174,6 +235,7 @@ class DeviceKernels:
         """Apply a host-resident op buffer (numpy uint8 IdxVal<I,T> bytes); fetch results / Ok
         flags land in the host numpy arrays h_results / h_ok (lmr_apply_mvmi_host). Synchronous:
         returns when the host results are valid."""
+        self.flush()
         d = self._desc(shard, shard_len, kind, dt, op, cmp_bits, eps_bits)
         st = self.lib.lmr_apply_mvmi_host(self.ctx, byref(d), h_records.ctypes.data, int(h_records.nbytes),
                                           int(iw), None if h_results is None else h_results.ctypes.data,
@@ -190,6 +252,7 @@ class DeviceKernels:
 
     def apply_svmi(self, shard, shard_len, kind, dt, op, scalar_bits, indices, n, iw,
                    results=None, ok=None, cmp_bits=0, eps_bits=0):
+        self.flush()
         self._maybe_reserve(n)
         d = self._desc(shard, shard_len, kind, dt, op, cmp_bits, eps_bits)
         sv = c_uint64(int(scalar_bits) & 0xFFFFFFFFFFFFFFFF)
@@ -199,6 +262,7 @@ class DeviceKernels:
 
     def apply_mvsi(self, shard, shard_len, kind, dt, op, vals, n, index, results=None, ok=None,
                    cmp_bits=0, eps_bits=0):
+        self.flush()
         d = self._desc(shard, shard_len, kind, dt, op, cmp_bits, eps_bits)
         st = self.lib.lmr_apply_mvsi(self.ctx, byref(d), _p(vals), int(n), int(index), _p(results),
                                      _p(ok), self.stream())
@@ -207,6 +271,7 @@ class DeviceKernels:
     def pack(self, layout, gidx, n, vals, dt, iw, stable=True, want_pos=True):
         """Partition by destination PE -> (idx, vals, pos, counts[int64 device]).
         stable=False: lmr_pack_unordered (no order inside a PE's range)."""
+        self.flush()
         npes = layout.num_pes
         out_idx = self.empty(n * iw, torch.uint8)
         out_vals = self.empty(n * dt.bytes, torch.uint8) if vals is not None else None
@@ -221,6 +286,7 @@ class DeviceKernels:
 
     def reduce(self, data, n, dt, op):
         """lmr_reduce over n elements -> (has, value bits) (one 9-byte readback)."""
+        self.flush()
         out = self.empty(2, torch.int64)
         has = out[1:].view(torch.uint8)[:1]
         st = self.lib.lmr_reduce(self.ctx, int(dt.code), int(op), _p(data), int(n), _p(out), _p(has),
@@ -235,6 +301,7 @@ class DeviceKernels:
         global indices (device) unless i_len == 1 (h_index); vals: v_len elements
         (device) unless v_len == 1 (h_val_bits). `expect`: records this PE will likely
         receive; the workspace grows to hold them before the call."""
+        self.flush()
         if expect:
             self._maybe_reserve(int(expect))
         d = self._desc(shard, shard_len, kind, dt, op, cmp_bits, eps_bits)
@@ -251,6 +318,7 @@ class DeviceKernels:
         resolve(am_id) -> (shape, kind, dtype code) of a registered op AM, or None;
         shard_of(view) -> (device tensor, shard_len, strategy) for a decoded AM, or None
         to skip it. Returns {entry index: reply bytes} for the returning AMs."""
+        self.flush()
         errs = []
 
         def res_cb(_user, am_id, shape, kind, dtype):
@@ -296,6 +364,7 @@ class DeviceKernels:
         return {e: bytes(replies[int(offs[e]):int(offs[e]) + int(lens[e])]) for e in range(n.value) if lens[e]}
 
     def scatter_results(self, res_in, pos, n, eb, res_out, ok_in=None, ok_out=None):
+        self.flush()
         st = self.lib.lmr_scatter_results(_p(res_in), _p(pos), int(n), int(eb), _p(res_out),
                                           _p(ok_in), _p(ok_out), self.stream())
         check(st, "lmr_scatter_results")

@@ -1,0 +1,212 @@
+"""Mixed staged sessions (lmr_stage_op) and the deferred batches of the op-builder API.
+
+Batches of different ops on one shard staged into one session are applied in one sweep,
+op phase by op phase in staging order per element. Checked against the oracle:
+  * order-insensitive phases (and / or / xor / add / sub, count-free first phase, counted
+    later ones): the final shard equals the serial per-phase replay, bit for bit;
+  * returning phases between them (swap, compare_exchange, fetch_add): each phase's
+    returned olds / Results are a valid linearisation (oracle/linearize.c) from the state
+    the earlier phases left, and the phase's final state is the one the later phases
+    started from (derived: swap's leftover value, or the later invertible phases undone).
+  * the array API: spawned batches are deferred and applied at the next flush point
+    (block, wait_all, to_numpy, local_data), results valid after block().
+Reference: consecutive batches on one array reach the owner as separate op AMs applied
+concurrently (impl/src/array_ops.rs:863-1408), so per-phase order is one allowed outcome."""
+import numpy as np
+import pytest
+import torch
+
+from opgen import ADD, AND, CAS, FETCH_ADD, OR, STORE, SUB, SWAP, XOR
+from test_gpu_parity import to_dev
+
+pytestmark = pytest.mark.gpu
+
+U32 = 2
+L = (1 << 22) + 333                     # 257 tiles of 16K u32: two-level partition
+N = 1 << 18
+
+
+def _idx(rng, n, hot):
+    """Half uniform over the shard, half on `hot` elements (~4 records each)."""
+    u = rng.integers(0, L, n)
+    h = hot[rng.integers(0, hot.size, n)]
+    return np.where(rng.random(n) < 0.5, u, h).astype(np.uint64)
+
+
+def _fold(op, init, idx, vals):
+    out = init.copy()
+    i = idx.astype(np.int64)
+    if op == AND:
+        np.bitwise_and.at(out, i, vals)
+    elif op == OR:
+        np.bitwise_or.at(out, i, vals)
+    elif op == XOR:
+        np.bitwise_xor.at(out, i, vals)
+    elif op == ADD:
+        np.add.at(out, i, vals)
+    elif op == SUB:
+        np.subtract.at(out, i, vals)
+    return out
+
+
+def test_mixed_session_order_insensitive_phases(world, lam):
+    k = world.team().kernels
+    dt = lam.dtype_of("u32")
+    rng = np.random.default_rng(4242)
+    hot = rng.choice(L, 40000, replace=False)
+    s0 = rng.integers(0, 2**32, L, dtype=np.uint64).astype(np.uint32)
+    phases = [(AND, rng.integers(0, 2**32, N, dtype=np.uint64).astype(np.uint32) | np.uint32(0x0F0F0000)),
+              (OR, rng.integers(0, 2**32, N, dtype=np.uint64).astype(np.uint32) & np.uint32(0x00FF00FF)),
+              (XOR, rng.integers(0, 2**32, N, dtype=np.uint64).astype(np.uint32)),
+              (ADD, rng.integers(0, 2**32, N, dtype=np.uint64).astype(np.uint32)),
+              (AND, rng.integers(0, 2**32, N, dtype=np.uint64).astype(np.uint32) | np.uint32(0xF0F00F0F)),
+              (SUB, rng.integers(0, 2**32, N, dtype=np.uint64).astype(np.uint32))]
+    idxs = [_idx(rng, N, hot) for _ in phases]
+    k.reserve(4 * N)                       # workspace holds 4 phases: the session also flushes when full
+    shard = to_dev(s0)
+    k.profile(True)
+    k.profile_read(reset=True)
+    try:
+        for j, ((op, v), i) in enumerate(zip(phases, idxs)):
+            if j == 0:
+                k.stage_begin(shard, L, 1, dt, op)
+            else:
+                k.stage_op(op)
+            k.stage_soa(to_dev(i), 8, to_dev(v), 0, N)
+        k.stage_finish()
+        stages = k.profile_read(reset=True)
+    finally:
+        k.profile(False)
+    assert k.errors() == 0
+    got = shard.cpu().numpy().view(np.uint32)
+    ref = s0.copy()
+    for (op, v), i in zip(phases, idxs):
+        ref = _fold(op, ref, i, v)
+    assert np.array_equal(got, ref)
+    # the count-free first phase is applied at the switch; the counted phases 2..6 share one
+    # sweep, or two when the workspace (at least 4 phases) fills
+    assert stages["tile_apply"][1] in (2, 3), stages
+
+
+def _swap_final(init, idx, vals, rets):
+    """The state a linearisable swap phase leaves: per element init + sum(vals) - sum(rets)
+    (the one value no later swap returned)."""
+    acc = init.astype(np.uint64).copy()
+    np.add.at(acc, idx.astype(np.int64), vals.astype(np.uint64))
+    np.subtract.at(acc, idx.astype(np.int64), rets.astype(np.uint64))
+    return acc.astype(np.uint32)
+
+
+def test_mixed_session_returning_phases(world, lam, orc):
+    k = world.team().kernels
+    dt = lam.dtype_of("u32")
+    rng = np.random.default_rng(777)
+    hot = rng.choice(L, 30000, replace=False)
+    s0 = rng.integers(0, 8, L, dtype=np.uint64).astype(np.uint32)
+    r32 = lambda hi: rng.integers(0, hi, N, dtype=np.uint64).astype(np.uint32)
+    iA, vA = _idx(rng, N, hot), r32(2**32) | np.uint32(0xFFFFFFF0)
+    iS, vS = _idx(rng, N, hot), r32(8)
+    iX, vX = _idx(rng, N, hot), r32(8)
+    iC, vC = _idx(rng, N, hot), r32(8)
+    iF, vF = _idx(rng, N, hot), r32(1000)
+    iD, vD = _idx(rng, N, hot), r32(2**32)
+    cur = np.uint32(3)
+    k.reserve(8 * N)
+    shard = to_dev(s0)
+    rS, rC, okC, rF = (k.empty(N, torch.int32), k.empty(N, torch.int32), k.empty(N, torch.uint8),
+                       k.empty(N, torch.int32))
+    k.stage_begin(shard, L, 1, dt, AND)
+    k.stage_soa(to_dev(iA), 8, to_dev(vA), 0, N)
+    k.stage_op(SWAP)
+    k.stage_soa(to_dev(iS), 8, to_dev(vS), 0, N, rS)
+    k.stage_op(XOR)
+    k.stage_soa(to_dev(iX), 8, to_dev(vX), 0, N)
+    k.stage_op(CAS, int(cur))
+    k.stage_soa(to_dev(iC), 8, to_dev(vC), 0, N, rC, okC)
+    k.stage_op(FETCH_ADD)
+    k.stage_soa(to_dev(iF), 8, to_dev(vF), 0, N, rF)
+    k.stage_op(ADD)
+    k.stage_soa(to_dev(iD), 8, to_dev(vD), 0, N)
+    k.stage_finish()
+    assert k.errors() == 0
+    final = shard.cpu().numpy().view(np.uint32)
+    u = lambda t: t.cpu().numpy().view(np.uint32)
+    s1 = _fold(AND, s0, iA, vA)
+    s2 = _swap_final(s1, iS, vS, u(rS))
+    st, bad = orc.check_linearizable(1, U32, np.uint32, SWAP, s1, s2, iS, vS, u(rS))
+    assert st == 0, ("swap", st, bad)
+    s3 = _fold(XOR, s2, iX, vX)
+    s5 = _fold(SUB, final, iD, vD)                     # undo the last add phase
+    # fetch_add phase: its start state = its end state minus the phase's sum
+    s4 = _fold(SUB, s5, iF, vF)
+    st, bad = orc.check_linearizable(1, U32, np.uint32, FETCH_ADD, s4, s5, iF, vF, u(rF))
+    assert st == 0, ("fetch_add", st, bad)
+    st, bad = orc.check_linearizable(1, U32, np.uint32, CAS, s3, s4, iC, vC, u(rC), okC.cpu().numpy(),
+                                     current=cur)
+    assert st == 0, ("compare_exchange", st, bad)
+    assert okC.cpu().numpy().any() and (~okC.cpu().numpy().astype(bool)).any()
+
+
+def test_deferred_batches_array_api(world, lam, orc):
+    """Spawned batches are staged and applied at the next flush point, in issue order."""
+    team = world.team()
+    arr = lam.AtomicArray(team, L, lam.Distribution.Block, "u32")
+    rng = np.random.default_rng(99)
+    hot = rng.choice(L, 30000, replace=False)
+    s0 = rng.integers(0, 8, L, dtype=np.uint64).astype(np.uint32)
+    arr.local_data().copy_(torch.from_numpy(s0.view(np.int32)).to(team.kernels.device))
+    r32 = lambda hi: rng.integers(0, hi, N, dtype=np.uint64).astype(np.uint32)
+    iA, vA = _idx(rng, N, hot), r32(2**32)
+    iS, vS = _idx(rng, N, hot), r32(8)
+    iO, vO = _idx(rng, N, hot), r32(2**32)
+    ti = lambda a: torch.from_numpy(a.astype(np.int64)).to(team.kernels.device)
+    tv = lambda a: torch.from_numpy(a.view(np.int32)).to(team.kernels.device)
+    k = team.kernels
+    k.profile(True)
+    k.profile_read(reset=True)
+    try:
+        arr.batch_bit_xor(ti(iA), tv(vA)).spawn()
+        hS = arr.batch_swap(ti(iS), tv(vS)).spawn()
+        arr.batch_bit_or(ti(iO), tv(vO)).spawn()
+        assert k._deferred is not None                    # nothing applied yet
+        rS = hS.block()                                   # flush point
+        stages = k.profile_read(reset=True)
+    finally:
+        k.profile(False)
+    assert k._deferred is None
+    # xor (count-free) applied at the switch, swap + or in one sweep
+    assert stages["tile_apply"][1] == 2, stages
+    final = arr.to_numpy()
+    s1 = _fold(XOR, s0, iA, vA)
+    rs = rS.cpu().numpy().view(np.uint32)
+    s2 = _swap_final(s1, iS, vS, rs)
+    st, bad = orc.check_linearizable(1, U32, np.uint32, SWAP, s1, s2, iS, vS, rs)
+    assert st == 0, ("swap", st, bad)
+    assert np.array_equal(final, _fold(OR, s2, iO, vO))
+    # a read flushes too: a batch followed by local_data() sees the batch applied
+    arr.batch_add(ti(iA), tv(vA)).spawn()
+    after = arr.local_data().cpu().numpy().view(np.uint32)
+    assert np.array_equal(after, _fold(ADD, final, iA, vA))
+
+
+def test_small_stream_after_other_op_phase(world, lam):
+    """A small stream (applied at once) staged after records of another op is applied
+    after them: the session's earlier phases go first."""
+    k = world.team().kernels
+    dt = lam.dtype_of("u32")
+    rng = np.random.default_rng(5)
+    shard = to_dev(np.zeros(L, np.uint32))
+    i0 = rng.integers(0, 1000, N).astype(np.uint64)
+    res = k.empty(N, torch.int32)
+    k.stage_begin(shard, L, 1, dt, FETCH_ADD)
+    k.stage_soa(to_dev(i0), 8, None, 1, N, res)            # staged (counted region)
+    k.stage_op(STORE)
+    k.stage_soa(to_dev(np.arange(1000, dtype=np.uint64)), 8, None, 7, 1000)   # small: applied now
+    k.stage_op(ADD)
+    k.stage_soa(to_dev(i0), 8, None, 1, N)                 # staged again, after the store
+    k.stage_finish()
+    assert k.errors() == 0
+    got = shard.cpu().numpy().view(np.uint32)[:1000]
+    ref = np.full(1000, 7, np.uint32)
+    np.add.at(ref, i0.astype(np.int64), 1)
+    assert np.array_equal(got, ref)
