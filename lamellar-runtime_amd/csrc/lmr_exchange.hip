@@ -173,14 +173,18 @@ lmr_status_t tp_alltoallv(const lmr_transport_t* tp, XState* x, const void* send
                           hipStream_t s) {
     if (!tp->host_buffers)
         return tp->alltoallv(tp->self, send, sb, so, recv, rb, ro, unit, reinterpret_cast<lmr_stream_t>(s));
-    // send segments are packed back to back into the host staging (a count-free pack leaves
-    // them in fixed regions); the callbacks see prefix offsets on both sides
-    std::vector<uint64_t> cso(tp->num_pes);
+    // segments are packed back to back in the host staging on both sides (a count-free pack
+    // leaves the send segments in fixed regions; a PE's own records leave a gap in the receive
+    // layout): the callbacks see prefix offsets
+    std::vector<uint64_t> cso(tp->num_pes), cro(tp->num_pes);
     uint64_t st_end = 0, rt_end = 0;
+    bool rcontig = true;
     for (uint32_t p = 0; p < tp->num_pes; p++) {
         cso[p] = st_end;
         st_end += sb[p];
-        rt_end = std::max(rt_end, ro[p] + rb[p]);
+        cro[p] = rt_end;
+        rcontig = rcontig && (rb[p] == 0 || ro[p] == rt_end);
+        rt_end += rb[p];
     }
     if (x->h_send.need(st_end + 8) != hipSuccess || x->h_recv.need(rt_end + 8) != hipSuccess) return LMR_E_HIP;
     for (uint32_t p = 0; p < tp->num_pes; p++)
@@ -188,10 +192,16 @@ lmr_status_t tp_alltoallv(const lmr_transport_t* tp, XState* x, const void* send
                                     sb[p], hipMemcpyDeviceToHost, s) != hipSuccess)
             return LMR_E_HIP;
     if (hipStreamSynchronize(s) != hipSuccess) return LMR_E_HIP;
-    lmr_status_t st = tp->alltoallv(tp->self, x->h_send.p, sb, cso.data(), x->h_recv.p, rb, ro, unit,
+    lmr_status_t st = tp->alltoallv(tp->self, x->h_send.p, sb, cso.data(), x->h_recv.p, rb, cro.data(), unit,
                                     reinterpret_cast<lmr_stream_t>(s));
     if (st != LMR_OK) return st;
-    if (rt_end) return hs(hipMemcpyAsync(recv, x->h_recv.p, rt_end, hipMemcpyHostToDevice, s));
+    if (rcontig) return rt_end ? hs(hipMemcpyAsync(static_cast<uint8_t*>(recv) + cro[0], x->h_recv.p, rt_end,
+                                                   hipMemcpyHostToDevice, s))
+                               : LMR_OK;
+    for (uint32_t p = 0; p < tp->num_pes; p++)
+        if (rb[p] && hipMemcpyAsync(static_cast<uint8_t*>(recv) + ro[p], static_cast<uint8_t*>(x->h_recv.p) + cro[p], rb[p],
+                                    hipMemcpyHostToDevice, s) != hipSuccess)
+            return LMR_E_HIP;
     return LMR_OK;
 }
 
@@ -280,6 +290,15 @@ bool valid_layout(const lmr_layout_t* L) {
 bool free_pack_enabled() {
     const char* e = getenv("LAMELLAR_FREE_PACK");
     return !(e && e[0] == '0');
+}
+
+// A PE's records for itself skip the transport (dst == src bypasses RCCL): staged
+// straight from the send buffer, results copied back on the device. LAMELLAR_EXCHANGE_SELF=
+// transport sends them through the transport like any other (a 1-PE rehearsal always does, so
+// it makes the RCCL calls of the multi-GPU run).
+bool self_bypass_enabled() {
+    const char* e = getenv("LAMELLAR_EXCHANGE_SELF");
+    return !(e && e[0] == 't');
 }
 
 uint64_t exchange_chunk() {
@@ -419,6 +438,8 @@ lmr_status_t lmr_batch_exchange(lmr_ctx_t* ctx, const lmr_transport_t* tp, const
     // nothing returned: the count-free pack (fixed per-PE regions, no count pass); a chunk
     // whose records overflow a region is packed again with the counted pack
     const bool free_pack = !returning && npes <= 512 && free_pack_enabled();
+    const uint32_t me = layout->my_pe;
+    const bool bypass = npes > 1 && self_bypass_enabled();
     auto region_cap = [&](uint64_t c) -> uint64_t {
         const uint64_t q = (c + npes - 1) / npes;
         return q + q / 8 + 4096;
@@ -465,6 +486,9 @@ lmr_status_t lmr_batch_exchange(lmr_ctx_t* ctx, const lmr_transport_t* tp, const
         // all-to-all-v of chunk j-2 has read it
         const bool packed = !mvsi && j < my_k && cnt > 0;
         if (x->send_used[b] && hipStreamWaitEvent(x->sp, x->ev_send_free[b], 0) != hipSuccess) return LMR_E_HIP;
+        // (own records are staged from send buffer b on the apply stream: that must be done too)
+        if (bypass && x->recv_used[b] && hipStreamWaitEvent(x->sp, x->ev_recv_free[b], 0) != hipSuccess)
+            return LMR_E_HIP;
         const uint32_t cap = uint32_t(free_pack ? region_cap(cnt) : 0);
         auto counted_pack = [&]() -> lmr_status_t {
             return lmr_pack_unordered(ctx, layout, gidx + lo, cnt, scalar ? nullptr : static_cast<const uint8_t*>(d_vals) + lo * eb,
@@ -533,6 +557,9 @@ lmr_status_t lmr_batch_exchange(lmr_ctx_t* ctx, const lmr_transport_t* tp, const
                 }
             }
         }
+        // own records: out of the transport's splits (the receive layout keeps their gap)
+        const uint64_t self_io = iso[me], self_vo = vso[me];
+        if (bypass) isb[me] = irb[me] = vsb[me] = vrb[me] = 0;
         ChunkRec cr;
         cr.lo = mvsi ? 0 : lo;
         cr.hi = mvsi ? n : hi;
@@ -578,9 +605,12 @@ lmr_status_t lmr_batch_exchange(lmr_ctx_t* ctx, const lmr_transport_t* tp, const
             if (c == 0) { p++; continue; }
             void* res = returning ? x->res[j].as<uint8_t>() + ro * eb : nullptr;
             uint8_t* okp = want_ok ? x->rok[j].as<uint8_t>() + ro : nullptr;
+            const bool own = bypass && p == me;         // this PE's own records: from the send buffer
+            const uint8_t* src_i = own ? x->send_idx[b].as<uint8_t>() + self_io : x->recv_idx[b].as<uint8_t>() + io;
+            const uint8_t* src_v = own ? send_vals + self_vo : x->recv_vals[b].as<uint8_t>() + vo;
             if (r[1] >= 0) {                            // MVSI: one atomic block at its index
                 lmr_apply_desc_t d = *desc;
-                st = lmr_apply_mvsi(ctx, &d, x->recv_vals[b].as<uint8_t>() + vo, c, uint64_t(r[1]), res, okp, sa);
+                st = lmr_apply_mvsi(ctx, &d, src_v, c, uint64_t(r[1]), res, okp, sa);
                 if (st != LMR_OK) return st;
                 vo += c * eb;
                 ro += c;
@@ -595,12 +625,13 @@ lmr_status_t lmr_batch_exchange(lmr_ctx_t* ctx, const lmr_transport_t* tp, const
                 const int64_t* q = h_recv + uint64_t(e) * LMR_XHDR_WORDS;
                 if (cr.recv_cnt[e] == 0) { e++; continue; }
                 if (q[1] >= 0 || q[2] != sc || (sc && q[3] != bits)) break;
+                if (bypass && (e == me) != own) break;  // own records are a stream of their own
                 tot += cr.recv_cnt[e];
                 e++;
+                if (own) break;
             }
             const uint64_t ubits = uint64_t(bits);
-            st = lmr_stage_soa(ctx, x->recv_idx[b].as<uint8_t>() + io, iw, sc ? nullptr : x->recv_vals[b].as<uint8_t>() + vo,
-                               sc ? &ubits : nullptr, tot, res, okp, sa);
+            st = lmr_stage_soa(ctx, src_i, iw, sc ? nullptr : src_v, sc ? &ubits : nullptr, tot, res, okp, sa);
             if (st != LMR_OK) return st;
             io += tot * iw;
             if (!sc) vo += tot * eb;
@@ -632,6 +663,14 @@ lmr_status_t lmr_batch_exchange(lmr_ctx_t* ctx, const lmr_transport_t* tp, const
                 if (x->back.need(nsent * eb + 8) != hipSuccess || (want_ok && x->back_ok.need(nsent + 8) != hipSuccess))
                     return LMR_E_HIP;
             }
+            if (bypass && cr.recv_cnt[me]) {           // own results: a device copy, not the transport
+                if (hipMemcpyAsync(static_cast<uint8_t*>(x->back.p) + ro[me], x->res[j].as<uint8_t>() + so[me], sb[me],
+                                   hipMemcpyDeviceToDevice, x->sa) != hipSuccess ||
+                    (want_ok && hipMemcpyAsync(x->back_ok.as<uint8_t>() + oro[me], x->rok[j].as<uint8_t>() + oso[me],
+                                               osb[me], hipMemcpyDeviceToDevice, x->sa) != hipSuccess))
+                    return LMR_E_HIP;
+            }
+            if (bypass) sb[me] = rb[me] = osb[me] = orb[me] = 0;
             st = tp_alltoallv(tp, x, x->res[j].p, sb.data(), so.data(), x->back.p, rb.data(), ro.data(), unit_for(eb),
                               x->sa);
             if (st == LMR_OK && want_ok)

@@ -53,6 +53,7 @@ class HostTransport:
         from . import _capi
         self.num_pes, self.my_pe, self.group = num_pes, my_pe, group
         self.error = None
+        self.self_bytes = 0                                  # bytes this PE sent itself (tests)
         self._a2a = _capi.ALLTOALL_FN(self._alltoall)       # keep the thunks alive
         self._a2av = _capi.ALLTOALLV_FN(self._alltoallv)
         self.t = _capi.lmr_transport_t(num_pes, my_pe, 1, 0, None, self._a2a, self._a2av)
@@ -84,6 +85,7 @@ class HostTransport:
             # the library's splits are back to back (offsets are prefix sums)
             if any(so[p] != sum(sb[:p]) for p in range(n)) or any(ro[p] != sum(rb[:p]) for p in range(n)):
                 raise ValueError("alltoallv splits are not contiguous")
+            self.self_bytes += sb[self.my_pe]
             s, r = _host_view(send, sum(sb)), _host_view(recv, sum(rb))
             sw, rw, ss, rs = _widen(s, r, sb, rb, int(unit))
             dist.all_to_all_single(rw, sw, output_split_sizes=rs, input_split_sizes=ss, group=self.group)

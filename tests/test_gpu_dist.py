@@ -51,6 +51,7 @@ fj = rng.integers(0, 3001, 50000).astype(np.uint64)
 f.batch_add(fj, 1.0).block(); world.barrier()
 out["f_after"] = f.to_numpy()
 out["gi"], out["gv"], out["fi"], out["fj"] = gi, gv, fi, fj
+out["self_bytes"] = np.array(getattr(world.team().transport(), "self_bytes", -1) if ws > 1 else -1)
 np.savez(os.path.join(os.environ["LMR_OUT"], f"pe{me}.npz"), **out)
 world.barrier()
 '''
@@ -96,6 +97,10 @@ def _check(orc, outdir, ws, dist_kind):
     for r in range(ws):
         np.add.at(fexp, pe[r]["fj"].astype(np.int64), 1.0)
     assert np.array_equal(pe[0]["f_after"], fexp)
+    if ws > 1:                        # a PE's own records never went through the transport
+        via = os.environ.get("LAMELLAR_EXCHANGE_SELF", "") == "transport"
+        for r in range(ws):
+            assert (int(pe[r]["self_bytes"]) > 0) == via, (r, int(pe[r]["self_bytes"]))
 
 
 @pytest.mark.parametrize("dist_kind", [0, 1], ids=["Block", "Cyclic"])
