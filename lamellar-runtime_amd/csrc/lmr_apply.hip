@@ -725,22 +725,19 @@ struct RegionOp {
 };
 
 __global__ void k_tile_plan_count(const uint32_t* tile_start, uint32_t num_tiles, uint32_t thresh,
-                                  int combinable, uint32_t* tile_items) {
+                                  int combinable, uint32_t* tile_items, uint32_t* extra) {
     const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= num_tiles) return;
     const uint32_t c = tile_start[t + 1] - tile_start[t];
-    tile_items[t] = (c == 0) ? 0u : ((combinable && c > thresh) ? (c + kSplit - 1) / kSplit : 1u);
+    const uint32_t m = (c == 0) ? 0u : ((combinable && c > thresh) ? (c + kSplit - 1) / kSplit : 1u);
+    tile_items[t] = m;
+    extra[t] = m > 1 ? m : 0u;          // delta pieces (scanned into the delta list)
 }
 
 // Item slot t holds tile t's owner item (mode 0) or a skip marker (mode 2:
 // empty or split tile). Every delta piece of a split tile goes to the delta
 // list at delta_base[t] (exclusive scan of the per-tile piece counts), served
 // by its own persistent kernel so the owner kernel stays lean on registers.
-__global__ void k_tile_plan_extra(const uint32_t* tile_items, uint32_t num_tiles, uint32_t* extra) {
-    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
-    if (t < num_tiles) extra[t] = tile_items[t] > 1 ? tile_items[t] : 0u;
-}
-
 __global__ void k_tile_plan_fill(const uint32_t* tile_start, uint32_t num_tiles, const uint32_t* delta_base,
                                  const uint32_t* tile_items, TileItem* items, TileItem* delta) {
     const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
@@ -1386,8 +1383,7 @@ static hipError_t launch_tile_sweep(int dtype, const ApplyArgs& a, const TiledWs
     const uint32_t thresh = uint32_t(std::min<uint64_t>(0xFFFFFFFFull, std::max<uint64_t>(4 * avg, 65536)));
     const unsigned pg = (T + 255) / 256;
     hipLaunchKernelGGL(k_tile_plan_count, dim3(pg), dim3(256), 0, s, w.tile_start, T, thresh,
-                       op_combines(a.op) ? 1 : 0, w.tile_items);
-    hipLaunchKernelGGL(k_tile_plan_extra, dim3(pg), dim3(256), 0, s, w.tile_items, T, w.tile_items2);
+                       op_combines(a.op) ? 1 : 0, w.tile_items, w.tile_items2);
     hipError_t e = scan_exclusive_u32(w.tile_items2, T, w.plan_partials, w.item_count, s);
     if (e != hipSuccess) return e;
     TileItem* items = reinterpret_cast<TileItem*>(w.items);
@@ -1806,7 +1802,7 @@ __global__ __launch_bounds__(1024) void k_fine_piece(PieceArgs a) {
 // work plan over all regions: owner item per touched tile; a hot tile of a
 // combinable op becomes delta pieces of <= kSplit records over each region's range
 __global__ void k_stage_plan_count(const uint32_t* rts, uint32_t nreg, uint32_t stride, uint32_t num_tiles,
-                                   uint32_t thresh, int combinable, uint32_t* tile_items) {
+                                   uint32_t thresh, int combinable, uint32_t* tile_items, uint32_t* extra) {
     const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= num_tiles) return;
     uint32_t tot = 0, pieces = 0;
@@ -1815,7 +1811,9 @@ __global__ void k_stage_plan_count(const uint32_t* rts, uint32_t nreg, uint32_t 
         tot += c;
         pieces += (c + kSplit - 1) / kSplit;
     }
-    tile_items[t] = (tot == 0) ? 0u : ((combinable && tot > thresh && pieces > 1) ? pieces : 1u);
+    const uint32_t m = (tot == 0) ? 0u : ((combinable && tot > thresh && pieces > 1) ? pieces : 1u);
+    tile_items[t] = m;
+    extra[t] = m > 1 ? m : 0u;
 }
 
 __global__ void k_stage_plan_fill(const uint32_t* rts, uint32_t nreg, uint32_t stride, uint32_t num_tiles,
@@ -1997,8 +1995,7 @@ hipError_t launch_stage_finish(const TiledWs& w, StageSession& s, hipStream_t st
         const uint32_t thresh = uint32_t(std::min<uint64_t>(0xFFFFFFFFull, std::max<uint64_t>(4 * avg, 65536)));
         const unsigned pg = unsigned((T + 255) / 256);
         hipLaunchKernelGGL(k_stage_plan_count, dim3(pg), dim3(256), 0, st, w.rts, uint32_t(s.nreg), stride, T,
-                           thresh, (!mixed && op_combines(a.op)) ? 1 : 0, w.tile_items);
-        hipLaunchKernelGGL(k_tile_plan_extra, dim3(pg), dim3(256), 0, st, w.tile_items, T, w.tile_items2);
+                           thresh, (!mixed && op_combines(a.op)) ? 1 : 0, w.tile_items, w.tile_items2);
         e = scan_exclusive_u32(w.tile_items2, T, w.plan_partials, w.item_count, st);
         if (e != hipSuccess) return e;
         TileItem* items = reinterpret_cast<TileItem*>(w.items);

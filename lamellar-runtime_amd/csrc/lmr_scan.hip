@@ -86,11 +86,44 @@ __global__ __launch_bounds__(1024) void k_scan_apply(uint32_t* __restrict__ d, u
     }
 }
 
+// one block for short arrays (tile starts, plans, coarse offsets): kScanItems elements per
+// pass with the carry in registers, one launch instead of three
+__global__ __launch_bounds__(1024) void k_scan_single(uint32_t* __restrict__ d, uint64_t m,
+                                                      uint32_t* __restrict__ d_total, const uint32_t* only_if) {
+    if (only_if && *only_if == 0) return;
+    __shared__ uint32_t tot;
+    uint32_t carry = 0;
+    for (uint64_t b0 = 0; b0 < m; b0 += kScanItems) {
+        const uint64_t base = b0 + uint64_t(threadIdx.x) * 4;
+        uint32_t v[4];
+        uint32_t sum = 0;
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+            v[i] = (base + i < m) ? d[base + i] : 0;
+            sum += v[i];
+        }
+        uint32_t e = carry + block_excl_scan(sum, &tot);
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+            if (base + i < m) d[base + i] = e;
+            e += v[i];
+        }
+        carry += tot;
+    }
+    if (threadIdx.x == 0 && d_total) *d_total = carry;
+}
+
+constexpr uint64_t kScanSingleMax = 16 * kScanItems;
+
 hipError_t scan_exclusive_u32(uint32_t* d, uint64_t m, uint32_t* partials, uint32_t* d_total,
                               hipStream_t s, const uint32_t* only_if) {
     if (m == 0) {
         if (d_total) return hipMemsetAsync(d_total, 0, sizeof(uint32_t), s);
         return hipSuccess;
+    }
+    if (m <= kScanSingleMax) {
+        hipLaunchKernelGGL(k_scan_single, dim3(1), dim3(1024), 0, s, d, m, d_total, only_if);
+        return hipGetLastError();
     }
     uint64_t nb = (m + kScanItems - 1) / kScanItems;
     hipLaunchKernelGGL(k_scan_reduce, dim3(unsigned(nb)), dim3(1024), 0, s, d, m, partials, only_if);
