@@ -13,18 +13,21 @@ import json
 import os
 import sys
 
-# stage -> (anchor kernels, first one present counts invocations; kernels whose bytes belong to the stage)
+# stage -> (anchor kernels: their launches summed count invocations; kernels whose bytes belong
+# to the stage). Staged sessions: one bin_scatter / fine_scatter invocation per region, one
+# tile_apply / unpartition invocation per tile sweep.
 STAGES = {
-    "bin_count": (("k_bin_count",), ("k_bin_count",)),
-    "bin_scatter": (("k_coarse_free", "k_coarse_scatter", "k_coarse_rm", "k_bin_scatter"),
-                    ("k_coarse_free", "k_coarse_scatter", "k_coarse_offsets", "k_bin_scatter", "k_coarse_rm")),
-    "fine_scatter": (("k_fine_free", "k_fine_scatter", "k_fine_rm"),
-                     ("k_fine_free", "k_fine_scatter", "k_fine_rm", "k_rm_seg_sizes")),
-    "tile_apply": (("k_tile_owner",), ("k_tile_owner", "k_tile_delta", "k_tile_plan_count", "k_tile_plan_extra",
-                                       "k_tile_plan_fill")),
+    "bin_count": (("k_bin_count", "k_ccount"), ("k_bin_count", "k_ccount")),
+    "bin_scatter": (("k_coarse_free", "k_coarse_scatter", "k_bin_scatter"),
+                    ("k_coarse_free", "k_coarse_scatter", "k_coarse_offsets", "k_bin_scatter")),
+    "fine_scatter": (("k_fine_free", "k_fine_scatter", "k_fine_piece"),
+                     ("k_fine_free", "k_fine_scatter", "k_fine_piece", "k_piece_count", "k_free_tile_totals")),
+    "tile_apply": (("k_tile_owner",), ("k_tile_owner", "k_tile_delta", "k_tile_plan_count", "k_stage_plan_count",
+                                       "k_tile_plan_fill", "k_stage_plan_fill")),
     "unpartition": (("k_tile_owner",), ("k_unpartition",)),
     "direct": (("k_apply_direct",), ("k_apply_direct",)),
-    "pack": (("k_pack_count",), ("k_pack_count", "k_pack_scatter", "k_pack_stage", "k_dest_offsets")),
+    "pack": (("k_pack_count", "k_pack_stage"), ("k_pack_count", "k_pack_scatter", "k_pack_stage", "k_dest_offsets",
+                                                 "k_fill_counts")),
     "scatter_results": (("k_scatter_results",), ("k_scatter_results",)),
 }
 
@@ -56,9 +59,11 @@ def main():
         cnt[b] += n
     out = {}
     for st, (anchors, ks) in STAGES.items():
-        anchor = next((a for a in anchors if cnt.get(a)), None)
-        if anchor:
-            out[st] = sum(tot.get(x, 0.0) for x in ks) / cnt[anchor]
+        inv = sum(cnt.get(a, 0) for a in anchors)
+        if st == "pack" and cnt.get("k_pack_count") and cnt.get("k_pack_stage"):
+            inv = cnt["k_pack_count"]                      # counted pack: both kernels per invocation
+        if inv:
+            out[st] = sum(tot.get(x, 0.0) for x in ks) / inv
             print(f"stage {st:16s} {out[st] / 1e6:10.1f} MB per invocation")
     if len(sys.argv) > 2:
         json.dump(out, open(sys.argv[2], "w"), indent=1)
