@@ -1245,9 +1245,10 @@ static int fine_blocks_cap() {
 // dst[k] = src[map[k]] over G block-contiguous ranges of `chunk` records, each split into
 // `split` sub-ranges (LMR_UNPART_SPLIT overrides); LMR_UNPART_NT threads per block,
 // LMR_UNPART_U gathers in flight per thread (defaults 1024, and 4 for 8-byte values, 16 for
-// narrower ones). The one-shot path's ranges are the forward pass's chunks, one per CU
-// (split 1); the staged regions' are 64K-record ranges, about 1.6 per CU at C5's size,
-// and 8 sub-ranges per range balance them: C5 un-partition 0.84 -> 0.62 ms (same box).
+// narrower ones). The one-shot path's ranges are the forward pass's chunks, one per CU,
+// split into ~8K-record sub-ranges; the staged regions' are 64K-record ranges, about 1.6
+// per CU at C5's size, and 8 sub-ranges per range balance them: C5 un-partition 0.84 ->
+// 0.62 ms (same box).
 // Measured and not kept: 256 / 512-thread blocks, 2 or 8 gathers per thread for 8-byte
 // values (C3 0.81 -> 0.82-0.90 ms), and (value, ok) packed into one u64 for Result ops
 // on narrow types (C5: un-partition -0.01 ms, tile sweep +0.02 ms)
@@ -1534,7 +1535,9 @@ hipError_t launch_apply_tiled(int dtype, int index_size, const ApplyArgs& a, con
     const uint8_t* ok_src = (a.ret == LMR_RET_RESULT) ? ok_bin : nullptr;
     auto gather = [&](const uint32_t* map, const uint32_t* n_dev, const uint8_t* src, uint8_t* dst,
                       const uint8_t* oks, uint8_t* okd) {
-        (void)launch_unpartition(vb, map, a.n, n_dev, b.chunk, G, src, dst, oks, okd, s);
+        // ~8K-record sub-ranges, as the staged path's (C3 one-shot un-partition 0.82 -> 0.75 ms at 16)
+        const int split = int(std::min<uint64_t>(64, std::max<uint64_t>(1, b.chunk / 8192)));
+        (void)launch_unpartition(vb, map, a.n, n_dev, b.chunk, G, src, dst, oks, okd, s, split);
     };
     if (num_tiles > uint64_t(kFine)) {
         uint8_t* ok_tmp = ok_src ? reinterpret_cast<uint8_t*>(w.bin_lidx) : nullptr;
