@@ -1245,20 +1245,24 @@ static int fine_blocks_cap() {
 // dst[k] = src[map[k]] over G block-contiguous ranges of `chunk` records, each split into
 // `split` sub-ranges (LMR_UNPART_SPLIT overrides); LMR_UNPART_NT threads per block,
 // LMR_UNPART_U gathers in flight per thread (defaults 1024, and 4 for 8-byte values, 16 for
-// narrower ones). The one-shot path's ranges are the forward pass's chunks, one per CU,
-// split into ~8K-record sub-ranges; the staged regions' are 64K-record ranges, about 1.6
-// per CU at C5's size, and 8 sub-ranges per range balance them: C5 un-partition 0.84 ->
-// 0.62 ms (same box).
+// narrower ones). The ranges (the one-shot path's forward chunks, one per CU; the staged
+// regions' 64K-record ranges) are split into sub-ranges of 32 KB of values (split = 0): one
+// block each, so the grid balances over the CUs. Measured per sub-range size (same box):
+// C3 (8-byte) 8K records 0.68 ms, 4K 0.62, 2K 0.66; C5 (4-byte) 16K 0.60, 8K 0.57, 4K 0.61;
+// C3 one-shot: 256K-record chunks unsplit 0.82 ms, 4K sub-ranges 0.64.
 // Measured and not kept: 256 / 512-thread blocks, 2 or 8 gathers per thread for 8-byte
 // values (C3 0.81 -> 0.82-0.90 ms), and (value, ok) packed into one u64 for Result ops
 // on narrow types (C5: un-partition -0.01 ms, tile sweep +0.02 ms)
 static hipError_t launch_unpartition(int vb, const uint32_t* map, uint64_t n, const uint32_t* n_dev, uint64_t chunk,
                                      uint64_t G, const uint8_t* src, uint8_t* dst, const uint8_t* oks, uint8_t* okd,
-                                     hipStream_t s, int dflt_split = 1) {
+                                     hipStream_t s, int dflt_split = 0) {
     static const int split_env = env_int("LMR_UNPART_SPLIT", 0, 0, 64);
     static const int nt = env_int("LMR_UNPART_NT", 1024, 64, 1024);
     static const int uq = env_int("LMR_UNPART_U", 0, 0, 16);
-    const int split = split_env ? split_env : dflt_split;
+    const uint64_t sub = 32768 / uint64_t(vb);
+    const int split = split_env ? split_env
+                    : dflt_split ? dflt_split
+                                 : int(std::min<uint64_t>(64, std::max<uint64_t>(1, (chunk + sub - 1) / sub)));
     const uint64_t c2 = (chunk + split - 1) / split;
     const unsigned grid = unsigned(std::max<uint64_t>(1, G * uint64_t(split)));
     const int u = uq ? uq : (vb >= 8 ? 4 : 16);
@@ -1535,9 +1539,7 @@ hipError_t launch_apply_tiled(int dtype, int index_size, const ApplyArgs& a, con
     const uint8_t* ok_src = (a.ret == LMR_RET_RESULT) ? ok_bin : nullptr;
     auto gather = [&](const uint32_t* map, const uint32_t* n_dev, const uint8_t* src, uint8_t* dst,
                       const uint8_t* oks, uint8_t* okd) {
-        // ~8K-record sub-ranges, as the staged path's (C3 one-shot un-partition 0.82 -> 0.75 ms at 16)
-        const int split = int(std::min<uint64_t>(64, std::max<uint64_t>(1, b.chunk / 8192)));
-        (void)launch_unpartition(vb, map, a.n, n_dev, b.chunk, G, src, dst, oks, okd, s, split);
+        (void)launch_unpartition(vb, map, a.n, n_dev, b.chunk, G, src, dst, oks, okd, s);
     };
     if (num_tiles > uint64_t(kFine)) {
         uint8_t* ok_tmp = ok_src ? reinterpret_cast<uint8_t*>(w.bin_lidx) : nullptr;
@@ -2046,7 +2048,7 @@ hipError_t launch_stage_finish(const TiledWs& w, StageSession& s, hipStream_t st
             if (Gu > 1024) Gu = 1024;
             if (Gu < 1) Gu = 1;
             const uint64_t chunk = (n + Gu - 1) / Gu;
-            (void)launch_unpartition(vb, map, n, n_dev, chunk, Gu, src, dst, oks, okd, st, 8);
+            (void)launch_unpartition(vb, map, n, n_dev, chunk, Gu, src, dst, oks, okd, st);
         };
         for (int r = 0; r < s.nreg; r++) {
             const StageRegion& g = s.reg[r];
