@@ -245,6 +245,7 @@ struct PartArgs {
     int spill;                    // 1: records beyond a full bucket region are applied to the shard
                                   //    at once (device atomics); 0: they are dropped (never used)
     int accumulate;               // 1: add this launch's tile counts to the rows (staged regions)
+    int xcd_swz;                  // 1: k_fine_free's ranges dealt by xcd_block (one bucket's blocks share an XCD)
     void* shard;                  // spill target
     int op;
     uint64_t val_bits;            // the scalar value when val is null (spilled records)
@@ -620,8 +621,11 @@ __global__ __launch_bounds__(NT) void k_fine_free(PartArgs p) {
     small_excl_scan(s_fill, s_vs, C, &s_total);        // bucket c = virtual records [s_vs[c], s_vs[c] + s_fill[c])
     __syncthreads();
     const uint64_t total = s_total;
-    const uint32_t v_lo = uint32_t(total * blockIdx.x / gridDim.x);
-    const uint32_t v_hi = uint32_t(total * (blockIdx.x + 1) / gridDim.x);
+    // consecutive ranges (one bucket's) on one XCD: the runs they append to a tile merge in its L2
+    const uint32_t nb = gridDim.x;
+    const uint32_t lb = xcd_block(p.xcd_swz != 0);
+    const uint32_t v_lo = uint32_t(total * lb / nb);
+    const uint32_t v_hi = uint32_t(total * (lb + 1) / nb);
     uint32_t c = 0;
     while (c + 1 < C && s_vs[c + 1] <= v_lo) c++;
     uint32_t m_idx[RPT];
@@ -715,6 +719,10 @@ __global__ __launch_bounds__(NT) void k_fine_free(PartArgs p) {
 // combined with the record's LDS prefix — a valid linearisation with each
 // workgroup's records applied as one block.
 constexpr uint32_t kSplit = 16 * 1024;     // records per delta item (16 per thread)
+#ifndef LMR_WAVE_COMBINE
+#define LMR_WAVE_COMBINE 1
+#endif
+constexpr bool kWaveCombine = LMR_WAVE_COMBINE != 0;   // lds_acc_wave in the delta pass (A/B builds: -DLMR_WAVE_COMBINE=0)
 
 struct TileItem { uint32_t tile, lo, hi, mode; };
 
@@ -824,6 +832,75 @@ __device__ __forceinline__ T delta_finish(int op, T base, T prefix) {
         return T(base ^ prefix);
     }
     return base;
+}
+
+// a (+) b for the delta accumulation ops (FETCH_ADD / AND / OR / XOR), wrapping for integers
+template <typename T>
+__device__ __forceinline__ T acc_comb(int acc, T a, T b) {
+    using U = typename bits_of<T>::U;
+    if (acc == LMR_OP_FETCH_ADD) {
+        if constexpr (is_flt<T>::v) return a + b; else return T(U(U(a) + U(b)));
+    }
+    if constexpr (!is_flt<T>::v) {
+        if (acc == LMR_OP_FETCH_AND) return T(a & b);
+        if (acc == LMR_OP_FETCH_OR) return T(a | b);
+        return T(a ^ b);
+    }
+    return a;
+}
+template <typename T>
+__device__ __forceinline__ T shfl_t(T x, int src) {
+    using U = typename bits_of<T>::U;
+    if constexpr (sizeof(T) == 8) return from_bits<T>(U(__shfl((unsigned long long)U(to_bits(x)), src, 64)));
+    else return from_bits<T>(U(__shfl(uint32_t(U(to_bits(x))), src, 64)));
+}
+template <typename T>
+__device__ __forceinline__ T shfl_up_t(T x, int d) {
+    using U = typename bits_of<T>::U;
+    if constexpr (sizeof(T) == 8) return from_bits<T>(U(__shfl_up((unsigned long long)U(to_bits(x)), d, 64)));
+    else return from_bits<T>(U(__shfl_up(uint32_t(U(to_bits(x))), d, 64)));
+}
+
+// One record per active lane accumulated into an LDS delta tile with `acc`, returning the
+// element's previous delta. When many lanes of the wave name the first active lane's element
+// (a hot element: Zipf streams put most of a hot tile's records on it), those lanes combine
+// their values with a wave scan and one lane applies the sum: one LDS atomic instead of up to
+// 64 serialised ones; lane j of the group gets base (+) the values of the group's lanes before j
+// (the group applied in lane order, as one step). Called by every lane of the wave.
+template <typename T>
+__device__ __forceinline__ T lds_acc_wave(typename word_of<T>::W* tile, uint32_t l, T v, bool active, int acc,
+                                          T ident, int kind, uint32_t* err) {
+    const int lane = threadIdx.x & 63;
+    const uint64_t act = __ballot(active);
+    T res = ident;
+    bool done = false;
+    uint8_t ok = 0;
+    if (act) {
+        const int f = __ffsll((unsigned long long)act) - 1;
+        const uint32_t l0 = __shfl(l, f, 64);
+        const bool in = active && l == l0;
+        const uint64_t m = __ballot(in);
+        if (__popcll(m) >= 8) {
+            T x = in ? v : ident;
+#pragma unroll
+            for (int d = 1; d < 64; d <<= 1) {
+                const T y = shfl_up_t(x, d);
+                if (lane >= d) x = acc_comb(acc, y, x);
+            }
+            T excl = shfl_up_t(x, 1);
+            if (lane == 0) excl = ident;
+            const T total = shfl_t(x, 63);
+            T base = ident;
+            if (lane == f) base = rmw_lds<T>(tile + l0, acc, kind, total, ident, ident, ok, err);
+            base = shfl_t(base, f);
+            if (in) {
+                res = acc_comb(acc, base, excl);
+                done = true;
+            }
+        }
+    }
+    if (active && !done) res = rmw_lds<T>(tile + l, acc, kind, v, ident, ident, ok, err);
+    return res;
 }
 
 // OPT >= 0 fixes the op at compile time (hot paths); -1 reads it from the args.
@@ -943,50 +1020,76 @@ __global__ __launch_bounds__(1024) void k_tile_delta(TileArgs a) {
     const U ident_bits = (op == LMR_OP_AND || op == LMR_OP_FETCH_AND) ? ~U(0) : U(0);
     const int acc = delta_acc_op(op);
     const int gop = delta_global_op(op);
+    // elements some record of the piece touched (fetch forms: only those need their base)
+    __shared__ uint32_t touched[16384 / 32];
     for (uint32_t it = blockIdx.x; it < nitems; it += gridDim.x) {
         const TileItem w = a.delta[it];
         const uint64_t base = uint64_t(w.tile) << a.tile_shift;
         const uint32_t len = uint32_t(min(uint64_t(1) << a.tile_shift, a.shard_len - base));
         T* shard = reinterpret_cast<T*>(a.shard) + base;
         for (uint32_t e = threadIdx.x; e < len; e += blockDim.x) tile[e] = ident;
+        if (ret != LMR_RET_NONE)
+            for (uint32_t e = threadIdx.x; e < (len + 31) / 32; e += blockDim.x) touched[e] = 0;
         __syncthreads();
         T pre[kSplit / 1024];
 #pragma unroll
         for (int k = 0; k < int(kSplit / 1024); k++) {
             const uint32_t r = w.lo + threadIdx.x + uint32_t(k) * 1024u;
-            if (r < w.hi) {
-                const uint32_t l = bin_lidx[r];
-                const T v = a.scalar ? sv : bin_val[r];
+            const bool in = r < w.hi;
+            const uint32_t l = in ? bin_lidx[r] : 0u;
+            const T v = !in ? T(0) : a.scalar ? sv : bin_val[r];
+            if (kWaveCombine) {
+                pre[k] = lds_acc_wave<T>(tile, l, v, in, acc, from_bits<T>(ident_bits), a.kind, a.err);
+            } else if (in) {
                 uint8_t ok = 0;
                 pre[k] = rmw_lds<T>(tile + l, acc, a.kind, v, cmp, eps, ok, a.err);
             }
+            // the first record on an element sees the identity (later ones may too: harmless)
+            if (in && ret != LMR_RET_NONE && U(to_bits(pre[k])) == U(ident_bits)) atomicOr(&touched[l >> 5], 1u << (l & 31));
         }
         __syncthreads();
-        for (uint32_t e = threadIdx.x; e < len; e += blockDim.x) {
-            T d;
-            if constexpr (sizeof(T) >= 4) d = tile[e];
-            else d = T(U(tile[e]));
-            uint8_t ok = 0;
-            T b;
-            if (U(to_bits(d)) != U(ident_bits)) b = rmw_global<T>(shard + e, gop, a.kind, d, cmp, eps, ok, a.err);
-            else if (ret != LMR_RET_NONE) b = rmw_global<T>(shard + e, LMR_OP_LOAD, a.kind, d, cmp, eps, ok, a.err);
-            else continue;
-            if (ret != LMR_RET_NONE) {
-                if constexpr (sizeof(T) >= 4) tile[e] = b;
-                else tile[e] = W(U(b));
+        // one device-scope atomic per changed element, a load per touched unchanged one;
+        // every element's operation is issued before any result is waited for
+        constexpr int kPer = kTileBytes / int(sizeof(W)) / 1024;   // elements per thread (a tile's words / 1024)
+        T b[kPer];
+        bool need[kPer];
+#pragma unroll
+        for (int k = 0; k < kPer; k++) {
+            const uint32_t e = threadIdx.x + uint32_t(k) * 1024u;
+            need[k] = false;
+            if (e < len) {
+                T d;
+                if constexpr (sizeof(T) >= 4) d = tile[e];
+                else d = T(U(tile[e]));
+                uint8_t ok = 0;
+                if (U(to_bits(d)) != U(ident_bits)) {
+                    b[k] = rmw_global<T>(shard + e, gop, a.kind, d, cmp, eps, ok, a.err);
+                    need[k] = true;
+                } else if (ret != LMR_RET_NONE && ((touched[e >> 5] >> (e & 31)) & 1u)) {
+                    b[k] = rmw_global<T>(shard + e, LMR_OP_LOAD, a.kind, d, cmp, eps, ok, a.err);
+                    need[k] = true;
+                }
             }
         }
         if (ret != LMR_RET_NONE) {
+#pragma unroll
+            for (int k = 0; k < kPer; k++) {
+                const uint32_t e = threadIdx.x + uint32_t(k) * 1024u;
+                if (need[k]) {
+                    if constexpr (sizeof(T) >= 4) tile[e] = b[k];
+                    else tile[e] = W(U(b[k]));
+                }
+            }
             __syncthreads();
 #pragma unroll
             for (int k = 0; k < int(kSplit / 1024); k++) {
                 const uint32_t r = w.lo + threadIdx.x + uint32_t(k) * 1024u;
                 if (r < w.hi) {
                     const uint32_t l = bin_lidx[r];
-                    T b;
-                    if constexpr (sizeof(T) >= 4) b = tile[l];
-                    else b = T(U(tile[l]));
-                    reinterpret_cast<T*>(a.results)[r] = delta_finish<T>(op, b, pre[k]);
+                    T bb;
+                    if constexpr (sizeof(T) >= 4) bb = tile[l];
+                    else bb = T(U(tile[l]));
+                    reinterpret_cast<T*>(a.results)[r] = delta_finish<T>(op, bb, pre[k]);
                 }
             }
         }
@@ -1241,6 +1344,17 @@ static int fine_blocks_cap() {
     static int v = env_int("LMR_FINE_BLOCKS", 512, 1, 1 << 20);
     return v;
 }
+// k_fine_free's grid: 1024 blocks with XCD-grouped ranges (C2 fine 1.29 -> 1.26 ms vs 512)
+static int free_fine_blocks() {
+    static int v = env_int("LMR_FREE_FINE_BLOCKS", 1024, 8, 1 << 20);
+    return v;
+}
+// LMR_FINE_XCD=0: k_fine_free's ranges dealt in plain block order (xcd_block off). The piece
+// and counted fine passes keep plain order: with it, C5 fine 0.81 -> 0.89 ms, C3 +0.03 ms
+static int fine_xcd() {
+    static int v = env_int("LMR_FINE_XCD", 1, 0, 1);
+    return v;
+}
 
 // dst[k] = src[map[k]] over G block-contiguous ranges of `chunk` records, each split into
 // `split` sub-ranges (LMR_UNPART_SPLIT overrides); LMR_UNPART_NT threads per block,
@@ -1346,6 +1460,7 @@ static PartArgs free_args(int dtype, const ApplyArgs& a, const TiledWs& w, uint3
     q.ff_fill = w.ff + 64; q.ff_tfill = w.ff + 64 + kMaxCoarse;
     q.capc = uint32_t(w.tmp_cap / q.C); q.tmp_cap = w.tmp_cap;
     q.spill = 1; q.shard = a.shard; q.op = a.op;
+    q.xcd_swz = fine_xcd();
     return q;
 }
 
@@ -1374,7 +1489,7 @@ static hipError_t launch_free_finish(int vb, const PartArgs& q, const TiledWs& w
     ProfScope ps(prof, LMR_STAGE_FINE_SCATTER, s, n);
     dispatch_vb_rpt<2>(vb, fine_rpt(vb), [&](auto vbt, auto rpt) {
         constexpr int VBc = decltype(vbt)::value, R = decltype(rpt)::value;
-        hipLaunchKernelGGL((k_fine_free<VBc, R, 1024>), dim3(unsigned(fine_blocks_cap())), dim3(1024), 0, s, q);
+        hipLaunchKernelGGL((k_fine_free<VBc, R, 1024>), dim3(unsigned(free_fine_blocks())), dim3(1024), 0, s, q);
     });
     return hipGetLastError();
 }

@@ -482,6 +482,17 @@ __host__ __device__ inline int key_bits(uint32_t nkeys) {
     return b;
 }
 
+// ---------------------------------------------------------------- XCD-grouped block ids
+// Blocks b and b + 8 share an XCD (observed round-robin placement; speed only, never
+// correctness). The swizzled id gives each XCD a contiguous range of ids, so work items
+// with consecutive ids (runs appended to the same bins) are written through one L2 and
+// the partial lines where one run meets the next merge there instead of being written
+// back from two XCDs (count-free fine pass, C2: 1.55 -> 1.29 ms on one box).
+__device__ __forceinline__ uint32_t xcd_block(bool on) {
+    const uint32_t nb = gridDim.x, b = blockIdx.x;
+    return (on && (nb & 7) == 0) ? (b & 7) * (nb >> 3) + (b >> 3) : b;
+}
+
 // ---------------------------------------------------------------- LDS-staged write-out
 // Write-out of one bucket-sorted LDS round: bucket c's hist[c] records, staged at
 // LDS [base[c], base[c] + hist[c]), go to global [cursor[c], ...). Waves take
