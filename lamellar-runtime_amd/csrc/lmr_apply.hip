@@ -238,9 +238,9 @@ struct PartArgs {
     uint32_t* counts;             // count-free partition: [G][num_tiles] per-block tile count rows
     uint32_t* err;
     // count-free partition (k_coarse_free / k_fine_free)
-    uint32_t* ff_fill;            // [C] records reserved in each coarse bucket's region
+    uint32_t* ff_fill;            // [C * kSegs] records reserved in each segment of every bucket region
     uint32_t* ff_tfill;           // [num_tiles] records reserved in each tile
-    uint32_t capc;                // records per coarse bucket region
+    uint32_t capc;                // records per coarse bucket region (kXcds sub-regions + a shared area)
     uint64_t tmp_cap;             // temp arrays' capacity (records)
     int spill;                    // 1: records beyond a full bucket region are applied to the shard
                                   //    at once (device atomics); 0: they are dropped (never used)
@@ -489,15 +489,32 @@ __global__ __launch_bounds__(1024) void k_fine_scatter(PartArgs p) {
 // A bucket that outgrows its region (a batch concentrated on a few 8 MB stretches
 // of the shard) applies its extra records to the shard at once with device atomics
 // (spill): the op is order-insensitive, so any split between the two is exact.
+// Bucket region layout (count-free): kXcds sub-regions of capc / 16 slots, one per XCD, then
+// a shared area (the rest, ~capc / 2). A block appends its runs to its own XCD's sub-region,
+// so the runs of one bucket written through one L2 are adjacent there and their partial lines
+// merge in it; what a sub-region cannot take goes to the shared area (skewed streams, e.g.
+// each block's records on a few buckets), and past that to the spill.
+constexpr uint32_t kXcds = 8;
+constexpr uint32_t kSegs = kXcds + 1;                 // segments per bucket region
+__host__ __device__ inline uint32_t sub_cap(uint32_t capc) { return capc / 16; }
+__host__ __device__ inline uint32_t seg_base(uint32_t capc, uint32_t x) { return x * sub_cap(capc); }
+__host__ __device__ inline uint32_t seg_cap(uint32_t capc, uint32_t x) {
+    return x < kXcds ? sub_cap(capc) : capc - kXcds * sub_cap(capc);
+}
+__device__ __forceinline__ uint32_t xcc_id() { return __builtin_amdgcn_s_getreg((3 << 11) | 20) & (kXcds - 1); }  // HW_REG_XCC_ID
+
 template <int IW, int VB, int RPT>
 __global__ __launch_bounds__(1024) void k_coarse_free(PartArgs p) {
     using V = typename idx_t<VB>::I;
     constexpr uint32_t kRound = RPT * 1024;
     extern __shared__ uint32_t th[];                   // [num_tiles] this block's tile counts
-    __shared__ uint32_t hist[kMaxCoarse], base[kMaxCoarse], cursor[kMaxCoarse], tot;
+    __shared__ uint32_t hist[kMaxCoarse], base[kMaxCoarse], tot;
+    __shared__ uint32_t seg_a[kMaxCoarse], len_a[kMaxCoarse], seg_b[kMaxCoarse];   // a round's run: 2 pieces
     __shared__ uint32_t s_idx[kRound];
     __shared__ V s_val[kRound];
     const uint32_t g = blockIdx.x, C = p.C;
+    const uint32_t xcc = xcc_id();
+    const uint32_t capx = sub_cap(p.capc), caps = seg_cap(p.capc, kXcds);
     const int cshift = p.tile_shift + kFineShift;
     for (uint32_t t = threadIdx.x; t < p.num_tiles; t += blockDim.x) th[t] = 0;
     const uint64_t lo = uint64_t(g) * p.chunk;
@@ -534,12 +551,12 @@ __global__ __launch_bounds__(1024) void k_coarse_free(PartArgs p) {
         __syncthreads();
         small_excl_scan(hist, base, C, &tot);
         __syncthreads();
-        // reserve this round's run in every bucket region; the returned fill is
-        // consumed after the LDS staging below, which hides the atomic's latency
+        // reserve this round's run of every bucket in the XCD's sub-region; the returned
+        // fill is consumed after the LDS staging below, which hides the atomic's latency
         uint32_t rsv = 0, cnt = 0;
         if (threadIdx.x < C) {
             cnt = hist[threadIdx.x];
-            if (cnt) rsv = atomicAdd(&p.ff_fill[threadIdx.x], cnt);
+            if (cnt) rsv = atomicAdd(&p.ff_fill[threadIdx.x * kSegs + xcc], cnt);
         }
 #pragma unroll
         for (int j = 0; j < RPT; j++) {
@@ -549,7 +566,12 @@ __global__ __launch_bounds__(1024) void k_coarse_free(PartArgs p) {
             s_val[q] = m_val[j];
         }
         if (threadIdx.x < C) {
-            cursor[threadIdx.x] = rsv;                     // bucket-relative
+            const uint32_t c = threadIdx.x;
+            const uint32_t a = rsv >= capx ? 0u : min(cnt, capx - rsv);
+            seg_a[c] = seg_base(p.capc, xcc) + rsv;
+            len_a[c] = a;
+            // the rest (a full sub-region) goes to the shared area (rare for mixed streams)
+            seg_b[c] = (cnt > a) ? atomicAdd(&p.ff_fill[c * kSegs + kXcds], cnt - a) : 0u;
         }
         if (r0 + kRound < hi) load_round(r0 + kRound);     // prefetch the next round
         __syncthreads();
@@ -557,14 +579,17 @@ __global__ __launch_bounds__(1024) void k_coarse_free(PartArgs p) {
         // device atomics (the op is order-insensitive) and taken out of the tile counts.
         const uint32_t nw = blockDim.x >> 6, wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
         const uint32_t wpb = C >= nw ? 1u : nw / C, bstep = nw / wpb;
+        const uint32_t sb = seg_base(p.capc, kXcds);
         for (uint32_t c = wave / wpb; c < C; c += bstep) {
-            const uint32_t len = hist[c], b = base[c], d = cursor[c];
+            const uint32_t len = hist[c], b = base[c], la = len_a[c], da = seg_a[c], db = seg_b[c];
             const uint64_t reg = uint64_t(c) * p.capc;
             for (uint32_t i = (wave % wpb) * 64 + lane; i < len; i += wpb * 64) {
                 const uint32_t q = b + i;
-                if (d + i < p.capc) {
-                    p.tmp_idx[reg + d + i] = s_idx[q];
-                    if (p.tmp_val) reinterpret_cast<V*>(p.tmp_val)[reg + d + i] = s_val[q];
+                const uint32_t j = i - la;                  // position in the shared part
+                if (i < la || db + j < caps) {
+                    const uint64_t d = reg + (i < la ? da + i : sb + db + j);
+                    p.tmp_idx[d] = s_idx[q];
+                    if (p.tmp_val) reinterpret_cast<V*>(p.tmp_val)[d] = s_val[q];
                 } else if (p.spill) {                       // not binned: out of the tile counts
                     atomicSub(&th[s_idx[q] >> p.tile_shift], 1u);
                     uint8_t ok;
@@ -602,6 +627,32 @@ __global__ __launch_bounds__(1024) void k_free_tile_totals(const uint32_t* rows,
     }
 }
 
+// exclusive scan of in[0..m) (m <= 2 * NT) into out[], total into *tot; every thread calls it
+template <int NT>
+__device__ __noinline__ void block_excl_scan(const uint32_t* in, uint32_t* out, uint32_t m, uint32_t* part,
+                                                uint32_t* tot) {
+    const uint32_t t = threadIdx.x, lane = t & 63, w = t >> 6;
+    const uint32_t a = 2 * t < m ? in[2 * t] : 0u, b = 2 * t + 1 < m ? in[2 * t + 1] : 0u;
+    uint32_t inc = a + b;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t y = __shfl_up(inc, d, 64);
+        if (int(lane) >= d) inc += y;
+    }
+    if (lane == 63) part[w] = inc;
+    __syncthreads();
+    if (t == 0) {
+        uint32_t run = 0;
+        for (int i = 0; i < NT / 64; i++) { const uint32_t x = part[i]; part[i] = run; run += x; }
+        *tot = run;
+    }
+    __syncthreads();
+    const uint32_t ex = part[w] + inc - (a + b);
+    if (2 * t < m) out[2 * t] = ex;
+    if (2 * t + 1 < m) out[2 * t + 1] = ex + a;
+    __syncthreads();
+}
+
 // Rounds are read through buffer descriptors (BufStream): with flat loads the compiler kept
 // one 64-bit pointer per record of the round alive and spilled them. Measured on one box
 // (tools/ab_mix.sh): fine pass 1.558 -> 1.548 ms at 12K rounds; 768-thread blocks with
@@ -611,15 +662,18 @@ __global__ __launch_bounds__(NT) void k_fine_free(PartArgs p) {
     using V = typename idx_t<VB>::I;
     constexpr uint32_t kRound = RPT * NT;
     __shared__ uint32_t hist[kFine], base[kFine], cursor[kFine], tot;
-    __shared__ uint32_t s_fill[kMaxCoarse], s_vs[kMaxCoarse], s_total;
+    __shared__ uint32_t s_fill[kMaxCoarse * kSegs], s_vs[kMaxCoarse * kSegs], s_pb[kMaxCoarse * kSegs];
+    __shared__ uint32_t s_part[NT / 64], s_total;
     __shared__ uint16_t s_l[kRound];
     __shared__ V s_val[kRound];
-    const uint32_t C = p.C;
+    const uint32_t C = p.C * kSegs;                    // segments: (bucket, sub-region / shared area)
     const uint32_t lmask = (1u << p.tile_shift) - 1u;
-    for (uint32_t c = threadIdx.x; c < C; c += blockDim.x) s_fill[c] = min(p.ff_fill[c], p.capc);  // spilled: clipped
+    for (uint32_t c = threadIdx.x; c < C; c += blockDim.x) {
+        s_fill[c] = min(p.ff_fill[c], seg_cap(p.capc, c % kSegs));   // overflowed: clipped
+        s_pb[c] = (c / kSegs) * p.capc + seg_base(p.capc, c % kSegs);  // physical first slot
+    }
     __syncthreads();
-    small_excl_scan(s_fill, s_vs, C, &s_total);        // bucket c = virtual records [s_vs[c], s_vs[c] + s_fill[c])
-    __syncthreads();
+    block_excl_scan<NT>(s_fill, s_vs, C, s_part, &s_total);   // segment c = virtual records [s_vs[c], + s_fill[c])
     const uint64_t total = s_total;
     // consecutive ranges (one bucket's) on one XCD: the runs they append to a tile merge in its L2
     const uint32_t nb = gridDim.x;
@@ -642,10 +696,10 @@ __global__ __launch_bounds__(NT) void k_fine_free(PartArgs p) {
             m_val[j] = bv.load<V>(o * VB);
         }
     };
-    // bucket c's slice of [v_lo, v_hi) as physical temp slots
+    // segment cc's slice of [v_lo, v_hi) as physical temp slots
     auto seg = [&](uint32_t cc, uint32_t& lo, uint32_t& hi) {
         const uint32_t a = max(v_lo, s_vs[cc]), b = min(v_hi, s_vs[cc] + s_fill[cc]);
-        lo = cc * p.capc + (a - s_vs[cc]);
+        lo = s_pb[cc] + (a - s_vs[cc]);
         hi = lo + (b > a ? b - a : 0u);
     };
     // invariant: the current bucket's first round is loaded (prefetched) on entry
@@ -660,7 +714,7 @@ __global__ __launch_bounds__(NT) void k_fine_free(PartArgs p) {
             lo = nlo; hi = nhi;
             continue;
         }
-        const uint32_t t0 = c * kFine;
+        const uint32_t t0 = (c / kSegs) * kFine;
         const uint32_t nf = min(uint32_t(kFine), p.num_tiles - t0);
         const uint32_t ts = threadIdx.x < nf ? p.tile_start[t0 + threadIdx.x] : 0u;
         for (uint32_t r0 = lo; r0 < hi; r0 += kRound) {
@@ -1209,17 +1263,19 @@ bool tiled_supported(int dtype, uint64_t shard_len) {
 
 // count-free partition counters: [0] unused (was the overflow flag), [64, 64 + C) bucket
 // fills, then one fill per tile
-static size_t ff_words() { return 64 + size_t(kMaxCoarse) + size_t(kMaxTiles); }
+static size_t ff_words() { return 64 + size_t(kMaxCoarse) * kSegs + size_t(kMaxTiles); }
 
 // temp arrays: 25 % (+ 8192 records per coarse bucket) above the piece capacity, the
 // headroom the count-free partition's fixed per-bucket regions need (3 B per record)
+// temp slots: a count-free bucket region is 8 XCD sub-regions of capc / 16 (a uniform stream's
+// share with 12 % headroom) and a shared area of ~capc / 2 (a bucket's whole share): 2.25 x
 static uint64_t tmp_cap_for(uint64_t cap) {
-    return cap + cap / 4 + uint64_t(kMaxCoarse) * 8192;
+    return 2 * cap + cap / 4 + uint64_t(kMaxCoarse) * 8192;
 }
 
 uint64_t max_rec_cap() {
     // every temp slot index (< tmp_cap_for(cap)) must fit the kernels' uint32 slot math
-    return (uint64_t(0xFFFFFFFFull) - uint64_t(kMaxCoarse) * 8192) / 5 * 4;
+    return (uint64_t(0xFFFFFFFFull) - uint64_t(kMaxCoarse) * 8192) / 9 * 4;
 }
 
 size_t tiled_ws_bytes(uint64_t cap) {
@@ -1457,7 +1513,7 @@ static PartArgs free_args(int dtype, const ApplyArgs& a, const TiledWs& w, uint3
     q.tmp_idx = w.tmp_idx; q.tmp_val = w.tmp_val;          // values always materialised
     q.bin_lidx = w.bin_lidx; q.bin_val = w.bin_val;
     q.err = a.err;
-    q.ff_fill = w.ff + 64; q.ff_tfill = w.ff + 64 + kMaxCoarse;
+    q.ff_fill = w.ff + 64; q.ff_tfill = w.ff + 64 + kMaxCoarse * kSegs;
     q.capc = uint32_t(w.tmp_cap / q.C); q.tmp_cap = w.tmp_cap;
     q.spill = 1; q.shard = a.shard; q.op = a.op;
     q.xcd_swz = fine_xcd();

@@ -546,7 +546,7 @@ def test_free_partition_bucket_overflow_spills(world, orc, lam, dt, monkeypatch)
     tile = 8192 if t(0).itemsize == 8 else 16384
     shard_len = 640 * tile + 3                     # 641 tiles: 6 coarse buckets
     C = 6
-    capc = (R + R // 4 + 128 * 8192) // C           # one coarse bucket's region of the temp arrays
+    capc = (2 * R + R // 4 + 128 * 8192) // C       # one coarse bucket's region of the temp arrays
     n = min(max(1 << 21, 2 * capc + 4096), R)
     assert n >= 2 * capc, "workspace too large for a forced spill"
     shard0 = rand_elems(dt, shard_len, rng, ADD)
@@ -698,7 +698,7 @@ def test_staged_free_session_spill_and_flush(world, orc, lam, dt, op):
     shard_len = (1 << 22) + 5
     tile = 8192 if t(0).itemsize == 8 else 16384
     C = -(-(-(-shard_len // tile)) // 128)
-    capc = (R + R // 4 + 128 * 8192) // C           # a coarse bucket's region (temp-array headroom)
+    capc = (2 * R + R // 4 + 128 * 8192) // C       # a coarse bucket's region (temp-array headroom)
     m = 150000
     n_skew = -(-2 * capc // m)                       # twice what bucket 0's region holds
     n_all = max(n_skew + 8, R // m + 4)              # more than the workspace: several sweeps
