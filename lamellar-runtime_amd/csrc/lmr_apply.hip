@@ -662,69 +662,73 @@ __global__ __launch_bounds__(NT) void k_fine_free(PartArgs p) {
     using V = typename idx_t<VB>::I;
     constexpr uint32_t kRound = RPT * NT;
     __shared__ uint32_t hist[kFine], base[kFine], cursor[kFine], tot;
-    __shared__ uint32_t s_fill[kMaxCoarse * kSegs], s_vs[kMaxCoarse * kSegs], s_pb[kMaxCoarse * kSegs];
+    __shared__ uint32_t s_fill[kMaxCoarse * kSegs], s_vs[kMaxCoarse * kSegs + 1];
     __shared__ uint32_t s_part[NT / 64], s_total;
     __shared__ uint16_t s_l[kRound];
     __shared__ V s_val[kRound];
-    const uint32_t C = p.C * kSegs;                    // segments: (bucket, sub-region / shared area)
+    const uint32_t NB = p.C, C = p.C * kSegs;          // buckets; segments (bucket, sub-region / shared area)
     const uint32_t lmask = (1u << p.tile_shift) - 1u;
-    for (uint32_t c = threadIdx.x; c < C; c += blockDim.x) {
+    for (uint32_t c = threadIdx.x; c < C; c += blockDim.x)
         s_fill[c] = min(p.ff_fill[c], seg_cap(p.capc, c % kSegs));   // overflowed: clipped
-        s_pb[c] = (c / kSegs) * p.capc + seg_base(p.capc, c % kSegs);  // physical first slot
-    }
     __syncthreads();
-    block_excl_scan<NT>(s_fill, s_vs, C, s_part, &s_total);   // segment c = virtual records [s_vs[c], + s_fill[c])
+    block_excl_scan<NT>(s_fill, s_vs, C, s_part, &s_total);   // segment c = virtual records [s_vs[c], s_vs[c + 1])
+    if (threadIdx.x == 0) s_vs[C] = s_total;
+    __syncthreads();
     const uint64_t total = s_total;
     // consecutive ranges (one bucket's) on one XCD: the runs they append to a tile merge in its L2
     const uint32_t nb = gridDim.x;
     const uint32_t lb = xcd_block(p.xcd_swz != 0);
     const uint32_t v_lo = uint32_t(total * lb / nb);
     const uint32_t v_hi = uint32_t(total * (lb + 1) / nb);
-    uint32_t c = 0;
-    while (c + 1 < C && s_vs[c + 1] <= v_lo) c++;
+    auto bstart = [&](uint32_t b) { return s_vs[b * kSegs]; };     // bucket b = virtual [bstart(b), bstart(b + 1))
     uint32_t m_idx[RPT];
     V m_val[RPT];
-    // the round [r0, hi) through buffer descriptors based at r0 (records past hi read 0)
-    auto load_round = [&](uint32_t r0, uint32_t hi) {
-        const uint32_t m = hi > r0 ? min(hi - r0, kRound) : 0u;
-        const BufStream bi(p.tmp_idx + r0, m * 4);
-        const BufStream bv(p.tmp_val + uint64_t(r0) * VB, p.tmp_val ? m * VB : 0u);
+    // Round [v0, min(v0 + kRound, e)) of bucket b's virtual records: a round runs across the
+    // bucket's segments (no partial round per segment); each record's slot is its segment's
+    // base + its offset in it, read through buffer descriptors over the bucket's region
+    // (records past e read 0). free_partition_rpt keeps capc * VB below 2^31.
+    auto load_round = [&](uint32_t b, uint32_t v0, uint32_t e) {
+        const BufStream bi(p.tmp_idx + uint64_t(b) * p.capc, p.capc * 4u);
+        const BufStream bv(p.tmp_val + uint64_t(b) * p.capc * VB, p.tmp_val ? p.capc * uint32_t(VB) : 0u);
+        const uint32_t* vs = s_vs + b * kSegs;
+        uint32_t k = 0;
 #pragma unroll
         for (int j = 0; j < RPT; j++) {
-            const uint32_t o = uint32_t(j) * NT + threadIdx.x;
-            m_idx[j] = bi.load<uint32_t>(o * 4);
-            m_val[j] = bv.load<V>(o * VB);
+            const uint32_t v = v0 + uint32_t(j) * NT + threadIdx.x;
+            uint32_t off = 0x3FFFFFFFu;                              // past the region: reads 0
+            if (v < e) {
+                while (v >= vs[k + 1]) k++;
+                off = seg_base(p.capc, k) + (v - vs[k]);
+            }
+            m_idx[j] = bi.load<uint32_t>(off * 4u);
+            m_val[j] = bv.load<V>(off * uint32_t(VB));
         }
     };
-    // segment cc's slice of [v_lo, v_hi) as physical temp slots
-    auto seg = [&](uint32_t cc, uint32_t& lo, uint32_t& hi) {
-        const uint32_t a = max(v_lo, s_vs[cc]), b = min(v_hi, s_vs[cc] + s_fill[cc]);
-        lo = s_pb[cc] + (a - s_vs[cc]);
-        hi = lo + (b > a ? b - a : 0u);
+    // the next bucket at or after bb with records in [v_lo, v_hi)
+    auto next_bucket = [&](uint32_t bb) {
+        while (bb < NB && bstart(bb) < v_hi && max(v_lo, bstart(bb)) >= min(v_hi, bstart(bb + 1))) bb++;
+        return bb;
     };
+    uint32_t b = 0;
+    while (b + 1 < NB && bstart(b + 1) <= v_lo) b++;
+    b = next_bucket(b);
     // invariant: the current bucket's first round is loaded (prefetched) on entry
-    uint32_t lo, hi;
-    seg(c, lo, hi);
-    if (lo < hi) load_round(lo, hi);
-    for (; c < C && s_vs[c] < v_hi; c++) {
-        uint32_t nlo = 0, nhi = 0;
-        if (c + 1 < C && s_vs[c + 1] < v_hi) seg(c + 1, nlo, nhi);
-        if (lo == hi) {
-            if (nlo < nhi) load_round(nlo, nhi);
-            lo = nlo; hi = nhi;
-            continue;
-        }
-        const uint32_t t0 = (c / kSegs) * kFine;
+    if (b < NB && bstart(b) < v_hi) load_round(b, max(v_lo, bstart(b)), min(v_hi, bstart(b + 1)));
+    while (b < NB && bstart(b) < v_hi) {
+        const uint32_t a = max(v_lo, bstart(b)), e = min(v_hi, bstart(b + 1));
+        const uint32_t bn = next_bucket(b + 1);
+        const bool has_next = bn < NB && bstart(bn) < v_hi;
+        const uint32_t t0 = b * kFine;
         const uint32_t nf = min(uint32_t(kFine), p.num_tiles - t0);
         const uint32_t ts = threadIdx.x < nf ? p.tile_start[t0 + threadIdx.x] : 0u;
-        for (uint32_t r0 = lo; r0 < hi; r0 += kRound) {
+        for (uint32_t v0 = a; v0 < e; v0 += kRound) {
             for (uint32_t f = threadIdx.x; f < nf; f += blockDim.x) hist[f] = 0;
             __syncthreads();
             // (tile, validity) are recomputed from m_idx where needed (registers)
             uint32_t m_rank[RPT];
 #pragma unroll
             for (int j = 0; j < RPT; j++)
-                m_rank[j] = (r0 + uint32_t(j) * NT + threadIdx.x < hi)
+                m_rank[j] = (v0 + uint32_t(j) * NT + threadIdx.x < e)
                                 ? atomicAdd(&hist[(m_idx[j] >> p.tile_shift) - t0], 1u) : 0u;
             __syncthreads();
             small_excl_scan(hist, base, nf, &tot);
@@ -736,29 +740,31 @@ __global__ __launch_bounds__(NT) void k_fine_free(PartArgs p) {
             }
 #pragma unroll
             for (int j = 0; j < RPT; j++) {
-                if (r0 + uint32_t(j) * NT + threadIdx.x >= hi) continue;
+                if (v0 + uint32_t(j) * NT + threadIdx.x >= e) continue;
                 const uint32_t q = base[(m_idx[j] >> p.tile_shift) - t0] + m_rank[j];
                 s_l[q] = uint16_t(m_idx[j] & lmask);
                 s_val[q] = m_val[j];
             }
             if (threadIdx.x < nf) cursor[threadIdx.x] = ts + rsv;
             {   // one prefetch site (the next round of this bucket, else the next bucket's
-                // first; an empty range reads nothing): one set of registers for the round
-                const bool more = r0 + kRound < hi;
-                load_round(more ? r0 + kRound : nlo, more ? hi : nhi);
+                // first; nothing left: an empty range reads nothing): one set of registers
+                const bool more = v0 + kRound < e;
+                const uint32_t nbk = more ? b : (has_next ? bn : b);
+                load_round(nbk, more ? v0 + kRound : (has_next ? max(v_lo, bstart(bn)) : e),
+                           more ? e : (has_next ? min(v_hi, bstart(bn + 1)) : e));
             }
             __syncthreads();
-            V* bv = reinterpret_cast<V*>(p.bin_val);
+            V* bvp = reinterpret_cast<V*>(p.bin_val);
             if (p.tmp_val)
                 bucket_writeout(hist, base, cursor, nf, [&](uint32_t q, uint32_t dst) {
                     p.bin_lidx[dst] = s_l[q];
-                    bv[dst] = s_val[q];
+                    bvp[dst] = s_val[q];
                 });
             else
                 bucket_writeout(hist, base, cursor, nf, [&](uint32_t q, uint32_t dst) { p.bin_lidx[dst] = s_l[q]; });
             __syncthreads();
         }
-        lo = nlo; hi = nhi;
+        b = bn;
     }
 }
 
@@ -1474,6 +1480,7 @@ static int free_partition_rpt(int dtype, int op, int ret, uint64_t n, uint64_t n
     const uint64_t capc = tmp_cap / C;
     if (n / C + n / (4 * C) + 8192 > capc) return 0;
     const int vb = dtype_bytes(dtype);
+    if (capc * uint64_t(vb) >= (uint64_t(1) << 31)) return 0;   // k_fine_free's buffer descriptors
     // the largest round that fits next to the LDS tile counts (static + dynamic LDS
     // <= 160 KiB); 8-byte values: 10K-record rounds at 8192 tiles (12K with the
     // counted pass). 4-byte values take 8K rounds here (C5: coarse 0.80 -> 0.72 ms)
