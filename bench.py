@@ -125,6 +125,10 @@ class AddUniform(Workload):
 
     def describe(self):
         a = self.args
+        if self.npes == 1 and os.environ.get("LAMELLAR_FORCE_EXCHANGE", "0") == "1":
+            return ("C4 one-rank rehearsal: 2^%d batched u64 add records through the forced exchange "
+                    "(lmr_batch_exchange over a 1-rank RCCL communicator), uniform-random indices into "
+                    "a 2^%d-element AtomicArray<u64>" % (a.records_log2 or 28, a.elems_log2 or 26))
         if self.npes == 1:
             return ("C2: 2^%d batched u64 add records, uniform-random indices into a 2^%d-element "
                     "AtomicArray<u64>" % (a.records_log2 or 28, a.elems_log2 or 26))
