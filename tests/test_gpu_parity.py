@@ -410,6 +410,34 @@ def test_tiled_two_level_partition_bit_exact(world, orc, lam, dt, partition):
             assert np.array_equal(c.ok_d, c.ok_o)
 
 
+@pytest.mark.parametrize("dt,op", [("u64", ADD), ("i64", XOR), ("u64", FETCH_ADD), ("u32", ADD), ("i64", FETCH_ADD)])
+def test_tiled_ragged_batch_lengths(world, orc, lam, dt, op, partition):
+    """Odd batch lengths, not a multiple of any LDS round: the coarse pass's paired 16-B
+    record loads end on a single record, and the tile apply's 4-record groups start and end
+    on unaligned bin ranges (head and tail records one per thread). Colliding streams:
+    exact final state (integers) and, for fetch_add with v = 1, exact olds per element."""
+    k = world.team().kernels
+    k.reserve(1 << 21)
+    rng = np.random.default_rng(77 + CODE[dt] + op)
+    shard_len = (1 << 21) + 37
+    t = NP[dt]
+    for n in (1, 3, 65537, (1 << 20) + 777):
+        idx = rng.integers(0, shard_len, n).astype(np.uint64)
+        shard0 = rand_elems(dt, shard_len, rng, op)
+        vals = np.ones(n, dtype=t) if op == FETCH_ADD else rand_vals(dt, n, rng, op)
+        c = Case(k, orc, lam, dt, op, shard0, idx, vals, "soa", 2)
+        assert c.err == 0 and c.st_o == 0, (dt, op, n)
+        assert bits_equal(c.got, c.ref), (dt, op, n)
+        if op == FETCH_ADD:                  # olds of an element: base, base + 1, ..., base + m - 1
+            olds = c.res_d.view(np.uint64)
+            order = np.lexsort((olds, idx))
+            si, so = idx[order], olds[order]
+            first = np.r_[0, np.flatnonzero(si[1:] != si[:-1]) + 1]
+            start = np.repeat(first, np.diff(np.r_[first, n]))
+            rank = (np.arange(n) - start).astype(np.uint64)
+            assert np.array_equal(so, shard0.view(np.uint64)[si.astype(np.int64)] + rank), (dt, n)
+
+
 def test_tiled_two_level_collisions(world, orc, lam, partition):
     """Colliding u64 fetch_add over > 128 tiles: exact final state; each element's olds
     are exactly init, init+1, ..., init+m-1 (v = 1)."""
