@@ -106,8 +106,9 @@ class lmr_shard_t(Structure):
     _fields_ = [("shard", c_void_p), ("shard_len", c_uint64), ("strategy", c_uint32), ("reserved_", c_uint32)]
 
 
-AM_RESOLVER_FN = ctypes.CFUNCTYPE(c_int, c_void_p, ctypes.c_int32, POINTER(c_uint32), POINTER(c_uint32),
-                                  POINTER(c_uint32))
+# (user, cmd, am_id, body, avail, *shape, *kind, *dtype, *body_bytes) -> 0 op AM / 1 other AM (sized)
+AM_RESOLVER_FN = ctypes.CFUNCTYPE(c_int, c_void_p, c_uint32, ctypes.c_int32, c_void_p, c_uint64, POINTER(c_uint32),
+                                  POINTER(c_uint32), POINTER(c_uint32), POINTER(c_uint64))
 SHARD_RESOLVER_FN = ctypes.CFUNCTYPE(c_int, c_void_p, POINTER(lmr_am_view_t), POINTER(lmr_shard_t))
 
 # name -> (restype, argtypes). Every symbol of include/lamellar_gpu_ops.h.
@@ -174,7 +175,7 @@ SIGNATURES = {
 }
 
 STAGES = ["direct", "mvsi", "bin_count", "scan", "bin_scatter", "tile_apply", "pack",
-          "scatter_results", "fine_scatter", "unpartition", "window"]
+          "scatter_results", "fine_scatter", "unpartition", "window", "ordered"]
 
 _lib = None
 

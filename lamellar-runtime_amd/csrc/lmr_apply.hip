@@ -1165,10 +1165,20 @@ __global__ __launch_bounds__(1024) void k_tile_delta(TileArgs a) {
     const uint32_t nitems = *a.delta_count;
     const uint16_t* bin_lidx = a.bin_lidx;
     const T* bin_val = reinterpret_cast<const T*>(a.bin_val);
-    const W ident = (op == LMR_OP_AND || op == LMR_OP_FETCH_AND) ? W(~U(0)) : W(0);
-    const U ident_bits = (op == LMR_OP_AND || op == LMR_OP_FETCH_AND) ? ~U(0) : U(0);
+    // floats: -0.0 is the identity of IEEE addition (-0.0 + x == x for every x, +0.0 and
+    // NaN included; +0.0 + -0.0 would be +0.0), and a - v is a + (-v) bit for bit, so a
+    // float sub piece accumulates -v and is applied as an add: base + (sum of its values)
+    // then keeps the sign of zero a serial chain of single RMWs gives
+    constexpr bool kFlt = is_flt<T>::v;
+    const bool fsub = kFlt && (op == LMR_OP_SUB || op == LMR_OP_FETCH_SUB);
+    const U ident_bits = (op == LMR_OP_AND || op == LMR_OP_FETCH_AND) ? ~U(0)
+                         : kFlt ? U(U(1) << (8 * sizeof(U) - 1)) : U(0);
+    W ident;
+    if constexpr (kFlt) ident = from_bits<T>(ident_bits);
+    else ident = W(ident_bits);
     const int acc = delta_acc_op(op);
-    const int gop = delta_global_op(op);
+    const int gop = fsub ? int(LMR_OP_FETCH_ADD) : delta_global_op(op);
+    const int fop = fsub ? int(LMR_OP_FETCH_ADD) : op;
     // elements some record of the piece touched (fetch forms: only those need their base)
     __shared__ uint32_t touched[16384 / 32];
     for (uint32_t it = blockIdx.x; it < nitems; it += gridDim.x) {
@@ -1186,7 +1196,8 @@ __global__ __launch_bounds__(1024) void k_tile_delta(TileArgs a) {
             const uint32_t r = w.lo + threadIdx.x + uint32_t(k) * 1024u;
             const bool in = r < w.hi;
             const uint32_t l = in ? bin_lidx[r] : 0u;
-            const T v = !in ? T(0) : a.scalar ? sv : bin_val[r];
+            T v = !in ? T(0) : a.scalar ? sv : bin_val[r];
+            if (fsub) v = -v;
             if (kWaveCombine) {
                 pre[k] = lds_acc_wave<T>(tile, l, v, in, acc, from_bits<T>(ident_bits), a.kind, a.err);
             } else if (in) {
@@ -1238,7 +1249,7 @@ __global__ __launch_bounds__(1024) void k_tile_delta(TileArgs a) {
                     T bb;
                     if constexpr (sizeof(T) >= 4) bb = tile[l];
                     else bb = T(U(tile[l]));
-                    reinterpret_cast<T*>(a.results)[r] = delta_finish<T>(op, bb, pre[k]);
+                    reinterpret_cast<T*>(a.results)[r] = delta_finish<T>(fop, bb, pre[k]);
                 }
             }
         }

@@ -150,7 +150,7 @@ bool valid_iw(uint32_t iw) { return iw == 1 || iw == 2 || iw == 4 || iw == 8; }
 
 lmr_status_t check_desc(const lmr_apply_desc_t* d) {
     if (!d || d->dtype >= LMR_NUM_DTYPES || d->op >= LMR_NUM_OPS || d->kind > LMR_KIND_READ_ONLY ||
-        d->strategy > LMR_STRATEGY_TILED)
+        d->strategy > LMR_STRATEGY_ORDERED)
         return LMR_E_INVALID;
     if (!lmr_op_supported(d->kind, d->dtype, d->op)) return LMR_E_UNSUPPORTED;
     return LMR_OK;
@@ -230,6 +230,8 @@ uint64_t staged_mode_split(int dtype, int op, int ret, uint64_t shard_len, uint6
 lmr_status_t run_apply(lmr_ctx* ctx, const lmr_apply_desc_t* d, ApplyArgs a, int iw,
                        hipStream_t s) {
     const int eb = dtype_bytes(int(d->dtype));
+    if (d->strategy == LMR_STRATEGY_ORDERED || (d->strategy == LMR_STRATEGY_AUTO && a.n < kOrderedAuto))
+        return hip_status(launch_apply_ordered(ctx, int(d->dtype), iw, a, s));
     bool tiled = false;
     if (d->strategy == LMR_STRATEGY_TILED) {
         if (!ctx->ws || ctx->rec_cap == 0) return LMR_E_WORKSPACE;
@@ -318,6 +320,7 @@ lmr_status_t lmr_ctx_destroy(lmr_ctx_t* ctx) {
     xstate_free(ctx->xch);
     win_state_free(ctx->win);
     wire_bufs_free(ctx->wire);
+    ord_bufs_free(ctx->ord);
     if (ctx->ws) (void)hipFree(ctx->ws);
     if (ctx->d_err) (void)hipFree(ctx->d_err);
     if (ctx->prof) {
@@ -568,7 +571,8 @@ lmr_status_t lmr_reduce(lmr_ctx_t* ctx, uint32_t dtype, uint32_t op, const void*
 lmr_status_t lmr_apply_mvmi(lmr_ctx_t* ctx, const lmr_apply_desc_t* desc, const void* d_idx_vals,
                             uint64_t nbytes, uint32_t index_size, void* d_results, uint8_t* d_ok,
                             lmr_stream_t stream) {
-    if (!ctx || !valid_iw(index_size)) return LMR_E_INVALID;
+    if (!ctx) return LMR_E_INVALID;
+    index_size = am_index_width(index_size);
     lmr_status_t st = check_desc(desc);
     if (st != LMR_OK) return st;
     const uint32_t rb = lmr_record_bytes(index_size, desc->dtype);
@@ -587,7 +591,8 @@ lmr_status_t lmr_apply_mvmi(lmr_ctx_t* ctx, const lmr_apply_desc_t* desc, const 
 lmr_status_t lmr_apply_svmi(lmr_ctx_t* ctx, const lmr_apply_desc_t* desc, const void* val,
                             const void* d_indices, uint64_t n, uint32_t index_size, void* d_results,
                             uint8_t* d_ok, lmr_stream_t stream) {
-    if (!ctx || !valid_iw(index_size) || !val) return LMR_E_INVALID;
+    if (!ctx || !val) return LMR_E_INVALID;
+    index_size = am_index_width(index_size);
     lmr_status_t st = check_desc(desc);
     if (st != LMR_OK) return st;
     if (n == 0) return LMR_OK;

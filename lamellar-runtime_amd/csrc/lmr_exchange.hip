@@ -216,6 +216,7 @@ struct RcclApi {
     decltype(&ncclGroupEnd) group_end = nullptr;
     decltype(&ncclSend) send = nullptr;
     decltype(&ncclRecv) recv = nullptr;
+    decltype(&ncclCommAbort) comm_abort = nullptr;
     bool ok = false;
 };
 
@@ -234,6 +235,7 @@ const RcclApi& rccl() {
         api.group_end = reinterpret_cast<decltype(api.group_end)>(dlsym(h, "ncclGroupEnd"));
         api.send = reinterpret_cast<decltype(api.send)>(dlsym(h, "ncclSend"));
         api.recv = reinterpret_cast<decltype(api.recv)>(dlsym(h, "ncclRecv"));
+        api.comm_abort = reinterpret_cast<decltype(api.comm_abort)>(dlsym(h, "ncclCommAbort"));
         api.ok = api.get_unique_id && api.comm_init_rank && api.comm_destroy && api.group_start &&
                  api.group_end && api.send && api.recv;
     });
@@ -254,33 +256,55 @@ ncclDataType_t nccl_type(uint32_t unit) {
     }
 }
 
+// A failed ncclSend / ncclRecv inside the group still ends the group (RCCL requires the
+// ncclGroupEnd), and the call reports the first failure.
 lmr_status_t rccl_alltoall(void* self, const void* send, void* recv, uint64_t bytes, lmr_stream_t stream) {
     RcclTransport* t = static_cast<RcclTransport*>(self);
+    if (!t->comm) return LMR_E_HIP;                  // aborted after an earlier failure
     const uint32_t unit = (bytes % 8 == 0) ? 8 : (bytes % 4 == 0 ? 4 : 1);
     const size_t cnt = size_t(bytes / unit);
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
     const RcclApi& R = rccl();
     if (R.group_start() != ncclSuccess) return LMR_E_HIP;
-    for (uint32_t p = 0; p < t->tp.num_pes; p++) {
-        R.send(static_cast<const uint8_t*>(send) + uint64_t(p) * bytes, cnt, nccl_type(unit), int(p), t->comm, s);
-        R.recv(static_cast<uint8_t*>(recv) + uint64_t(p) * bytes, cnt, nccl_type(unit), int(p), t->comm, s);
+    bool ok = true;
+    for (uint32_t p = 0; p < t->tp.num_pes && ok; p++) {
+        ok = R.send(static_cast<const uint8_t*>(send) + uint64_t(p) * bytes, cnt, nccl_type(unit), int(p), t->comm, s) ==
+                 ncclSuccess &&
+             R.recv(static_cast<uint8_t*>(recv) + uint64_t(p) * bytes, cnt, nccl_type(unit), int(p), t->comm, s) ==
+                 ncclSuccess;
     }
-    return R.group_end() == ncclSuccess ? LMR_OK : LMR_E_HIP;
+    return (R.group_end() == ncclSuccess && ok) ? LMR_OK : LMR_E_HIP;
 }
 
 lmr_status_t rccl_alltoallv(void* self, const void* send, const uint64_t* sb, const uint64_t* so, void* recv,
                             const uint64_t* rb, const uint64_t* ro, uint32_t unit, lmr_stream_t stream) {
     RcclTransport* t = static_cast<RcclTransport*>(self);
+    if (!t->comm) return LMR_E_HIP;
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
     const ncclDataType_t ty = nccl_type(unit == 2 ? 1 : unit);
     const uint32_t u = (unit == 8 || unit == 4) ? unit : 1;
     const RcclApi& R = rccl();
     if (R.group_start() != ncclSuccess) return LMR_E_HIP;
-    for (uint32_t p = 0; p < t->tp.num_pes; p++) {
-        if (sb[p]) R.send(static_cast<const uint8_t*>(send) + so[p], size_t(sb[p] / u), ty, int(p), t->comm, s);
-        if (rb[p]) R.recv(static_cast<uint8_t*>(recv) + ro[p], size_t(rb[p] / u), ty, int(p), t->comm, s);
+    bool ok = true;
+    for (uint32_t p = 0; p < t->tp.num_pes && ok; p++) {
+        if (sb[p]) ok = R.send(static_cast<const uint8_t*>(send) + so[p], size_t(sb[p] / u), ty, int(p), t->comm, s) ==
+                        ncclSuccess;
+        if (ok && rb[p]) ok = R.recv(static_cast<uint8_t*>(recv) + ro[p], size_t(rb[p] / u), ty, int(p), t->comm, s) ==
+                              ncclSuccess;
     }
-    return R.group_end() == ncclSuccess ? LMR_OK : LMR_E_HIP;
+    return (R.group_end() == ncclSuccess && ok) ? LMR_OK : LMR_E_HIP;
+}
+
+// After a transport failure the peers may never post their halves of the queued send / recv
+// pairs, so waiting for the device could block forever: an RCCL transport aborts its
+// communicator first (ncclCommAbort ends the queued RCCL kernels; the transport then refuses
+// every later call and the job must make a new one). A host-buffer transport's failure leaves
+// only local copies on the device.
+void transport_abort(const lmr_transport_t* tp) {
+    if (!tp || tp->alltoall != rccl_alltoall) return;
+    RcclTransport* t = static_cast<RcclTransport*>(tp->self);
+    if (t->comm && rccl().comm_abort) rccl().comm_abort(t->comm);
+    t->comm = nullptr;
 }
 
 bool valid_layout(const lmr_layout_t* L) {
@@ -377,7 +401,7 @@ lmr_status_t lmr_transport_rccl_destroy(lmr_transport_t* tp) {
     RcclTransport* t = static_cast<RcclTransport*>(tp->self);
     (void)hipSetDevice(t->device);
     (void)hipDeviceSynchronize();
-    if (t->comm) rccl().comm_destroy(t->comm);
+    if (t->comm) rccl().comm_destroy(t->comm);       // (an aborted communicator is already gone)
     delete t;
     return LMR_OK;
 }
@@ -461,13 +485,16 @@ lmr_status_t lmr_batch_exchange(lmr_ctx_t* ctx, const lmr_transport_t* tp, const
     // context stays usable; the device work already enqueued drains first
     struct SessionGuard {
         lmr_ctx_t* c;
+        const lmr_transport_t* t;
         bool armed = true;
+        bool tp_failed = false;       // a transport call failed: abort it before draining
         ~SessionGuard() {
             if (!armed) return;
+            if (tp_failed) transport_abort(t);
             (void)hipDeviceSynchronize();
             stage_abort(c->stage);
         }
-    } guard{ctx};
+    } guard{ctx, tp};
     struct ChunkRec {
         std::vector<uint64_t> send_cnt, recv_cnt;
         uint64_t lo, hi, total;
@@ -530,7 +557,7 @@ lmr_status_t lmr_batch_exchange(lmr_ctx_t* ctx, const lmr_transport_t* tp, const
         // (one wait per chunk; the next chunk's pack is not enqueued yet, the previous
         // chunk's staging runs meanwhile): sent rows, then received rows
         st = tp_alltoall(tp, x, x->hdr_send[b].p, x->hdr_recv.p, LMR_XHDR_WORDS * 8, x->sx);
-        if (st != LMR_OK) return st;
+        if (st != LMR_OK) { guard.tp_failed = true; return st; }
         if (hipMemcpyAsync(x->h_hdr.p, x->hdr_send[b].p, size_t(npes) * LMR_XHDR_WORDS * 8, hipMemcpyDeviceToHost,
                            x->sx) != hipSuccess)
             return LMR_E_HIP;
@@ -586,7 +613,7 @@ lmr_status_t lmr_batch_exchange(lmr_ctx_t* ctx, const lmr_transport_t* tp, const
         if (st == LMR_OK)
             st = tp_alltoallv(tp, x, send_vals, vsb.data(), vso.data(), x->recv_vals[b].p, vrb.data(), vro.data(),
                               unit_for(eb), x->sx);
-        if (st != LMR_OK) return st;
+        if (st != LMR_OK) { guard.tp_failed = true; return st; }
         if (hipEventRecord(x->ev_send_free[b], x->sx) != hipSuccess) return LMR_E_HIP;
         x->send_used[b] = true;
         if (hipEventRecord(x->ev_x, x->sx) != hipSuccess || hipStreamWaitEvent(x->sa, x->ev_x, 0) != hipSuccess)
@@ -676,7 +703,11 @@ lmr_status_t lmr_batch_exchange(lmr_ctx_t* ctx, const lmr_transport_t* tp, const
             if (st == LMR_OK && want_ok)
                 st = tp_alltoallv(tp, x, x->rok[j].p, osb.data(), oso.data(), x->back_ok.p, orb.data(), oro.data(), 1,
                                   x->sa);
-            if (st != LMR_OK) return st;
+            if (st != LMR_OK) {                         // (the session is already applied)
+                transport_abort(tp);
+                (void)hipDeviceSynchronize();
+                return st;
+            }
             if (nsent == 0) continue;
             if (mvsi) {                                 // results come back in value order
                 if (hipMemcpyAsync(d_results, x->back.p, nsent * eb, hipMemcpyDeviceToDevice, x->sa) != hipSuccess ||

@@ -97,7 +97,7 @@ lmr_status_t lmr_apply_mvmi_host(lmr_ctx_t* ctx, const lmr_apply_desc_t* desc, c
                                  uint64_t nbytes, uint32_t index_size, void* h_results, uint8_t* h_ok,
                                  lmr_stream_t stream) {
     if (!ctx || !desc) return LMR_E_INVALID;
-    if (index_size != 1 && index_size != 2 && index_size != 4 && index_size != 8) return LMR_E_INVALID;
+    index_size = am_index_width(index_size);
     if (desc->dtype >= LMR_NUM_DTYPES) return LMR_E_INVALID;
     const uint32_t rb = lmr_record_bytes(index_size, desc->dtype);
     const uint32_t eb = rb ? uint32_t(dtype_bytes(int(desc->dtype))) : 0;

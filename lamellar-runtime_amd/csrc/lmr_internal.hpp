@@ -14,6 +14,7 @@ namespace lmr { struct StageState; void stage_state_free(StageState* s); void st
 namespace lmr { struct XState; void xstate_free(XState* x); }
 namespace lmr { struct WinState; void win_state_free(WinState* w); }
 namespace lmr { struct WireBufs; void wire_bufs_free(WireBufs* b); }
+namespace lmr { struct OrdBufs; void ord_bufs_free(OrdBufs* b); }
 
 struct lmr_ctx {
     int device = 0;
@@ -29,6 +30,7 @@ struct lmr_ctx {
     lmr::XState* xch = nullptr;        // multi-PE exchange state (lmr_batch_exchange), lazily made
     lmr::WinState* win = nullptr;      // window partition of shards above one tiled window, lazily made
     lmr::WireBufs* wire = nullptr;     // staging of lmr_apply_msg (AM wire format), lazily made
+    lmr::OrdBufs* ord = nullptr;       // sort buffers of the ordered apply (n > 1024), lazily made
 };
 
 namespace lmr {
@@ -118,6 +120,9 @@ struct ApplyArgs {
 // launchers (dtype-dispatching), defined in lmr_apply.hip
 hipError_t launch_apply_direct(int dtype, int index_size, const ApplyArgs& a, hipStream_t s);
 hipError_t launch_apply_mvsi(int dtype, const ApplyArgs& a, uint64_t index, hipStream_t s);
+// LMR_STRATEGY_ORDERED (lmr_ordered.hip): per element in record order, one atomic block each
+hipError_t launch_apply_ordered(lmr_ctx* ctx, int dtype, int index_size, const ApplyArgs& a, hipStream_t s);
+constexpr uint64_t kOrderedAuto = 1000;   // AUTO: below this many records (one reference AM at 1 PE)
 // tiled apply of SoA/AoS records; returns hipErrorNotSupported when the shard
 // is too large for the single-level tile histogram.
 hipError_t launch_apply_tiled(int dtype, int index_size, const ApplyArgs& a, const TiledWs& w,
@@ -201,6 +206,12 @@ hipError_t launch_scatter_results(const uint8_t* in, const uint32_t* pos, uint64
                                   uint8_t* ok_out, Prof* prof, hipStream_t s);
 hipError_t apply_windowed(lmr_ctx* ctx, const lmr_apply_desc_t* d, const ApplyArgs& a, int iw, hipStream_t s,
                           const WindowApplyFn& apply_one);
+
+// The index width of an op AM's index_size byte: 1, 2, 4 or 8, and usize (8) for any other value,
+// as the generated apply bodies' `_ =>` arm reads them (impl/src/array_ops.rs:867-897).
+inline uint32_t am_index_width(uint32_t index_size) {
+    return (index_size == 1 || index_size == 2 || index_size == 4) ? index_size : 8u;
+}
 
 inline int dtype_bytes(int d) {
     switch (d) {

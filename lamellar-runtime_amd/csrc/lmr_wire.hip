@@ -149,8 +149,7 @@ lmr_status_t lmr_am_decode(const uint8_t* body, uint64_t len, uint32_t shape, ui
     if (shape == LMR_SHAPE_MVSI) v.index = r.uint(8);
     else v.index_size = uint32_t(r.uint(1));
     if (!r.ok) return LMR_E_LENGTH;
-    if (shape != LMR_SHAPE_MVSI && v.index_size != 1 && v.index_size != 2 && v.index_size != 4 && v.index_size != 8)
-        return LMR_E_INVALID;
+    if (shape != LMR_SHAPE_MVSI) v.index_size = am_index_width(v.index_size);   // `_ =>`: usize records
     v.body_bytes = r.pos;
     *out = v;
     return LMR_OK;
@@ -207,8 +206,21 @@ lmr_status_t lmr_msg_parse(const uint8_t* msg, uint64_t len, lmr_am_resolver_t r
             e.req_id = r.uint(8);
             e.req_sub_id = r.uint(8);
             if (!r.ok) return LMR_E_LENGTH;
-            if (c == LMR_CMD_RETURN_AM || !resolve || resolve(user, e.am_id, &e.shape, &e.kind, &e.dtype) != 0)
-                return LMR_E_UNSUPPORTED;                // not an op AM: its size is unknown here
+            uint64_t fb = 0;
+            const int rc = resolve ? resolve(user, c, e.am_id, msg + r.pos, len - r.pos, &e.shape, &e.kind, &e.dtype, &fb)
+                                   : 2;
+            if (rc == 1) {                               // a ReturnAm / user AM, sized by the runtime
+                if (fb > len - r.pos) return LMR_E_LENGTH;
+                e.shape = LMR_SHAPE_FOREIGN;
+                e.kind = e.dtype = 0;
+                e.body_offset = r.pos;
+                e.body_bytes = fb;
+                r.skip(fb);
+                add(e);
+                return LMR_OK;
+            }
+            if (rc != 0 || c == LMR_CMD_RETURN_AM || e.shape > LMR_SHAPE_MVSI)
+                return LMR_E_UNSUPPORTED;                // unknown: its serialized size is unknown here
             lmr_am_view_t v;
             lmr_status_t st = lmr_am_decode(msg + r.pos, len - r.pos, e.shape, e.kind, e.dtype, &v);
             if (st != LMR_OK) return st;
@@ -332,7 +344,7 @@ lmr_status_t lmr_apply_msg(lmr_ctx_t* ctx, const uint8_t* msg, uint64_t len, lmr
     std::vector<AmJob> jobs;
     std::vector<Group> groups;
     for (uint32_t e = 0; e < ne; e++) {
-        if (ent[e].cmd != LMR_CMD_AM) continue;
+        if (ent[e].cmd != LMR_CMD_AM || ent[e].shape == LMR_SHAPE_FOREIGN) continue;
         AmJob j;
         j.entry = e;
         st = lmr_am_decode(msg + ent[e].body_offset, len - ent[e].body_offset, ent[e].shape, ent[e].kind,
@@ -438,8 +450,8 @@ lmr_status_t lmr_apply_msg(lmr_ctx_t* ctx, const uint8_t* msg, uint64_t len, lmr
             B->dcap = need + need / 4;
         }
     }
-    // the previous call's copies out of the staging buffer are complete (it returned
-    // after syncing); fill records
+    // the previous call's copies out of the staging buffer are complete (every return after
+    // its first copy waited for the stream); fill records
     uint8_t* H = static_cast<uint8_t*>(B->h);
     uint8_t* D = static_cast<uint8_t*>(B->d);
     for (const AmJob& j : jobs) {
@@ -461,6 +473,12 @@ lmr_status_t lmr_apply_msg(lmr_ctx_t* ctx, const uint8_t* msg, uint64_t len, lmr
             memcpy(H + G.h_val, recs, size_t(j.n * uint64_t(eb)));
         }
     }
+    // from the first queued copy on, every return waits for the stream: the next call refills H
+    struct SyncOnExit {
+        hipStream_t s;
+        bool armed = true;
+        ~SyncOnExit() { if (armed) (void)hipStreamSynchronize(s); }
+    } drain{s};
     if (in_bytes && hipMemcpyAsync(D, H, in_bytes, hipMemcpyHostToDevice, s) != hipSuccess) return LMR_E_HIP;
     uint8_t* Dout = D + in_bytes;
     for (const Group& G : groups) {
@@ -479,6 +497,7 @@ lmr_status_t lmr_apply_msg(lmr_ctx_t* ctx, const uint8_t* msg, uint64_t len, lmr
     }
     if (out_bytes && hipMemcpyAsync(H + in_bytes, Dout, out_bytes, hipMemcpyDeviceToHost, s) != hipSuccess)
         return LMR_E_HIP;
+    drain.armed = false;
     if (hipStreamSynchronize(s) != hipSuccess) return LMR_E_HIP;
     // ---- replies
     const uint8_t* Hout = H + in_bytes;

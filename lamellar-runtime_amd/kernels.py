@@ -315,19 +315,24 @@ class DeviceKernels:
 
     def apply_msg(self, msg: bytes, resolve, shard_of, max_entries=1 << 16):
         """lmr_apply_msg over one lamellae message (single AM or batched) in host memory.
-        resolve(am_id) -> (shape, kind, dtype code) of a registered op AM, or None;
-        shard_of(view) -> (device tensor, shard_len, strategy) for a decoded AM, or None
-        to skip it. Returns {entry index: reply bytes} for the returning AMs."""
+        resolve(am_id) -> (shape, kind, dtype code) of a registered op AM, the serialized
+        body size (int) of another AM (a ReturnAm, a user AM: left to the runtime), or None
+        (unknown: the message is refused); shard_of(view) -> (device tensor, shard_len,
+        strategy) for a decoded AM, or None to skip it. Returns {entry index: reply bytes}
+        for the returning AMs."""
         self.flush()
         errs = []
 
-        def res_cb(_user, am_id, shape, kind, dtype):
+        def res_cb(_user, _cmd, am_id, _body, _avail, shape, kind, dtype, body_bytes):
             try:
                 r = resolve(int(am_id))
             except Exception as e:  # noqa: BLE001 - reported after the C call
                 errs.append(e)
-                return 1
+                return 2
             if r is None:
+                return 2
+            if isinstance(r, int):
+                body_bytes[0] = r
                 return 1
             shape[0], kind[0], dtype[0] = (int(x) for x in r)
             return 0

@@ -63,6 +63,7 @@ class Strategy(enum.IntEnum):
     Auto = 0
     Direct = 1
     Tiled = 2
+    Ordered = 3
 
 
 class LmrStatus(enum.IntEnum):

@@ -263,7 +263,7 @@ class LamellarWorldBuilder:
             strategy = self._strategy
             if strategy is None:
                 strategy = {"auto": Strategy.Auto, "direct": Strategy.Direct,
-                            "tiled": Strategy.Tiled}[os.environ.get("LAMELLAR_OP_STRATEGY", "auto")]
+                            "tiled": Strategy.Tiled, "ordered": Strategy.Ordered}[os.environ.get("LAMELLAR_OP_STRATEGY", "auto")]
             kernels = DeviceKernels(device, strategy=strategy)
         team = LamellarTeam(world_size, rank, device, kernels, group)
         return LamellarWorld(team)

@@ -1,6 +1,6 @@
 """Messages from the running runtime applied on the device (lmr_apply_msg): one batched
 lamellae message of 220 small op AMs (MVMI / SVMI / MVSI, four ops, three arrays, plus
-Data and Unit entries) encoded by oracle/wire.py, applied with the AMs of one (array, op,
+Data and Unit entries, a user AM and a ReturnAm) encoded by oracle/wire.py, applied with the AMs of one (array, op,
 operands) aggregated into one record stream, replies decoded and checked: final states
 against the oracle (order-insensitive ops), returned values against the linearizability
 checker (order-dependent ops), and the launch count against the number of groups."""
@@ -69,6 +69,12 @@ def test_batched_message_of_small_ams(world, orc):
         meta[-1] = (203, meta[-1][2], vals)
     entries.append(("unit", 6, 2))
     meta.append(None)
+    # a user AM and a ReturnAm among the op AMs (simple_batcher.rs:276-304): the resolver sizes
+    # them (the runtime's deserializer would), the library steps over them and leaves them be
+    entries.append(("am", 300, 0x77, 9000, 0, bytes(range(45))))
+    meta.append(None)
+    entries.append(("return_am", 301, 0x77, 9001, 0, bytes(19)))
+    meta.append(None)
     for j in range(30):
         vals = rng.integers(-8, 8, 30).astype(np.float64)
         am(204, 0xB000, wire.SHAPE_MVMI, 8, 1, rng.integers(100, 300, 30), f64bits(vals))
@@ -85,13 +91,14 @@ def test_batched_message_of_small_ams(world, orc):
     k.profile(True)
     k.profile_read(reset=True)
     try:
-        replies = k.apply_msg(msg, lambda am_id: reg.get(am_id), shard_of)
+        replies = k.apply_msg(msg, lambda am_id: {300: 45, 301: 19}.get(am_id, reg.get(am_id)), shard_of)
         stages = k.profile_read(reset=True)
     finally:
         k.profile(False)
     assert k.errors() == 0
-    # aggregation: one apply per (array, op, operands, value) group, one per MVSI AM
-    assert stages["direct"][1] == 5, stages
+    # aggregation: one apply per (array, op, operands, value) group, one per MVSI AM; groups
+    # below 1000 records (204, 205, 206) take the ordered path (AUTO), the others direct atomics
+    assert stages["direct"][1] == 2 and stages["ordered"][1] == 3, stages
     assert stages["mvsi"][1] == 10, stages
     A = shards[0xA000][0].cpu().numpy().view(np.uint64)
     B = shards[0xB000][0].cpu().numpy().view(np.float64)

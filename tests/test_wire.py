@@ -98,7 +98,8 @@ def test_am_decode_rejects_bad_fields(capi):
     body = wire.am_body(wire.SHAPE_MVMI, wire.KIND_NATIVE, 8, h, 40, b"", index_size=4)
     assert _view(capi, body, wire.SHAPE_MVMI, wire.KIND_NATIVE, 3)[0] == LMR_E_INVALID     # op tag
     body = wire.am_body(wire.SHAPE_MVMI, wire.KIND_NATIVE, 8, h, 0, b"", index_size=3)
-    assert _view(capi, body, wire.SHAPE_MVMI, wire.KIND_NATIVE, 3)[0] == LMR_E_INVALID     # index width
+    st, v = _view(capi, body, wire.SHAPE_MVMI, wire.KIND_NATIVE, 3)                       # index width 3:
+    assert st == 0 and v.index_size == 8                                                  # usize (`_ =>`)
     assert _view(capi, body, 3, wire.KIND_NATIVE, 3)[0] == LMR_E_INVALID                   # shape
     assert _view(capi, body, 0, 6, 3)[0] == LMR_E_INVALID                                  # kind
 
@@ -107,12 +108,18 @@ REG = {101: (wire.SHAPE_MVMI, wire.KIND_NATIVE, 3), 102: (wire.SHAPE_SVMI, wire.
        103: (wire.SHAPE_MVSI, wire.KIND_LOCAL_LOCK, 2)}
 
 
+USER = {}          # am_id -> serialized body size of a non-op AM (the runtime's deserializer knows it)
+
+
 def _resolver():
     from lamellar_runtime_amd import _capi
 
-    def res(_user, am_id, shape, kind, dtype):
-        if am_id not in REG:
+    def res(_user, _cmd, am_id, _body, _avail, shape, kind, dtype, body_bytes):
+        if am_id in USER:
+            body_bytes[0] = USER[am_id]
             return 1
+        if am_id not in REG:
+            return 2
         shape[0], kind[0], dtype[0] = REG[am_id]
         return 0
     return _capi.AM_RESOLVER_FN(res)
@@ -184,10 +191,44 @@ def test_msg_parse_batched_with_data_and_unit(capi):
     assert st == LMR_E_LENGTH and n2 == len(entries)
 
 
+def test_msg_parse_user_and_return_ams(capi):
+    """A batched message as the SimpleBatcher builds it (simple_batcher.rs:276-304): op AMs
+    mixed with user AMs and ReturnAms (sized by the resolver, reported as LMR_SHAPE_FOREIGN),
+    Data and Unit entries; every entry parsed in order."""
+    rng = np.random.default_rng(8)
+    bodies = _bodies(rng)
+    USER.clear()
+    USER.update({500: 37, 501: 0, 502: 200})
+    entries = [("am", bodies[0][0], 1, 10, 0, bodies[0][1]),
+               ("am", 500, 2, 11, 0, bytes(rng.integers(0, 256, 37, dtype=np.uint8))),
+               ("return_am", 502, 3, 12, 1, bytes(200)),
+               ("unit", 13, 0),
+               ("am", 501, 4, 14, 0, b""),
+               ("am", bodies[1][0], 5, 15, 0, bodies[1][1]),
+               ("data", 16, 2, b"", b"zz")]
+    msg = wire.message_batched(4, entries)
+    try:
+        st, ents, n = _parse(capi, msg)
+    finally:
+        USER.clear()
+    assert st == 0 and n == len(entries)
+    assert [e.cmd for e in ents] == [0, 0, 1, 3, 0, 0, 2]
+    assert [e.shape for e in ents[:3]] == [REG[bodies[0][0]][0], 3, 3] and ents[4].shape == 3
+    assert (ents[1].am_id, ents[1].body_bytes, ents[2].am_id, ents[2].body_bytes) == (500, 37, 502, 200)
+    assert bytes(msg[ents[1].body_offset:ents[1].body_offset + 37]) == entries[1][5]
+    assert ents[5].body_bytes == len(bodies[1][1]) and ents[5].shape == REG[bodies[1][0]][0]
+    # a foreign AM claiming more bytes than the message holds
+    USER[500] = 10 ** 6
+    try:
+        assert _parse(capi, msg)[0] == LMR_E_LENGTH
+    finally:
+        USER.clear()
+
+
 def test_msg_parse_errors(capi):
     rng = np.random.default_rng(7)
     am_id, body = _bodies(rng)[0]
-    # a return AM / an unregistered AM: its size is unknown here
+    # a return AM the resolver does not size / an unknown AM: its size is unknown here
     msg = wire.message_batched(0, [("return_am", am_id, 1, 2, 3, body)])
     assert _parse(capi, msg)[0] == LMR_E_UNSUPPORTED
     assert _parse(capi, wire.message_single(0, 999, 1, 2, 3, body))[0] == LMR_E_UNSUPPORTED
