@@ -16,11 +16,15 @@ input, every PE (one per GPU) issuing its own batch (weak scaling):
       compare_exchange), 2^30 / 8 records per PE split in equal fifths.
 value = ops applied by all PEs / max-over-PEs wall time of the timed steps.
 
-roofline: the dominant kernel's algorithmic HBM bytes per launch / its average
-launch time (HIP events recorded by the library on the launch stream), against
-the 8.0 TB/s HBM3E peak. cpu_baseline: the reference-structured threaded CPU
-apply (oracle/cpu_baseline.c, a restatement of the Rust path: the reference
-itself cannot be built here) on a bounded sample, rank 0, N = 1.
+roofline: op-level, for the whole step: SURVEY 8(d)'s algorithmic bytes per op
+(packed record + element read and write [+ returned value]) x ops per step / the
+step time, against the 8.0 TB/s HBM3E peak; `traffic` is the HBM bytes per step
+from the committed rocprofv3 PMC passes. Each kernel stage's own algorithmic bytes
+over its average launch time (HIP events the library records on the launch
+stream) are under apply_pipeline.stages. cpu_baseline: the reference-structured
+threaded CPU apply (oracle/cpu_baseline.c, a restatement of the Rust path: the
+reference itself cannot be built here) on a bounded sample, rank 0, N = 1, with
+3 warm-up runs; extra lines for T = 4, C1 and the 8-PE shared-memory C4 shape.
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c3|c5]
        python -m torch.distributed.run --nproc-per-node N bench.py --gpus N ...
@@ -310,8 +314,9 @@ def cpu_threads():
     return n
 
 
-def _timed(orc, reps, run):
-    run(True)                                              # warm-up (page-in, thread spin-up)
+def _timed(orc, reps, run, warm=3):
+    for _ in range(warm):                                  # 3 full-size warm-up runs
+        run(False)
     ts = sorted(run(False) for _ in range(reps))
     return ts[len(ts) // 2], ts
 
@@ -333,10 +338,9 @@ def cpu_baseline(args, cfg):
             init=None):
         shard = np.zeros(shard_len, dtype=npt) if init is None else init
 
-        def run(warm):
-            n = (1 << 16) if warm else gidx.size
-            st, t, _ = orc.cpu_baseline(dtype, npt, op, shard, gidx[:n], vals if np.ndim(vals) == 0 else vals[:n],
-                                        threads, threshold, want_results=results, current=cur)
+        def run(_warm):
+            st, t, _ = orc.cpu_baseline(dtype, npt, op, shard, gidx, vals, threads, threshold, want_results=results,
+                                        current=cur)
             assert st == 0
             return t.total_s
         med, ts = _timed(orc, reps, run)
@@ -374,6 +378,28 @@ def cpu_baseline(args, cfg):
                              "sample": f"C1 as add_test issues it: per-element add(idx, 1), one 1-record op "
                                        f"buffer per op (2^18 ops; a lower bound on the reference's per-AM "
                                        f"cost), median of 5 ({med11 * 1e3:.0f} ms)"})
+        # C4 (configs[3]): 8 PEs on one node exchanging op buffers through shared memory, the
+        # shmem lamellae's command-queue protocol restated (oracle/cpu_baseline.c), T / 8 threads each
+        P = 8
+        tpe = max(1, T // P)
+        n4p = 1 << max(16, args.cpu_sample_log2 - 4)
+        alen = P * el
+        L4 = orc.layout_new(alen, P, 0, 0)
+        shards = [np.zeros(orc.num_elems_pe(L4, p), dtype=np.uint64) for p in range(P)]
+        g4 = [rng.integers(0, alen, n4p, dtype=np.uint64) for _ in range(P)]
+        v4s = [rng.integers(0, 2**63, n4p, dtype=np.uint64) for _ in range(P)]
+
+        def run4(_warm):
+            st, t = orc.cpu_baseline_multi_pe(3, np.uint64, 0, alen, shards, g4, v4s, tpe)
+            assert st == 0
+            return t.total_s
+        med4p, _ = _timed(orc, 5, run4)
+        out["extra"].append({"value": P * n4p / med4p, "unit": "ops/s", "cores": P * tpe, "kind": "port",
+                             "sample": f"C4 (configs[3]) shape: {P} PEs x {tpe} threads, 2^{n4p.bit_length() - 1} "
+                                       f"u64 add records per PE uniform over a {P} x 2^{args.elems_log2 or 26}-element "
+                                       f"Block array, op buffers exchanged through shared memory with the shmem "
+                                       f"lamellae's checksummed command queues (restated), median of 5 "
+                                       f"({med4p * 1e3:.0f} ms)"})
     elif cfg == "c3":
         el = 1 << (args.elems_log2 or 24)
         n = 1 << 22

@@ -221,3 +221,223 @@ int cpu_baseline_run(uint32_t dtype, uint32_t op, void* shard, uint64_t shard_le
     free(th); free(ta); free(j->bytes); free(j->buf_start); free(j->locks); free(j);
     return st;
 }
+
+/* ------------------------------------------------------------------------------------
+ * C4: P PEs on one node exchanging op buffers through shared memory, as the
+ * shmem lamellae does (lamellar_run.sh:31-40 starts one process per PE). Each PE is a group
+ * of threads here (every PE's memory is visible to every other, like the /dev/shm
+ * segments); per PE:
+ *  - packers (max(1, T/4) chunks, operations.rs:462-480) map each global index to (PE,
+ *    offset) (unsafe.rs:1610-1647) and append IdxVal records to per-destination op buffers
+ *    of am_size_threshold bytes (unsafe/operations.rs:663-811), allocated in the sender's
+ *    own segment; a full buffer is sent: to the PE itself it is queued as is (the dst == src
+ *    shortcut, registered_active_message.rs:150-154), to another PE a CmdMsg {addr, size,
+ *    hash} goes into the destination's command queue with the additive checksum of the
+ *    bytes (command_queues.rs:26-35, 63-94, 725-807);
+ *  - every thread of the PE, once its packing is done, serves the PE's queue: a remote
+ *    buffer is copied out of the sender's segment and its checksum verified (get_data,
+ *    command_queues.rs:996-1021, 1395-1531), then its records are applied with SeqCst
+ *    atomics (the NativeAtomic apply above).
+ * The step ends when every PE has applied every buffer addressed to it.
+ * ------------------------------------------------------------------------------------ */
+typedef struct {
+    const uint8_t* addr;
+    uint64_t bytes;
+    uint64_t hash;       /* 0 for the dst == src shortcut (no copy, no check) */
+} cmd_msg_t;
+
+typedef struct {
+    pthread_mutex_t mu;
+    cmd_msg_t* q;
+    uint64_t head, tail, cap;
+} cmd_queue_t;
+
+typedef struct mpe_s mpe_t;
+typedef struct {
+    mpe_t* m;
+    uint32_t pe;
+    uint8_t* seg;             /* this PE's segment: op buffers are carved from it */
+    uint64_t seg_used;        /* bump pointer (atomic) */
+    uint64_t seg_cap;
+    void* shard;
+    cmd_queue_t queue;
+    const uint64_t* gidx;
+    const uint8_t* vals;
+    uint64_t n;
+    uint32_t packers;
+} mpe_pe_t;
+
+struct mpe_s {
+    uint32_t npes, tpe, dtype, op, index_size, rb, vo, tb;
+    lmr_layout_t L;
+    uint64_t per_batch;       /* records per op buffer */
+    mpe_pe_t* pe;
+    uint32_t packers_left;    /* atomic: packing threads still running, over all PEs */
+    uint64_t sent, applied;   /* atomic buffer counts */
+    int status;
+};
+
+typedef struct { mpe_t* m; uint32_t pe, t; } mpe_arg_t;
+
+static uint64_t add_hash(const uint8_t* p, uint64_t len) {
+    uint64_t s = 0, w;
+    uint64_t k = 0;
+    for (; k + 8 <= len; k += 8) { memcpy(&w, p + k, 8); s += w; }
+    for (; k < len; k++) s += p[k];
+    return s;
+}
+
+static void q_push(cmd_queue_t* q, cmd_msg_t c) {
+    pthread_mutex_lock(&q->mu);
+    if (q->tail == q->cap) {
+        uint64_t nc = q->cap ? 2 * q->cap : 1024;
+        cmd_msg_t* nq = (cmd_msg_t*)realloc(q->q, nc * sizeof(cmd_msg_t));
+        if (nq) { q->q = nq; q->cap = nc; }
+    }
+    if (q->tail < q->cap) q->q[q->tail++] = c;
+    pthread_mutex_unlock(&q->mu);
+}
+
+static int q_pop(cmd_queue_t* q, cmd_msg_t* c) {
+    int got = 0;
+    pthread_mutex_lock(&q->mu);
+    if (q->head < q->tail) { *c = q->q[q->head++]; got = 1; }
+    pthread_mutex_unlock(&q->mu);
+    return got;
+}
+
+static void mpe_send(mpe_t* m, uint32_t src, uint32_t dst, const uint8_t* buf, uint64_t bytes) {
+    cmd_msg_t c = {buf, bytes, src == dst ? 0 : add_hash(buf, bytes)};
+    __atomic_fetch_add(&m->sent, 1, __ATOMIC_SEQ_CST);
+    q_push(&m->pe[dst].queue, c);
+}
+
+static void mpe_apply_buf(mpe_t* m, mpe_pe_t* P, const uint8_t* recs, uint64_t bytes) {
+    const uint64_t nr = bytes / m->rb;
+    for (uint64_t k = 0; k < nr; k++) {
+        const uint8_t* r = recs + k * m->rb;
+        uint64_t idx = 0;
+        memcpy(&idx, r, m->index_size);
+        const uint8_t* vp = r + m->vo;
+#define MDO(D, NAME, T) case D: { T v; memcpy(&v, vp, sizeof(T)); (void)native_##NAME((T*)P->shard + idx, v, m->op, 0); break; }
+        switch (m->dtype) {
+        MDO(LMR_U8, u8, uint8_t) MDO(LMR_U16, u16, uint16_t) MDO(LMR_U32, u32, uint32_t)
+        MDO(LMR_U64, u64, uint64_t) MDO(LMR_I8, i8, int8_t) MDO(LMR_I16, i16, int16_t)
+        MDO(LMR_I32, i32, int32_t) MDO(LMR_I64, i64, int64_t)
+        default: break;
+        }
+#undef MDO
+    }
+}
+
+static void* mpe_thread(void* p) {
+    mpe_arg_t* a = (mpe_arg_t*)p;
+    mpe_t* m = a->m;
+    mpe_pe_t* P = &m->pe[a->pe];
+    const uint64_t bb = m->per_batch * m->rb;
+    if (a->t < P->packers) {
+        /* pack chunk t of this PE's input (operations.rs:462-480) */
+        const uint64_t per = P->n / P->packers;
+        const uint64_t lo = a->t * per, hi = (a->t + 1 == P->packers) ? P->n : lo + per;
+        uint8_t** cur = (uint8_t**)calloc(m->npes, sizeof(uint8_t*));
+        uint64_t* fill = (uint64_t*)calloc(m->npes, sizeof(uint64_t));
+        for (uint64_t k = lo; k < hi; k++) {
+            uint64_t pe = 0, off = 0;
+            if (!orc_pe_and_offset(&m->L, P->gidx[k], &pe, &off)) { m->status = LMR_E_OOB; continue; }
+            if (!cur[pe]) {
+                const uint64_t at = __atomic_fetch_add(&P->seg_used, bb, __ATOMIC_RELAXED);
+                if (at + bb > P->seg_cap) { m->status = LMR_E_WORKSPACE; continue; }
+                cur[pe] = P->seg + at;
+                fill[pe] = 0;
+            }
+            uint8_t* r = cur[pe] + fill[pe] * m->rb;
+            memcpy(r, &off, m->index_size);
+            memcpy(r + m->vo, P->vals + k * m->tb, m->tb);
+            if (++fill[pe] == m->per_batch) {
+                mpe_send(m, a->pe, (uint32_t)pe, cur[pe], bb);
+                cur[pe] = NULL;
+            }
+        }
+        for (uint32_t pe = 0; pe < m->npes; pe++)
+            if (cur[pe] && fill[pe]) mpe_send(m, a->pe, pe, cur[pe], fill[pe] * m->rb);
+        free(cur);
+        free(fill);
+        __atomic_fetch_sub(&m->packers_left, 1, __ATOMIC_SEQ_CST);
+    }
+    /* serve this PE's command queue until every buffer of every PE is applied */
+    uint8_t* local = (uint8_t*)malloc(bb);
+    for (;;) {
+        cmd_msg_t c;
+        if (q_pop(&P->queue, &c)) {
+            const uint8_t* src = c.addr;
+            if (c.hash) {                                   /* remote: get_data + checksum */
+                memcpy(local, c.addr, c.bytes);
+                if (add_hash(local, c.bytes) != c.hash) m->status = LMR_E_INVALID;
+                src = local;
+            }
+            mpe_apply_buf(m, P, src, c.bytes);
+            __atomic_fetch_add(&m->applied, 1, __ATOMIC_SEQ_CST);
+            continue;
+        }
+        if (__atomic_load_n(&m->packers_left, __ATOMIC_SEQ_CST) == 0 &&
+            __atomic_load_n(&m->applied, __ATOMIC_SEQ_CST) == __atomic_load_n(&m->sent, __ATOMIC_SEQ_CST))
+            break;
+        sched_yield();
+    }
+    free(local);
+    return NULL;
+}
+
+int cpu_baseline_multi_pe(uint32_t dtype, uint32_t op, uint32_t npes, uint32_t threads_per_pe, uint64_t array_len,
+                          void* const* shards, const uint64_t* const* gidx, const void* const* vals, uint64_t n_per_pe,
+                          uint64_t am_size_threshold, cpu_times_t* out) {
+    if (npes == 0 || npes > 64 || threads_per_pe == 0 || dtype >= LMR_F32 || orc_op_ret_kind(op) != LMR_RET_NONE)
+        return LMR_E_INVALID;
+    mpe_t* m = (mpe_t*)calloc(1, sizeof(mpe_t));
+    if (!m) return LMR_E_WORKSPACE;
+    m->npes = npes; m->tpe = threads_per_pe; m->dtype = dtype; m->op = op;
+    orc_layout_new(&m->L, array_len, npes, 0, LMR_DIST_BLOCK);
+    m->index_size = orc_index_size(&m->L);
+    m->tb = orc_dtype_bytes(dtype);
+    m->rb = orc_record_bytes(m->index_size, dtype);
+    m->vo = orc_record_val_offset(m->index_size, dtype);
+    m->per_batch = (uint64_t)ceilf((float)am_size_threshold / (float)m->rb);
+    if (m->per_batch == 0) m->per_batch = 1;
+    m->pe = (mpe_pe_t*)calloc(npes, sizeof(mpe_pe_t));
+    const uint32_t packers = threads_per_pe / 4 ? threads_per_pe / 4 : 1;
+    int st = LMR_OK;
+    for (uint32_t p = 0; p < npes && m->pe; p++) {
+        mpe_pe_t* P = &m->pe[p];
+        P->m = m; P->pe = p; P->shard = shards[p]; P->gidx = gidx[p];
+        P->vals = (const uint8_t*)vals[p]; P->n = n_per_pe;
+        P->packers = n_per_pe < 1000 ? 1 : packers;
+        /* every packer may leave one partial buffer per destination */
+        P->seg_cap = (n_per_pe / m->per_batch + (uint64_t)P->packers * npes + 2) * m->per_batch * m->rb;
+        P->seg = (uint8_t*)malloc(P->seg_cap);
+        pthread_mutex_init(&P->queue.mu, NULL);
+        if (!P->seg) st = LMR_E_WORKSPACE;
+        m->packers_left += P->packers;
+    }
+    const uint32_t nt = npes * threads_per_pe;
+    pthread_t* th = (pthread_t*)malloc(nt * sizeof(pthread_t));
+    mpe_arg_t* ta = (mpe_arg_t*)malloc(nt * sizeof(mpe_arg_t));
+    if (!m->pe || !th || !ta) st = LMR_E_WORKSPACE;
+    if (st == LMR_OK) {
+        const double t0 = now_s();
+        for (uint32_t i = 0; i < nt; i++) {
+            ta[i].m = m; ta[i].pe = i / threads_per_pe; ta[i].t = i % threads_per_pe;
+            pthread_create(&th[i], NULL, mpe_thread, &ta[i]);
+        }
+        for (uint32_t i = 0; i < nt; i++) pthread_join(th[i], NULL);
+        const double t1 = now_s();
+        if (out) { out->pack_s = 0; out->apply_s = t1 - t0; out->total_s = t1 - t0; out->n_buffers = m->sent; }
+        st = m->status;
+    }
+    for (uint32_t p = 0; m->pe && p < npes; p++) {
+        free(m->pe[p].seg);
+        free(m->pe[p].queue.q);
+        pthread_mutex_destroy(&m->pe[p].queue.mu);
+    }
+    free(th); free(ta); free(m->pe); free(m);
+    return st;
+}

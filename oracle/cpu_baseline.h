@@ -38,6 +38,14 @@ int cpu_baseline_run(uint32_t dtype, uint32_t op, void* shard, uint64_t shard_le
                      uint32_t threads, uint64_t am_size_threshold, const void* cmp, void* results,
                      cpu_times_t* out);
 
+/* C4: npes PEs (Block layout over array_len elements) of threads_per_pe threads each,
+ * exchanging op buffers through shared memory with the shmem lamellae's command-queue
+ * protocol restated (see cpu_baseline.c); ops that return nothing, integer types. shards[p]
+ * = PE p's shard (num_elems_pe elements), gidx[p] / vals[p] = PE p's n_per_pe records. */
+int cpu_baseline_multi_pe(uint32_t dtype, uint32_t op, uint32_t npes, uint32_t threads_per_pe, uint64_t array_len,
+                          void* const* shards, const uint64_t* const* gidx, const void* const* vals, uint64_t n_per_pe,
+                          uint64_t am_size_threshold, cpu_times_t* out);
+
 #ifdef __cplusplus
 }
 #endif

@@ -85,6 +85,8 @@ def lib():
             "cpu_baseline_run": (c_int, [c_uint32, c_uint32, c_void_p, c_uint64, c_void_p, c_void_p,
                                          c_void_p, c_uint64, c_uint32, c_uint64, c_void_p, c_void_p,
                                          POINTER(CpuTimes)]),
+            "cpu_baseline_multi_pe": (c_int, [c_uint32, c_uint32, c_uint32, c_uint32, c_uint64, c_void_p,
+                                              c_void_p, c_void_p, c_uint64, c_uint64, POINTER(CpuTimes)]),
         }
         for k, (r, a) in sig.items():
             f = getattr(l, k)
@@ -237,6 +239,26 @@ def cpu_baseline(dtype_code, np_dtype, op, shard, gidx, vals, threads, threshold
     st = lib().cpu_baseline_run(dtype_code, op, shard.ctypes.data, shard.size, _ptr(gidx), _ptr(v),
                                 _ptr(sv), n, threads, threshold, _ptr(c), _ptr(res), ctypes.byref(t))
     return st, t, res
+
+
+def cpu_baseline_multi_pe(dtype_code, np_dtype, op, array_len, shards, gidx, vals, threads_per_pe,
+                          threshold=100000):
+    """C4 CPU baseline (bench.py cpu_baseline leg): len(shards) PEs of threads_per_pe threads
+    exchanging op buffers through shared memory (the shmem lamellae's protocol restated,
+    cpu_baseline.c). shards[p] is updated in place; gidx[p] / vals[p] are PE p's records
+    (equal counts)."""
+    P = len(shards)
+    n = int(gidx[0].size)
+    gidx = [np.ascontiguousarray(g, dtype=np.uint64) for g in gidx]
+    vals = [np.ascontiguousarray(np.asarray(v).astype(np_dtype)) for v in vals]
+    assert all(g.size == n for g in gidx) and all(v.size == n for v in vals)
+    arr_p = (ctypes.c_void_p * P)(*[s.ctypes.data for s in shards])
+    arr_g = (ctypes.c_void_p * P)(*[g.ctypes.data for g in gidx])
+    arr_v = (ctypes.c_void_p * P)(*[v.ctypes.data for v in vals])
+    t = CpuTimes()
+    st = lib().cpu_baseline_multi_pe(dtype_code, op, P, threads_per_pe, array_len, arr_p, arr_g, arr_v, n,
+                                     threshold, ctypes.byref(t))
+    return st, t
 
 
 def check_linearizable(kind, dtype_code, np_dtype, op, init, final, idx, vals, rets=None, oks=None,
