@@ -141,6 +141,8 @@ SIGNATURES = {
     "lmr_reduce": (c_int, [c_void_p, c_uint32, c_uint32, c_void_p, c_uint64, c_void_p, c_void_p, c_void_p]),
     "lmr_pack_unordered": (c_int, [c_void_p, POINTER(lmr_layout_t), c_void_p, c_uint64, c_void_p, c_uint32,
                                    c_uint32, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
+    "lmr_pack_regions": (c_int, [c_void_p, POINTER(lmr_layout_t), c_void_p, c_uint64, c_void_p, c_uint32,
+                                 c_uint32, c_void_p, c_void_p, c_uint64, c_void_p, c_void_p, c_void_p]),
     "lmr_apply_mvmi": (c_int, [c_void_p, POINTER(lmr_apply_desc_t), c_void_p, c_uint64, c_uint32,
                                c_void_p, c_void_p, c_void_p]),
     "lmr_apply_svmi": (c_int, [c_void_p, POINTER(lmr_apply_desc_t), c_void_p, c_void_p, c_uint64,

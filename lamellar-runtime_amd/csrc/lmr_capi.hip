@@ -557,6 +557,33 @@ lmr_status_t lmr_pack_unordered(lmr_ctx_t* ctx, const lmr_layout_t* layout, cons
                        d_dest_counts, d_dest_offsets, false, stream);
 }
 
+lmr_status_t lmr_pack_regions(lmr_ctx_t* ctx, const lmr_layout_t* layout, const uint64_t* d_gidx, uint64_t n,
+                              const void* d_vals, uint32_t dtype, uint32_t index_size, void* d_out_idx,
+                              void* d_out_vals, uint64_t region_cap, uint32_t* d_fill, uint64_t* d_dest_counts,
+                              lmr_stream_t stream) {
+    if (!ctx || !valid_layout(layout) || !valid_iw(index_size) || dtype >= LMR_NUM_DTYPES || !d_fill ||
+        !d_dest_counts || n > 0xFFFFFFFFull || layout->num_pes > uint32_t(kMaxPackPes) || region_cap == 0 ||
+        uint64_t(layout->num_pes) * region_cap > 0xFFFFFFFFull)
+        return LMR_E_INVALID;
+    if (n > 0 && (!d_gidx || !d_out_idx || (d_vals && !d_out_vals))) return LMR_E_INVALID;
+    PackArgs a;
+    a.layout = *layout;
+    a.gidx = d_gidx;
+    a.vals = reinterpret_cast<const uint8_t*>(d_vals);
+    a.val_bytes = uint32_t(dtype_bytes(int(dtype)));
+    a.n = n;
+    a.index_size = index_size;
+    a.out_idx = reinterpret_cast<uint8_t*>(d_out_idx);
+    a.out_vals = reinterpret_cast<uint8_t*>(d_out_vals);
+    a.out_pos = nullptr;
+    a.dest_counts = d_dest_counts;
+    a.dest_offsets = nullptr;
+    a.err = ctx->d_err;
+    a.prof = ctx->prof;
+    a.stable = false;
+    return hip_status(launch_pack_free(a, d_fill, uint32_t(region_cap), reinterpret_cast<hipStream_t>(stream)));
+}
+
 // ---------------------------------------------------------------- reduce
 lmr_status_t lmr_reduce(lmr_ctx_t* ctx, uint32_t dtype, uint32_t op, const void* d_shard, uint64_t len,
                         uint64_t* d_out, uint8_t* d_has, lmr_stream_t stream) {

@@ -284,6 +284,20 @@ class DeviceKernels:
         check(st, "lmr_pack" if stable else "lmr_pack_unordered")
         return out_idx, out_vals, out_pos, counts
 
+    def pack_regions(self, layout, gidx, n, vals, dt, iw, cap):
+        """lmr_pack_regions: count-free pack into fixed regions of `cap` records per PE
+        -> (idx, vals, counts[int64 device]); a count above cap: that region overflowed."""
+        self.flush()
+        npes = layout.num_pes
+        out_idx = self.empty(npes * cap * iw, torch.uint8)
+        out_vals = self.empty(npes * cap * dt.bytes, torch.uint8) if vals is not None else None
+        fill = self.empty(npes, torch.int32)
+        counts = self.empty(npes, torch.int64)
+        st = self.lib.lmr_pack_regions(self.ctx, byref(layout), _p(gidx), int(n), _p(vals), int(dt.code), int(iw),
+                                       _p(out_idx), _p(out_vals), int(cap), _p(fill), _p(counts), self.stream())
+        check(st, "lmr_pack_regions")
+        return out_idx, out_vals, counts
+
     def reduce(self, data, n, dt, op):
         """lmr_reduce over n elements -> (has, value bits) (one 9-byte readback)."""
         self.flush()

@@ -38,6 +38,19 @@ def main():
         iw = _capi.lib().lmr_index_size(ctypes.byref(L))
         gidx = torch.randint(0, elems, (n,), dtype=torch.int64, device="cuda", generator=g)
         vals = torch.randint(0, 1 << 62, (n,), dtype=torch.int64, device="cuda", generator=g)
+        cap = (n + npes - 1) // npes
+        cap += cap // 8 + 4096
+        for _ in range(2):
+            k.pack_regions(L, gidx, n, vals, dt, iw, cap)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(a.reps):
+            k.pack_regions(L, gidx, n, vals, dt, iw, cap)
+        torch.cuda.synchronize()
+        ms = (time.perf_counter() - t0) / a.reps * 1e3
+        b = n * (8 + 8 + iw + 8)
+        print(f"npes {npes} iw {iw} count-free: {ms:.3f} ms per 2^{a.log2}-record pack, "
+              f"{b / ms / 1e9:.2f} TB/s on {b / n:.0f} B/record (read 16 + write)", flush=True)
         for want_pos in (False, True):
             for _ in range(2):
                 k.pack(L, gidx, n, vals, dt, iw, stable=False, want_pos=want_pos)
