@@ -1448,6 +1448,17 @@ static int bin_blocks_cap(int vb) {
     static int v = env_int("LMR_BIN_BLOCKS", 0, 0, kMaxBinBlocks);
     return v ? v : (coarse_rpt(vb) >= 8 ? 256 : 512);
 }
+// Delta-mode threshold: a tile of a combinable op splits into delta pieces when it holds more
+// than max(LMR_DELTA_MUL x the average tile's records, LMR_DELTA_MIN) records (C3: 4 x / 64K,
+// 2 x / 32K, 2 x / 16K, 1 x / 16K and 1 x / 8K all within 0.50-0.53 ms of tile sweep).
+static uint64_t delta_mul() {
+    static int v = env_int("LMR_DELTA_MUL", 4, 1, 1 << 20);
+    return uint64_t(v);
+}
+static uint64_t delta_min() {
+    static int v = env_int("LMR_DELTA_MIN", 65536, 1024, 1 << 30);
+    return uint64_t(v);
+}
 static int tile_grid_cap() {
     static int v = env_int("LMR_DELTA_BLOCKS", 1024, 1, 1 << 24);
     return v;
@@ -1663,7 +1674,7 @@ static hipError_t launch_tile_sweep(int dtype, const ApplyArgs& a, const TiledWs
                                     bool scalar, void* res_bin, uint8_t* ok_bin, hipStream_t s) {
     ProfScope ps(a.prof, LMR_STAGE_TILE_APPLY, s, n);
     const uint64_t avg = (n + T - 1) / T;
-    const uint32_t thresh = uint32_t(std::min<uint64_t>(0xFFFFFFFFull, std::max<uint64_t>(4 * avg, 65536)));
+    const uint32_t thresh = uint32_t(std::min<uint64_t>(0xFFFFFFFFull, std::max<uint64_t>(delta_mul() * avg, delta_min())));
     const unsigned pg = (T + 255) / 256;
     hipLaunchKernelGGL(k_tile_plan_count, dim3(pg), dim3(256), 0, s, w.tile_start, T, thresh,
                        op_combines(a.op) ? 1 : 0, w.tile_items, w.tile_items2);
@@ -2275,7 +2286,7 @@ hipError_t launch_stage_finish(const TiledWs& w, StageSession& s, hipStream_t st
     {
         ProfScope ps(a.prof, LMR_STAGE_TILE_APPLY, st, s.staged);
         const uint64_t avg = (s.staged + T - 1) / T;
-        const uint32_t thresh = uint32_t(std::min<uint64_t>(0xFFFFFFFFull, std::max<uint64_t>(4 * avg, 65536)));
+        const uint32_t thresh = uint32_t(std::min<uint64_t>(0xFFFFFFFFull, std::max<uint64_t>(delta_mul() * avg, delta_min())));
         const unsigned pg = unsigned((T + 255) / 256);
         hipLaunchKernelGGL(k_stage_plan_count, dim3(pg), dim3(256), 0, st, w.rts, uint32_t(s.nreg), stride, T,
                            thresh, (!mixed && op_combines(a.op)) ? 1 : 0, w.tile_items, w.tile_items2);
