@@ -259,7 +259,51 @@ struct PartArgs {
     void* shard;                  // spill target
     int op;
     uint64_t val_bits;            // the scalar value when val is null (spilled records)
+    // staged regions: coarse_off holds k_ccount's raw (bucket, block) counts; k_coarse_scatter
+    // derives its cursors from them and block 0 stores the bucket starts [C + 1] and the
+    // in-bounds total (no scan launch between the two passes)
+    uint32_t* bstart_out;         // non-null: coarse_off is raw counts
+    uint32_t* total_out;
 };
+
+__device__ __forceinline__ void small_excl_scan(const uint32_t* hist, uint32_t* base, uint32_t m, uint32_t* tot);
+
+// cursor[c] = (records of buckets < c) + (records of bucket c in blocks < g), from the raw
+// per-(bucket, block) counts cnt[c * G + g'] (C <= 128, G <= kMaxBinBlocks): wave w folds
+// buckets w, w + 16, ...; block 0 also stores the bucket starts and the total
+__device__ void coarse_cursors_from_counts(const PartArgs& p, uint32_t g, uint32_t* cursor, uint32_t* tot_s,
+                                           uint32_t* pre_s, uint32_t* tot_scan, uint32_t* total) {
+    const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    for (uint32_t c = wv; c < p.C; c += blockDim.x >> 6) {
+        const uint32_t* row = p.coarse_off + uint64_t(c) * p.G;
+        uint32_t all = 0, pre = 0;
+        for (uint32_t j = lane; j < p.G; j += 64) {
+            const uint32_t v = row[j];
+            all += v;
+            pre += j < g ? v : 0u;
+        }
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+            all += __shfl_xor(all, o, 64);
+            pre += __shfl_xor(pre, o, 64);
+        }
+        if (lane == 0) {
+            tot_s[c] = all;
+            pre_s[c] = pre;
+        }
+    }
+    __syncthreads();
+    small_excl_scan(tot_s, tot_scan, p.C, total);
+    __syncthreads();
+    for (uint32_t c = threadIdx.x; c < p.C; c += blockDim.x) cursor[c] = tot_scan[c] + pre_s[c];
+    if (g == 0) {
+        for (uint32_t c = threadIdx.x; c < p.C; c += blockDim.x) p.bstart_out[c] = tot_scan[c];
+        if (threadIdx.x == 0) {
+            p.bstart_out[p.C] = *total;
+            *p.total_out = *total;
+        }
+    }
+}
 
 // coarse_off[c][g] = start of block g's coarse-c records in the temp buffer
 //                  = tile_start[c*kFine] + sum_{t in c} (fine_off[t][g] - tile_start[t])
@@ -310,7 +354,9 @@ __global__ __launch_bounds__(1024) void k_coarse_scatter(PartArgs p) {
     __shared__ V s_val[kRound];
     const uint32_t g = blockIdx.x, C = p.C;
     const int cshift = p.tile_shift + kFineShift;
-    for (uint32_t c = threadIdx.x; c < C; c += blockDim.x) cursor[c] = p.coarse_off[uint64_t(c) * p.G + g];
+    if (p.bstart_out) coarse_cursors_from_counts(p, g, cursor, hist, base, reinterpret_cast<uint32_t*>(s_idx), &tot);
+    else
+        for (uint32_t c = threadIdx.x; c < C; c += blockDim.x) cursor[c] = p.coarse_off[uint64_t(c) * p.G + g];
     const uint64_t lo = uint64_t(g) * p.chunk;
     const uint64_t hi = min(lo + p.chunk, p.n);
     uint64_t m_raw[RPT];
@@ -832,32 +878,36 @@ struct RegionOp {
     uint64_t cmp_bits, eps_bits;
 };
 
-__global__ void k_tile_plan_count(const uint32_t* tile_start, uint32_t num_tiles, uint32_t thresh,
-                                  int combinable, uint32_t* tile_items, uint32_t* extra) {
-    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= num_tiles) return;
-    const uint32_t c = tile_start[t + 1] - tile_start[t];
-    const uint32_t m = (c == 0) ? 0u : ((combinable && c > thresh) ? (c + kSplit - 1) / kSplit : 1u);
-    tile_items[t] = m;
-    extra[t] = m > 1 ? m : 0u;          // delta pieces (scanned into the delta list)
-}
-
-// Item slot t holds tile t's owner item (mode 0) or a skip marker (mode 2:
-// empty or split tile). Every delta piece of a split tile goes to the delta
-// list at delta_base[t] (exclusive scan of the per-tile piece counts), served
-// by its own persistent kernel so the owner kernel stays lean on registers.
-__global__ void k_tile_plan_fill(const uint32_t* tile_start, uint32_t num_tiles, const uint32_t* delta_base,
-                                 const uint32_t* tile_items, TileItem* items, TileItem* delta) {
-    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= num_tiles) return;
-    const uint32_t m = tile_items[t];
-    const uint32_t lo = tile_start[t], hi = tile_start[t + 1];
-    items[t] = TileItem{t, lo, hi, m == 1 ? 0u : 2u};
-    if (m <= 1) return;
-    for (uint32_t j = 0; j < m; j++) {
-        const uint32_t l = lo + j * kSplit;
-        delta[delta_base[t] + j] = TileItem{t, l, min(hi, l + kSplit), 1u};
+// One block (T <= kMaxTiles): per-tile item counts, their scan and the fill in one launch
+// (the counts / scan / fill as three launches cost ~15 us per sweep). Mode 0 owner item,
+// mode 2 a skip marker (empty or split tile), delta pieces (mode 1) of split tiles listed
+// in tile order; *delta_count = their number.
+__global__ __launch_bounds__(1024) void k_tile_plan(const uint32_t* tile_start, uint32_t num_tiles, uint32_t thresh,
+                                                    int combinable, TileItem* items, TileItem* delta,
+                                                    uint32_t* delta_count) {
+    __shared__ uint32_t tot;
+    uint32_t carry = 0;
+    for (uint32_t t0 = 0; t0 < num_tiles; t0 += 1024) {
+        const uint32_t t = t0 + threadIdx.x;
+        uint32_t lo = 0, hi = 0, m = 0;
+        if (t < num_tiles) {
+            lo = tile_start[t];
+            hi = tile_start[t + 1];
+            const uint32_t c = hi - lo;
+            m = (c == 0) ? 0u : ((combinable && c > thresh) ? (c + kSplit - 1) / kSplit : 1u);
+        }
+        const uint32_t x = m > 1 ? m : 0u;
+        const uint32_t base = carry + block_excl_scan(x, &tot);
+        if (t < num_tiles) {
+            items[t] = TileItem{t, lo, hi, m == 1 ? 0u : 2u};
+            for (uint32_t j = 0; j < x; j++) {
+                const uint32_t l = lo + j * kSplit;
+                delta[base + j] = TileItem{t, l, min(hi, l + kSplit), 1u};
+            }
+        }
+        carry += tot;
     }
+    if (threadIdx.x == 0) *delta_count = carry;
 }
 
 struct TileArgs {
@@ -1148,7 +1198,7 @@ __global__ __launch_bounds__(1024, 8) void k_tile_owner(TileArgs a) {
     }
 }
 
-// Delta mode (combinable ops only; planned by k_tile_plan_count), persistent
+// Delta mode (combinable ops only; planned by k_tile_plan / k_stage_plan), persistent
 // over the delta list: combine kSplit records in an identity-initialised LDS
 // tile, push one device-scope atomic per touched element, rebuild fetch
 // results as base (+) the record's LDS prefix.
@@ -1262,13 +1312,13 @@ __global__ __launch_bounds__(1024) void k_tile_delta(TileArgs a) {
 // chunks), so each block's reads stay within the runs its chunk produced and
 // hit L2; map[k] == ~0 marks an out-of-bounds record (left unwritten).
 template <int VB, int U>
-__global__ __launch_bounds__(1024) void k_unpartition(const uint32_t* __restrict__ map, uint64_t n,
-                                                      const uint32_t* n_dev, uint64_t chunk,
-                                                      const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
-                                                      const uint8_t* __restrict__ ok_src, uint8_t* __restrict__ ok_dst) {
+__device__ __forceinline__ void unpartition_range(const uint32_t* __restrict__ map, uint64_t n,
+                                                  const uint32_t* n_dev, uint64_t chunk, uint32_t blk,
+                                                  const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
+                                                  const uint8_t* __restrict__ ok_src, uint8_t* __restrict__ ok_dst) {
     using V = typename idx_t<VB>::I;
     const uint64_t m = n_dev ? uint64_t(*n_dev) : n;
-    const uint64_t lo = uint64_t(blockIdx.x) * chunk;
+    const uint64_t lo = uint64_t(blk) * chunk;
     const uint64_t hi = min(lo + chunk, m);
     const V* s = reinterpret_cast<const V*>(src);
     V* d = reinterpret_cast<V*>(dst);
@@ -1292,6 +1342,39 @@ __global__ __launch_bounds__(1024) void k_unpartition(const uint32_t* __restrict
             if (ok_src) ok_dst[k] = ok_src[p[j]];
         }
     }
+}
+
+template <int VB, int U>
+__global__ __launch_bounds__(1024) void k_unpartition(const uint32_t* __restrict__ map, uint64_t n,
+                                                      const uint32_t* n_dev, uint64_t chunk,
+                                                      const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
+                                                      const uint8_t* __restrict__ ok_src, uint8_t* __restrict__ ok_dst) {
+    unpartition_range<VB, U>(map, n, n_dev, chunk, blockIdx.x, src, dst, ok_src, ok_dst);
+}
+
+// the same gather over several staged regions in one launch: region i owns blocks
+// [block0[i], block0[i + 1])
+struct UnpartRegion {
+    const uint32_t* map;
+    const uint32_t* n_dev;
+    uint64_t n, chunk;
+    const uint8_t* src;
+    uint8_t* dst;
+    const uint8_t* oks;
+    uint8_t* okd;
+    uint32_t block0;
+};
+struct UnpartTable {
+    UnpartRegion r[kMaxRegions];
+    uint32_t nr;
+};
+
+template <int VB, int U>
+__global__ __launch_bounds__(1024) void k_unpartition_multi(UnpartTable t) {
+    uint32_t i = 0;
+    while (i + 1 < t.nr && t.r[i + 1].block0 <= blockIdx.x) i++;
+    const UnpartRegion& g = t.r[i];
+    unpartition_range<VB, U>(g.map, g.n, g.n_dev, g.chunk, blockIdx.x - g.block0, g.src, g.dst, g.oks, g.okd);
 }
 
 // ------------------------------------------------------------------ dispatch
@@ -1388,7 +1471,7 @@ size_t tiled_ws_bytes(uint64_t cap) {
     size_t b = 0;
     auto al = [](size_t x) { return (x + 255) & ~size_t(255); };
     b += al(size_t(kMaxTiles) * kMaxBinBlocks * 4);                         // counts
-    b += al((size_t(kMaxTiles) * kMaxBinBlocks + kScanItems - 1) / kScanItems * 4);  // partials
+    b += al(scan_scratch_words(size_t(kMaxTiles) * kMaxBinBlocks) * 4);     // scan scratch (zeroed)
     b += al((size_t(kMaxTiles) + 1) * 4);                                   // tile_start
     b += al(cap * 2) + al(cap * 8) + al(cap * 4) + al(4);
     b += al((size_t(kMaxCoarse) * kMaxBinBlocks + 1) * 4);
@@ -1407,7 +1490,7 @@ TiledWs carve_tiled_ws(uint8_t* base, uint64_t cap) {
     uint8_t* p = base;
     w.counts = reinterpret_cast<uint32_t*>(p); p += al(size_t(kMaxTiles) * kMaxBinBlocks * 4);
     w.partials = reinterpret_cast<uint32_t*>(p);
-    p += al((size_t(kMaxTiles) * kMaxBinBlocks + kScanItems - 1) / kScanItems * 4);
+    p += al(scan_scratch_words(size_t(kMaxTiles) * kMaxBinBlocks) * 4);
     w.tile_start = reinterpret_cast<uint32_t*>(p); p += al((size_t(kMaxTiles) + 1) * 4);
     w.bin_lidx = reinterpret_cast<uint16_t*>(p); p += al(cap * 2);
     w.bin_val = p; p += al(cap * 8);
@@ -1573,6 +1656,36 @@ static hipError_t launch_unpartition(int vb, const uint32_t* map, uint64_t n, co
     return hipGetLastError();
 }
 
+// one k_unpartition_multi launch over the regions of t (block0 filled here); each region
+// split as launch_unpartition splits a single range
+static hipError_t launch_unpartition_multi(int vb, UnpartTable& t, hipStream_t s) {
+    if (t.nr == 0) return hipSuccess;
+    const uint64_t sub = 32768 / uint64_t(vb);
+    uint32_t blocks = 0;
+    for (uint32_t i = 0; i < t.nr; i++) {
+        UnpartRegion& g = t.r[i];
+        uint64_t Gu = (g.n + 65535) / 65536;
+        Gu = std::max<uint64_t>(1, std::min<uint64_t>(Gu, 1024));
+        const uint64_t chunk = (g.n + Gu - 1) / Gu;
+        const uint64_t split = std::min<uint64_t>(64, std::max<uint64_t>(1, (chunk + sub - 1) / sub));
+        g.chunk = (chunk + split - 1) / split;
+        g.block0 = blocks;
+        blocks += uint32_t(Gu * split);
+    }
+    auto go = [&](auto vbt) {
+        constexpr int VB = decltype(vbt)::value;
+        constexpr int UU = VB >= 8 ? 4 : 16;
+        hipLaunchKernelGGL((k_unpartition_multi<VB, UU>), dim3(blocks), dim3(1024), 0, s, t);
+    };
+    switch (vb) {
+    case 1: go(std::integral_constant<int, 1>{}); break;
+    case 2: go(std::integral_constant<int, 2>{}); break;
+    case 4: go(std::integral_constant<int, 4>{}); break;
+    default: go(std::integral_constant<int, 8>{}); break;
+    }
+    return hipGetLastError();
+}
+
 // Count-free partition (k_coarse_free / k_fine_free): order-insensitive ops with
 // nothing returned, two-level shards, and >= 25 % headroom per coarse bucket region
 // in the temp arrays for a uniform stream of n records (records past a full region
@@ -1675,14 +1788,9 @@ static hipError_t launch_tile_sweep(int dtype, const ApplyArgs& a, const TiledWs
     ProfScope ps(a.prof, LMR_STAGE_TILE_APPLY, s, n);
     const uint64_t avg = (n + T - 1) / T;
     const uint32_t thresh = uint32_t(std::min<uint64_t>(0xFFFFFFFFull, std::max<uint64_t>(delta_mul() * avg, delta_min())));
-    const unsigned pg = (T + 255) / 256;
-    hipLaunchKernelGGL(k_tile_plan_count, dim3(pg), dim3(256), 0, s, w.tile_start, T, thresh,
-                       op_combines(a.op) ? 1 : 0, w.tile_items, w.tile_items2);
-    hipError_t e = scan_exclusive_u32(w.tile_items2, T, w.plan_partials, w.item_count, s);
-    if (e != hipSuccess) return e;
     TileItem* items = reinterpret_cast<TileItem*>(w.items);
-    hipLaunchKernelGGL(k_tile_plan_fill, dim3(pg), dim3(256), 0, s, w.tile_start, T, w.tile_items2,
-                       w.tile_items, items, items + kMaxTiles);
+    hipLaunchKernelGGL(k_tile_plan, dim3(1), dim3(1024), 0, s, w.tile_start, T, thresh, op_combines(a.op) ? 1 : 0,
+                       items, items + kMaxTiles, w.item_count);
     TileArgs t;
     t.shard = a.shard; t.shard_len = a.shard_len; t.tile_shift = tile_shift_for(dtype);
     t.kind = a.kind; t.op = a.op; t.ret = res_bin ? a.ret : LMR_RET_NONE;
@@ -1849,13 +1957,14 @@ hipError_t launch_apply_tiled(int dtype, int index_size, const ApplyArgs& a, con
 // instead each arriving record stream (a *region*) is partitioned into 64 KiB
 // shard tiles on arrival, inside its own slice of the workspace, and one tile
 // sweep at the end applies every region:
-//   per region : k_ccount (coarse histogram per producer block) -> scan
-//                -> k_coarse_scatter (shared with the one-shot path)
-//                -> k_piece_table -> k_piece_count -> scan -> k_region_starts
-//                -> k_fine_piece                 (region now tile-sorted)
-//   finish     : k_stage_plan_count / _fill -> k_tile_owner over every region's
+//   per region : k_ccount (coarse histogram per producer block)
+//                -> k_coarse_scatter (shared with the one-shot path; its blocks fold the
+//                   raw counts into their cursors, block 0 stores the bucket starts)
+//                -> k_piece_count (piece table) -> scan
+//                -> k_fine_piece (region tile starts; region now tile-sorted)
+//   finish     : k_stage_plan -> k_tile_owner over every region's
 //                range of its tile (+ k_tile_delta for hot tiles)
-//                -> k_unpartition x 2 per region (results back to arrival order)
+//                -> k_unpartition_multi x 2 (every region's results back to arrival order)
 // The fine level works on fixed pieces of kPiece records of each coarse bucket
 // (not on per-producer-block segments as k_fine_scatter does), so its LDS rounds
 // stay full and its output runs long whatever the region size: a 2^25-record
@@ -1910,35 +2019,36 @@ struct PieceArgs {
     int tile_shift;
     uint32_t num_tiles;
     uint32_t C;
-    const uint32_t* pbase;      // [C + 1] first piece of bucket c; pbase[C] = pieces
-    const uint32_t* bstart;     // [C + 1] first temp slot of bucket c; bstart[C] = in-bounds records
+    uint32_t* pbase;            // [C + 1] first piece of bucket c; pbase[C] = pieces (k_piece_count writes it)
+    uint32_t* bstart;           // [C + 1] first temp slot of bucket c; bstart[C] = in-bounds records
     uint32_t* cnt;              // (c, f, p) tile counts at pbase[c]*kFine + f*np_c + p, then their scan
     uint16_t* bin_lidx;         // workspace bases (binned positions are absolute)
     uint8_t* bin_val;
     uint32_t* rpos;             // region temp slot -> binned position (null: nothing returned)
     uint32_t R;                 // the region's first workspace slot
+    uint32_t* ts;               // out: the region's tile starts (absolute binned positions)
 };
 
-// bucket sizes -> pieces of kPiece records; one block of 128 threads (C <= 128)
-__global__ __launch_bounds__(128) void k_piece_table(const uint32_t* coarse_off, uint32_t C, uint32_t G,
-                                                     const uint32_t* inb, uint32_t* pbase, uint32_t* bstart) {
-    __shared__ uint32_t np_s[kMaxCoarse], pb_s[kMaxCoarse], tot;
+// bucket starts (k_coarse_scatter's) -> pieces of kPiece records, computed by every block
+// of k_piece_count into its LDS (C <= 128 loads); block 0 also stores pbase for k_fine_piece
+__device__ void piece_table(const uint32_t* bstart, uint32_t C, uint32_t* pb_s, uint32_t* bs_s, uint32_t* np_s,
+                            uint32_t* tot) {
     const uint32_t c = threadIdx.x;
-    const uint32_t total = *inb;
+    const uint32_t total = bstart[C];
     if (c < C) {
-        const uint32_t s = coarse_off[uint64_t(c) * G];
-        const uint32_t e = (c + 1 < C) ? coarse_off[uint64_t(c + 1) * G] : total;
-        bstart[c] = s;
+        const uint32_t s = bstart[c];
+        const uint32_t e = bstart[c + 1];
+        bs_s[c] = s;
         np_s[c] = (e - s + kPiece - 1) / kPiece;
     }
     __syncthreads();
-    small_excl_scan(np_s, pb_s, C, &tot);
+    small_excl_scan(np_s, pb_s, C, tot);
     __syncthreads();
-    if (c < C) pbase[c] = pb_s[c];
     if (c == 0) {
-        pbase[C] = tot;
-        bstart[C] = total;
+        pb_s[C] = *tot;
+        bs_s[C] = total;
     }
+    __syncthreads();
 }
 
 struct PieceLoc { uint32_t c, p, np, lo, hi; };
@@ -1964,12 +2074,18 @@ __device__ __forceinline__ PieceLoc piece_loc(const PieceArgs& a, uint32_t pid) 
     return piece_loc(a.pbase, a.bstart, a.C, pid);
 }
 
-// per-piece tile histogram (one block per piece; grid = upper bound of pieces)
+// per-piece tile histogram (one block per piece; grid = upper bound of pieces). The
+// count entries of pieces past the table's end are never read (the scan folds them in
+// after every live entry), so nothing clears them.
 __global__ __launch_bounds__(1024) void k_piece_count(PieceArgs a) {
     __shared__ uint32_t hist[kFine];
+    __shared__ uint32_t s_pb[kMaxCoarse + 1], s_bs[kMaxCoarse + 1], s_np[kMaxCoarse], s_tot;
+    piece_table(a.bstart, a.C, s_pb, s_bs, s_np, &s_tot);
+    if (blockIdx.x == 0)
+        for (uint32_t c = threadIdx.x; c <= a.C; c += blockDim.x) a.pbase[c] = s_pb[c];
     const uint32_t pid = blockIdx.x;
-    if (pid >= a.pbase[a.C]) return;
-    const PieceLoc L = piece_loc(a, pid);
+    if (pid >= s_pb[a.C]) return;
+    const PieceLoc L = piece_loc(s_pb, s_bs, a.C, pid);
     const uint32_t t0 = L.c * kFine;
     if (threadIdx.x < kFine) hist[threadIdx.x] = 0;
     __syncthreads();
@@ -1988,22 +2104,23 @@ __global__ __launch_bounds__(1024) void k_piece_count(PieceArgs a) {
     __syncthreads();
     const uint32_t nf = min(uint32_t(kFine), a.num_tiles - t0);
     if (threadIdx.x < nf)
-        a.cnt[uint64_t(a.pbase[L.c]) * kFine + uint64_t(threadIdx.x) * L.np + L.p] = hist[threadIdx.x];
+        a.cnt[uint64_t(s_pb[L.c]) * kFine + uint64_t(threadIdx.x) * L.np + L.p] = hist[threadIdx.x];
 }
 
-// the region's tile starts (absolute binned positions) from the scanned piece counts
-__global__ void k_region_starts(PieceArgs a, uint32_t* ts) {
-    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
-    if (t > a.num_tiles) return;
-    const uint32_t inb = a.bstart[a.C];
-    if (t == a.num_tiles) {
-        ts[t] = a.R + inb;
-        return;
+// the region's tile starts (absolute binned positions) from the scanned piece counts;
+// pb / bs: the piece table (k_fine_piece's LDS copy)
+__device__ __forceinline__ void region_starts(const PieceArgs& a, const uint32_t* pb, const uint32_t* bs) {
+    const uint32_t inb = bs[a.C];
+    for (uint32_t t = blockIdx.x * blockDim.x + threadIdx.x; t <= a.num_tiles; t += gridDim.x * blockDim.x) {
+        if (t == a.num_tiles) {
+            a.ts[t] = a.R + inb;
+            continue;
+        }
+        const uint32_t c = t >> kFineShift, f = t & (kFine - 1);
+        const uint32_t np = pb[c + 1] - pb[c];
+        const uint64_t e = uint64_t(pb[c]) * kFine + uint64_t(f) * np;
+        a.ts[t] = a.R + (e < uint64_t(pb[a.C]) * kFine ? a.cnt[e] : inb);
     }
-    const uint32_t c = t >> kFineShift, f = t & (kFine - 1);
-    const uint32_t np = a.pbase[c + 1] - a.pbase[c];
-    const uint64_t e = uint64_t(a.pbase[c]) * kFine + uint64_t(f) * np;
-    ts[t] = a.R + (e < uint64_t(a.pbase[a.C]) * kFine ? a.cnt[e] : inb);
 }
 
 // fine level: each piece counting-sorted by tile in LDS rounds, written at its
@@ -2021,6 +2138,7 @@ __global__ __launch_bounds__(1024) void k_fine_piece(PieceArgs a) {
         s_bs[c] = a.bstart[c];
     }
     __syncthreads();
+    region_starts(a, s_pb, s_bs);
     const uint32_t npieces = s_pb[a.C];
     const uint32_t lmask = (1u << a.tile_shift) - 1u;
     const V sv = V(a.scalar_bits);
@@ -2093,36 +2211,38 @@ __global__ __launch_bounds__(1024) void k_fine_piece(PieceArgs a) {
     }
 }
 
-// work plan over all regions: owner item per touched tile; a hot tile of a
+// work plan over all regions, one block: owner item per touched tile; a hot tile of a
 // combinable op becomes delta pieces of <= kSplit records over each region's range
-__global__ void k_stage_plan_count(const uint32_t* rts, uint32_t nreg, uint32_t stride, uint32_t num_tiles,
-                                   uint32_t thresh, int combinable, uint32_t* tile_items, uint32_t* extra) {
-    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= num_tiles) return;
-    uint32_t tot = 0, pieces = 0;
-    for (uint32_t r = 0; r < nreg; r++) {
-        const uint32_t c = rts[uint64_t(r) * stride + t + 1] - rts[uint64_t(r) * stride + t];
-        tot += c;
-        pieces += (c + kSplit - 1) / kSplit;
+__global__ __launch_bounds__(1024) void k_stage_plan(const uint32_t* rts, uint32_t nreg, uint32_t stride,
+                                                     uint32_t num_tiles, uint32_t thresh, int combinable,
+                                                     TileItem* items, TileItem* delta, uint32_t* delta_count) {
+    __shared__ uint32_t tot;
+    uint32_t carry = 0;
+    for (uint32_t t0 = 0; t0 < num_tiles; t0 += 1024) {
+        const uint32_t t = t0 + threadIdx.x;
+        uint32_t m = 0;
+        if (t < num_tiles) {
+            uint32_t all = 0, pieces = 0;
+            for (uint32_t r = 0; r < nreg; r++) {
+                const uint32_t c = rts[uint64_t(r) * stride + t + 1] - rts[uint64_t(r) * stride + t];
+                all += c;
+                pieces += (c + kSplit - 1) / kSplit;
+            }
+            m = (all == 0) ? 0u : ((combinable && all > thresh && pieces > 1) ? pieces : 1u);
+        }
+        const uint32_t x = m > 1 ? m : 0u;
+        uint32_t j = carry + block_excl_scan(x, &tot);
+        if (t < num_tiles) {
+            items[t] = TileItem{t, 0u, 0u, m == 1 ? 0u : 2u};
+            if (x)
+                for (uint32_t r = 0; r < nreg; r++) {
+                    const uint32_t lo = rts[uint64_t(r) * stride + t], hi = rts[uint64_t(r) * stride + t + 1];
+                    for (uint32_t l = lo; l < hi; l += kSplit) delta[j++] = TileItem{t, l, min(hi, l + kSplit), 1u};
+                }
+        }
+        carry += tot;
     }
-    const uint32_t m = (tot == 0) ? 0u : ((combinable && tot > thresh && pieces > 1) ? pieces : 1u);
-    tile_items[t] = m;
-    extra[t] = m > 1 ? m : 0u;
-}
-
-__global__ void k_stage_plan_fill(const uint32_t* rts, uint32_t nreg, uint32_t stride, uint32_t num_tiles,
-                                  const uint32_t* delta_base, const uint32_t* tile_items, TileItem* items,
-                                  TileItem* delta) {
-    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= num_tiles) return;
-    const uint32_t m = tile_items[t];
-    items[t] = TileItem{t, 0u, 0u, m == 1 ? 0u : 2u};
-    if (m <= 1) return;
-    uint32_t j = delta_base[t];
-    for (uint32_t r = 0; r < nreg; r++) {
-        const uint32_t lo = rts[uint64_t(r) * stride + t], hi = rts[uint64_t(r) * stride + t + 1];
-        for (uint32_t l = lo; l < hi; l += kSplit) delta[j++] = TileItem{t, l, min(hi, l + kSplit), 1u};
-    }
+    if (threadIdx.x == 0) *delta_count = carry;
 }
 
 // ---- count-free staged regions (order-insensitive integer ops, nothing returned)
@@ -2206,6 +2326,7 @@ hipError_t launch_stage_region(int dtype, int index_size, const ApplyArgs& a, co
     q.tmp_val = a.val ? w.tmp_val + uint64_t(R) * vb : nullptr;
     q.qpos = has_res ? w.qpos + R : nullptr;
     q.err = a.err;
+    q.bstart_out = bstart; q.total_out = inb;       // raw counts: k_coarse_scatter derives its offsets
     hipError_t e;
     {
         ProfScope ps(a.prof, LMR_STAGE_BIN_COUNT, st, a.n);
@@ -2213,11 +2334,6 @@ hipError_t launch_stage_region(int dtype, int index_size, const ApplyArgs& a, co
             hipLaunchKernelGGL((k_ccount<decltype(iw)::value>), dim3(unsigned(G)), dim3(1024), 0, st, q);
             return hipGetLastError();
         });
-    }
-    if (e != hipSuccess) return e;
-    {
-        ProfScope ps(a.prof, LMR_STAGE_SCAN, st);
-        e = scan_exclusive_u32(w.coarse_off, uint64_t(C) * G, w.partials, inb, st);
     }
     if (e != hipSuccess) return e;
     {
@@ -2237,17 +2353,13 @@ hipError_t launch_stage_region(int dtype, int index_size, const ApplyArgs& a, co
     pa.tile_shift = shift; pa.num_tiles = T; pa.C = C; pa.pbase = pbase; pa.bstart = bstart;
     pa.cnt = w.counts; pa.bin_lidx = w.bin_lidx; pa.bin_val = w.bin_val;
     pa.rpos = has_res ? w.rpos + R : nullptr; pa.R = R;
+    pa.ts = w.rts + uint64_t(r) * (kMaxTiles + 1);
     const uint64_t max_pieces = (a.n + kPiece - 1) / kPiece + C;
     {
         ProfScope ps(a.prof, LMR_STAGE_FINE_SCATTER, st, a.n);
-        hipLaunchKernelGGL(k_piece_table, dim3(1), dim3(128), 0, st, w.coarse_off, C, uint32_t(G), inb, pbase, bstart);
-        e = hipMemsetAsync(w.counts, 0, size_t(max_pieces) * kFine * 4, st);
-        if (e != hipSuccess) return e;
         hipLaunchKernelGGL(k_piece_count, dim3(unsigned(max_pieces)), dim3(1024), 0, st, pa);
         e = scan_exclusive_u32(w.counts, max_pieces * kFine, w.partials, nullptr, st);
         if (e != hipSuccess) return e;
-        hipLaunchKernelGGL(k_region_starts, dim3((T + 1 + 255) / 256), dim3(256), 0, st, pa,
-                           w.rts + uint64_t(r) * (kMaxTiles + 1));
         const unsigned fgrid = unsigned(std::min<uint64_t>(max_pieces, uint64_t(fine_blocks_cap())));
         dispatch_vb_rpt<2>(vb, piece_fine_rpt(vb), [&](auto vbt, auto rpt) {
             constexpr int VBc = decltype(vbt)::value, RP = decltype(rpt)::value;
@@ -2287,14 +2399,9 @@ hipError_t launch_stage_finish(const TiledWs& w, StageSession& s, hipStream_t st
         ProfScope ps(a.prof, LMR_STAGE_TILE_APPLY, st, s.staged);
         const uint64_t avg = (s.staged + T - 1) / T;
         const uint32_t thresh = uint32_t(std::min<uint64_t>(0xFFFFFFFFull, std::max<uint64_t>(delta_mul() * avg, delta_min())));
-        const unsigned pg = unsigned((T + 255) / 256);
-        hipLaunchKernelGGL(k_stage_plan_count, dim3(pg), dim3(256), 0, st, w.rts, uint32_t(s.nreg), stride, T,
-                           thresh, (!mixed && op_combines(a.op)) ? 1 : 0, w.tile_items, w.tile_items2);
-        e = scan_exclusive_u32(w.tile_items2, T, w.plan_partials, w.item_count, st);
-        if (e != hipSuccess) return e;
         TileItem* items = reinterpret_cast<TileItem*>(w.items);
-        hipLaunchKernelGGL(k_stage_plan_fill, dim3(pg), dim3(256), 0, st, w.rts, uint32_t(s.nreg), stride, T,
-                           w.tile_items2, w.tile_items, items, items + kMaxTiles);
+        hipLaunchKernelGGL(k_stage_plan, dim3(1), dim3(1024), 0, st, w.rts, uint32_t(s.nreg), stride, T, thresh,
+                           (!mixed && op_combines(a.op)) ? 1 : 0, items, items + kMaxTiles, w.item_count);
         TileArgs t;
         t.shard = a.shard; t.shard_len = a.shard_len; t.tile_shift = shift;
         t.kind = a.kind; t.op = a.op; t.ret = a.ret;
@@ -2331,26 +2438,22 @@ hipError_t launch_stage_finish(const TiledWs& w, StageSession& s, hipStream_t st
         uint8_t* tmpres = w.bin_val;                              // bins are free after the tile sweep
         uint8_t* ok_tmp_all = (a.ret == LMR_RET_RESULT) ? reinterpret_cast<uint8_t*>(w.bin_lidx) : nullptr;
         const uint8_t* ok_src_all = (a.ret == LMR_RET_RESULT) ? ok_bin : nullptr;
-        auto gather = [&](const uint32_t* map, uint64_t n, const uint32_t* n_dev, const uint8_t* src, uint8_t* dst,
-                          const uint8_t* oks, uint8_t* okd) {
-            uint64_t Gu = (n + 65535) / 65536;
-            if (Gu > 1024) Gu = 1024;
-            if (Gu < 1) Gu = 1;
-            const uint64_t chunk = (n + Gu - 1) / Gu;
-            (void)launch_unpartition(vb, map, n, n_dev, chunk, Gu, src, dst, oks, okd, st);
-        };
+        // every returning region's first gather in one launch, then every second gather
+        UnpartTable t1{}, t2{};
         for (int r = 0; r < s.nreg; r++) {
             const StageRegion& g = s.reg[r];
             if (!g.results || g.ret == LMR_RET_NONE) continue;
             uint8_t* ok_tmp = g.ret == LMR_RET_RESULT ? ok_tmp_all : nullptr;
             const uint8_t* ok_src = g.ret == LMR_RET_RESULT ? ok_src_all : nullptr;
-            gather(w.rpos + g.base, g.n, w.sinfo + kStageInb + r, res_bin, tmpres + g.base * vb, ok_src,
-                   ok_tmp ? ok_tmp + g.base : nullptr);
             const bool want_ok = ok_tmp && g.ok;
-            gather(w.qpos + g.base, g.n, nullptr, tmpres + g.base * vb, reinterpret_cast<uint8_t*>(g.results),
-                   want_ok ? ok_tmp + g.base : nullptr, want_ok ? g.ok : nullptr);
+            t1.r[t1.nr++] = UnpartRegion{w.rpos + g.base, w.sinfo + kStageInb + r, g.n, 0, res_bin,
+                                         tmpres + g.base * vb, ok_src, ok_tmp ? ok_tmp + g.base : nullptr, 0};
+            t2.r[t2.nr++] = UnpartRegion{w.qpos + g.base, nullptr, g.n, 0, tmpres + g.base * vb,
+                                         reinterpret_cast<uint8_t*>(g.results), want_ok ? ok_tmp + g.base : nullptr,
+                                         want_ok ? g.ok : nullptr, 0};
         }
-        e = hipGetLastError();
+        e = launch_unpartition_multi(vb, t1, st);
+        if (e == hipSuccess) e = launch_unpartition_multi(vb, t2, st);
     }
     s.nreg = 0;
     s.staged = 0;

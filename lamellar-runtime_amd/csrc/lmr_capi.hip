@@ -75,7 +75,7 @@ struct CtxExtra {
 
 // The small pack / reduce scratch lives right after the error word in one allocation.
 size_t pack_scratch_bytes() {
-    return 256 + kPackScratchCounts * 4 + 256 + (kPackScratchCounts / kScanItems + 1) * 4 + 256 +
+    return 256 + kPackScratchCounts * 4 + 256 + scan_scratch_words(kPackScratchCounts) * 4 + 256 +
            size_t(kReduceBlocks) * 9 + 512;
 }
 
@@ -85,7 +85,7 @@ CtxExtra pack_scratch(lmr_ctx* c) {
     x.pack_counts = reinterpret_cast<uint32_t*>(p);
     p += ((kPackScratchCounts * 4 + 255) & ~size_t(255));
     x.pack_partials = reinterpret_cast<uint32_t*>(p);
-    p += (((kPackScratchCounts / kScanItems + 1) * 4 + 255) & ~size_t(255));
+    p += ((scan_scratch_words(kPackScratchCounts) * 4 + 255) & ~size_t(255));
     x.pack_total = reinterpret_cast<uint32_t*>(p);
     p += 256;
     x.red_part = reinterpret_cast<uint64_t*>(p);
@@ -307,7 +307,8 @@ lmr_status_t lmr_ctx_create(int device, lmr_ctx_t** out) {
     void* p = nullptr;
     if (hipMalloc(&p, pack_scratch_bytes()) != hipSuccess) { delete c; return LMR_E_HIP; }
     c->d_err = reinterpret_cast<uint32_t*>(p);
-    if (hipMemset(p, 0, 256) != hipSuccess) { (void)hipFree(p); delete c; return LMR_E_HIP; }
+    // the error word and the pack scan's look-back scratch start zeroed
+    if (hipMemset(p, 0, pack_scratch_bytes()) != hipSuccess) { (void)hipFree(p); delete c; return LMR_E_HIP; }
     *out = c;
     return LMR_OK;
 }
@@ -343,6 +344,11 @@ lmr_status_t lmr_ctx_reserve(lmr_ctx_t* ctx, uint64_t max_records) {
     if (hipMalloc(&p, b) != hipSuccess) return LMR_E_HIP;
     ctx->ws = reinterpret_cast<uint8_t*>(p);
     ctx->ws_bytes = b;
+    {   // the scan's look-back scratch starts zeroed (every scan leaves it so)
+        const TiledWs w = carve_tiled_ws(ctx->ws, max_records);
+        if (hipMemset(w.partials, 0, scan_scratch_words(size_t(kMaxTiles) * kMaxBinBlocks) * 4) != hipSuccess)
+            return LMR_E_HIP;
+    }
     ctx->rec_cap = max_records;
     return LMR_OK;
 }

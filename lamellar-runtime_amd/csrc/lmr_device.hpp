@@ -546,4 +546,35 @@ template <> struct idx_t<2> { using I = uint16_t; };
 template <> struct idx_t<4> { using I = uint32_t; };
 template <> struct idx_t<8> { using I = uint64_t; };
 
+// wave64 inclusive scan; block-wide (1024 threads) exclusive scan of one value per thread
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x) {
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        uint32_t y = __shfl_up(x, d, 64);
+        if (lane >= d) x += y;
+    }
+    return x;
+}
+
+// block-wide exclusive scan of one value per thread (blockDim.x == 1024); returns the
+// exclusive prefix, writes the block total to *total.
+__device__ __forceinline__ uint32_t block_excl_scan(uint32_t x, uint32_t* total) {
+    __shared__ uint32_t wsum[16];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    uint32_t inc = wave_incl_scan(x);
+    if (lane == 63) wsum[w] = inc;
+    __syncthreads();
+    if (w == 0) {
+        uint32_t v = lane < 16 ? wsum[lane] : 0;
+        uint32_t vi = wave_incl_scan(v);
+        if (lane < 16) wsum[lane] = vi - v;
+        if (lane == 15) *total = vi;
+    }
+    __syncthreads();
+    uint32_t r = inc - x + wsum[w];
+    __syncthreads();
+    return r;
+}
+
 }  // namespace lmr

@@ -89,9 +89,11 @@ size_t tiled_ws_bytes(uint64_t cap);
 uint64_t max_rec_cap();
 TiledWs carve_tiled_ws(uint8_t* base, uint64_t cap);
 
-// exclusive scan of d[0..m) in place; *d_total = sum (may be null). partials
-// must hold ceil(m / kScanItems) entries. only_if non-null: the launches do
-// nothing unless *only_if != 0 when they run (device-side condition).
+// exclusive scan of d[0..m) in place; *d_total = sum (may be null). partials: the
+// look-back scratch, scan_scratch_words(m) u32 words, 8-byte aligned, zeroed once when
+// allocated (every scan leaves it zeroed). only_if non-null: the launch does nothing
+// unless *only_if != 0 when it runs (device-side condition).
+uint64_t scan_scratch_words(uint64_t m);
 hipError_t scan_exclusive_u32(uint32_t* d, uint64_t m, uint32_t* partials, uint32_t* d_total,
                               hipStream_t s, const uint32_t* only_if = nullptr);
 

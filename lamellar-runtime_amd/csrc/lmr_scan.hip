@@ -1,90 +1,14 @@
 // lmr_scan.hip — exclusive prefix sum over u32 counters (bin / pack offsets).
-// Reduce-then-scan in three launches; each block covers kScanItems = 4096
-// elements with 1024 threads x 4 items, wave64 shuffles for the intra-wave scan.
+// Up to 64K counters: one block walks the array with the carry in registers. Above:
+// a single-pass scan with decoupled look-back, one launch: blocks take 4096-counter
+// tiles in ticket order, publish their aggregate, and wave 0 of each block folds up
+// to 64 predecessors' status words per step until it meets an inclusive prefix.
+// The status words and counters live in the caller's scratch and are zero between
+// calls: the last block to finish clears them, so no memset precedes a launch.
 #include "lmr_internal.hpp"
+#include "lmr_device.hpp"
 
 namespace lmr {
-
-__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x) {
-    const int lane = threadIdx.x & 63;
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-        uint32_t y = __shfl_up(x, d, 64);
-        if (lane >= d) x += y;
-    }
-    return x;
-}
-
-// block-wide exclusive scan of one value per thread (blockDim.x == 1024); returns the
-// exclusive prefix, writes the block total to *total.
-__device__ __forceinline__ uint32_t block_excl_scan(uint32_t x, uint32_t* total) {
-    __shared__ uint32_t wsum[16];
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    uint32_t inc = wave_incl_scan(x);
-    if (lane == 63) wsum[w] = inc;
-    __syncthreads();
-    if (w == 0) {
-        uint32_t v = lane < 16 ? wsum[lane] : 0;
-        uint32_t vi = wave_incl_scan(v);
-        if (lane < 16) wsum[lane] = vi - v;
-        if (lane == 15) *total = vi;
-    }
-    __syncthreads();
-    uint32_t r = inc - x + wsum[w];
-    __syncthreads();
-    return r;
-}
-
-__global__ __launch_bounds__(1024) void k_scan_reduce(const uint32_t* __restrict__ d, uint64_t m,
-                                                      uint32_t* __restrict__ partials, const uint32_t* only_if) {
-    if (only_if && *only_if == 0) return;
-    const uint64_t base = uint64_t(blockIdx.x) * kScanItems + uint64_t(threadIdx.x) * 4;
-    uint32_t s = 0;
-#pragma unroll
-    for (int i = 0; i < 4; i++)
-        if (base + i < m) s += d[base + i];
-    __shared__ uint32_t tot;
-    block_excl_scan(s, &tot);
-    if (threadIdx.x == 0) partials[blockIdx.x] = tot;
-}
-
-// single block: exclusive scan of the partials in place, grand total to *d_total
-__global__ __launch_bounds__(1024) void k_scan_partials(uint32_t* __restrict__ partials,
-                                                        uint64_t nb, uint32_t* __restrict__ d_total,
-                                                        const uint32_t* only_if) {
-    if (only_if && *only_if == 0) return;
-    __shared__ uint32_t tot;
-    uint32_t carry = 0;
-    for (uint64_t b0 = 0; b0 < nb; b0 += 1024) {
-        uint64_t i = b0 + threadIdx.x;
-        uint32_t x = i < nb ? partials[i] : 0;
-        uint32_t e = block_excl_scan(x, &tot);
-        if (i < nb) partials[i] = carry + e;
-        carry += tot;
-        __syncthreads();
-    }
-    if (threadIdx.x == 0 && d_total) *d_total = carry;
-}
-
-__global__ __launch_bounds__(1024) void k_scan_apply(uint32_t* __restrict__ d, uint64_t m,
-                                                     const uint32_t* __restrict__ partials, const uint32_t* only_if) {
-    if (only_if && *only_if == 0) return;
-    const uint64_t base = uint64_t(blockIdx.x) * kScanItems + uint64_t(threadIdx.x) * 4;
-    uint32_t v[4];
-    uint32_t s = 0;
-#pragma unroll
-    for (int i = 0; i < 4; i++) {
-        v[i] = (base + i < m) ? d[base + i] : 0;
-        s += v[i];
-    }
-    __shared__ uint32_t tot;
-    uint32_t e = block_excl_scan(s, &tot) + partials[blockIdx.x];
-#pragma unroll
-    for (int i = 0; i < 4; i++) {
-        if (base + i < m) d[base + i] = e;
-        e += v[i];
-    }
-}
 
 // one block for short arrays (tile starts, plans, coarse offsets): kScanItems elements per
 // pass with the carry in registers, one launch instead of three
@@ -114,6 +38,87 @@ __global__ __launch_bounds__(1024) void k_scan_single(uint32_t* __restrict__ d, 
 }
 
 constexpr uint64_t kScanSingleMax = 16 * kScanItems;
+constexpr uint64_t kStAgg = uint64_t(1) << 32, kStPrefix = uint64_t(2) << 32;
+
+// scratch: [0] ticket, [1] blocks done, then nb u64 status words (flag << 32 | value)
+__global__ __launch_bounds__(1024) void k_scan_lookback(uint32_t* __restrict__ d, uint64_t m,
+                                                        uint32_t* __restrict__ scratch, uint32_t nb,
+                                                        uint32_t* __restrict__ d_total, const uint32_t* only_if) {
+    if (only_if && *only_if == 0) return;
+    uint32_t* ctl = scratch;
+    uint64_t* st = reinterpret_cast<uint64_t*>(scratch + 2);
+    __shared__ uint32_t s_tile, s_excl, s_last, tot;
+    if (threadIdx.x == 0) s_tile = atomicAdd(&ctl[0], 1u);
+    __syncthreads();
+    const uint32_t tile = s_tile;
+    const uint64_t base = uint64_t(tile) * kScanItems + uint64_t(threadIdx.x) * 4;
+    uint32_t v[4];
+    uint32_t sum = 0;
+    if (base + 4 <= m && (reinterpret_cast<uintptr_t>(d) & 15) == 0) {
+        const uint4 q = *reinterpret_cast<const uint4*>(d + base);
+        v[0] = q.x; v[1] = q.y; v[2] = q.z; v[3] = q.w;
+    } else {
+#pragma unroll
+        for (int i = 0; i < 4; i++) v[i] = (base + i < m) ? d[base + i] : 0;
+    }
+#pragma unroll
+    for (int i = 0; i < 4; i++) sum += v[i];
+    uint32_t e = block_excl_scan(sum, &tot);
+    if (threadIdx.x < 64) {
+        const uint32_t lane = threadIdx.x;
+        const uint32_t agg = tot;
+        uint32_t excl = 0;
+        if (tile == 0) {
+            if (lane == 0) __hip_atomic_store(&st[0], kStPrefix | agg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        } else {
+            if (lane == 0) __hip_atomic_store(&st[tile], kStAgg | agg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            int64_t top = int64_t(tile) - 1;              // the nearest predecessor not folded yet
+            while (true) {
+                const int64_t j = top - int64_t(lane);
+                const uint64_t w = j >= 0 ? __hip_atomic_load(&st[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                                          : kStPrefix;   // before tile 0: an empty prefix
+                const uint32_t flag = uint32_t(w >> 32);
+                const uint64_t pre = __ballot(flag == 2u);
+                const uint64_t inv = __ballot(flag == 0u);
+                const int p = pre ? __ffsll(static_cast<unsigned long long>(pre)) - 1 : 64;   // nearest prefix
+                const uint64_t need = p >= 63 ? ~uint64_t(0) : ((uint64_t(2) << p) - 1);
+                if (inv & need) {                          // a predecessor up to it has not published
+                    __builtin_amdgcn_s_sleep(1);
+                    continue;
+                }
+                uint32_t x = int(lane) <= p ? uint32_t(w) : 0u;
+#pragma unroll
+                for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o, 64);
+                excl += x;
+                if (pre) break;
+                top -= 64;
+            }
+            if (lane == 0) __hip_atomic_store(&st[tile], kStPrefix | (excl + agg), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        if (lane == 0) s_excl = excl;
+    }
+    __syncthreads();
+    e += s_excl;
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        if (base + i < m) d[base + i] = e;
+        e += v[i];
+    }
+    if (tile == nb - 1 && threadIdx.x == 0 && d_total) *d_total = s_excl + tot;
+    // the last block to finish (every look-back read done) leaves the scratch zeroed
+    if (threadIdx.x == 0) s_last = atomicAdd(&ctl[1], 1u) == nb - 1;
+    __syncthreads();
+    if (s_last) {
+        for (uint32_t j = threadIdx.x; j < nb; j += blockDim.x)
+            __hip_atomic_store(&st[j], uint64_t(0), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (threadIdx.x == 0) {
+            __hip_atomic_store(&ctl[0], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(&ctl[1], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+}
+
+uint64_t scan_scratch_words(uint64_t m) { return 4 + 2 * ((m + kScanItems - 1) / kScanItems); }
 
 hipError_t scan_exclusive_u32(uint32_t* d, uint64_t m, uint32_t* partials, uint32_t* d_total,
                               hipStream_t s, const uint32_t* only_if) {
@@ -125,10 +130,9 @@ hipError_t scan_exclusive_u32(uint32_t* d, uint64_t m, uint32_t* partials, uint3
         hipLaunchKernelGGL(k_scan_single, dim3(1), dim3(1024), 0, s, d, m, d_total, only_if);
         return hipGetLastError();
     }
-    uint64_t nb = (m + kScanItems - 1) / kScanItems;
-    hipLaunchKernelGGL(k_scan_reduce, dim3(unsigned(nb)), dim3(1024), 0, s, d, m, partials, only_if);
-    hipLaunchKernelGGL(k_scan_partials, dim3(1), dim3(1024), 0, s, partials, nb, d_total, only_if);
-    hipLaunchKernelGGL(k_scan_apply, dim3(unsigned(nb)), dim3(1024), 0, s, d, m, partials, only_if);
+    const uint64_t nb = (m + kScanItems - 1) / kScanItems;
+    hipLaunchKernelGGL(k_scan_lookback, dim3(unsigned(nb)), dim3(1024), 0, s, d, m, partials, uint32_t(nb),
+                       d_total, only_if);
     return hipGetLastError();
 }
 
