@@ -69,9 +69,10 @@ def stage_bytes_per_op(stage, iw, vb, eb, n, shard_len, fetch):
     """Algorithmic HBM bytes per op of each kernel stage (Kernels):
     the bytes a stage must read and write per record, shard traffic amortised.
     Returned values travel binned -> temp -> input order through stored u32 maps
-    (qpos written by the coarse pass, rpos by the fine pass)."""
-    pos = 4 if fetch else 0
-    res = eb if fetch else 0
+    (qpos written by the coarse pass, rpos by the fine pass). fetch: the share of records
+    whose op returns a value (C5: 2 of 5 batches); the un-partition counts only those."""
+    pos = 4 * float(fetch)
+    res = eb * float(fetch)
     tile_elems = 65536 // max(eb, 4)
     two_level = (shard_len + tile_elems - 1) // tile_elems > 128
     return {
@@ -80,7 +81,7 @@ def stage_bytes_per_op(stage, iw, vb, eb, n, shard_len, fetch):
         "bin_scatter": iw + vb + 4 + vb + pos,          # coarse pass: record in, temp record (+ qpos) out
         "fine_scatter": 4 + vb + 2 + vb + pos,          # temp record in, tile-local record (+ rpos) out
         "tile_apply": 2 + vb + res + 2.0 * eb * shard_len / max(n, 1),
-        "unpartition": (2 if two_level else 1) * (pos + 2 * res),
+        "unpartition": (2 if two_level else 1) * (4 + 2 * eb) if fetch else 0.0,
         "pack": 8 + 8 + vb + iw + vb + 4,
         "scatter_results": 4 + 2 * eb,
         "mvsi": vb + res,
@@ -193,7 +194,7 @@ class FetchAddZipf(Workload):
 
 class MixedU32(Workload):
     """C5: u32 and/or/xor/swap/compare_exchange in equal fifths, one batch each."""
-    dtype, fetch, eb, vb = "u32", True, 4, 4
+    dtype, fetch, eb, vb = "u32", 0.4, 4, 4         # swap and compare_exchange return values
 
     def setup(self):
         a = self.args

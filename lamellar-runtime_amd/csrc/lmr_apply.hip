@@ -15,13 +15,10 @@
 //                      read+write of the shard.
 #include "lmr_internal.hpp"
 #include "lmr_device.hpp"
+#include "lmr_tile.hpp"
 #include <stdlib.h>
 #include <algorithm>
 
-// k_tile_owner reads 4 binned records per thread with wide loads (0: one record at a time)
-#ifndef LMR_OWN_VEC
-#define LMR_OWN_VEC 1
-#endif
 // k_coarse_free loads two consecutive u64 records per thread with 16-B loads (0: one at a time)
 #ifndef LMR_COARSE_PAIRS
 #define LMR_COARSE_PAIRS 1
@@ -264,6 +261,10 @@ struct PartArgs {
     // in-bounds total (no scan launch between the two passes)
     uint32_t* bstart_out;         // non-null: coarse_off is raw counts
     uint32_t* total_out;
+    uint32_t csub;                // staged regions: k_ccount blocks per producer block (count rows C x G*csub)
+    uint32_t* trows;              // staged regions: [G * csub][num_tiles] per-count-block tile counts (k_ccount)
+    uint32_t* ttot;               // staged regions: [num_tiles] tile totals (k_coarse_scatter folds the rows)
+    uint32_t* tfill;              // staged regions: [num_tiles] fine-pass fill counters (zeroed by k_coarse_scatter)
 };
 
 __device__ __forceinline__ void small_excl_scan(const uint32_t* hist, uint32_t* base, uint32_t m, uint32_t* tot);
@@ -274,13 +275,14 @@ __device__ __forceinline__ void small_excl_scan(const uint32_t* hist, uint32_t* 
 __device__ void coarse_cursors_from_counts(const PartArgs& p, uint32_t g, uint32_t* cursor, uint32_t* tot_s,
                                            uint32_t* pre_s, uint32_t* tot_scan, uint32_t* total) {
     const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const uint32_t S = p.csub ? p.csub : 1u, GS = p.G * S, gs = g * S;
     for (uint32_t c = wv; c < p.C; c += blockDim.x >> 6) {
-        const uint32_t* row = p.coarse_off + uint64_t(c) * p.G;
+        const uint32_t* row = p.coarse_off + uint64_t(c) * GS;
         uint32_t all = 0, pre = 0;
-        for (uint32_t j = lane; j < p.G; j += 64) {
+        for (uint32_t j = lane; j < GS; j += 64) {
             const uint32_t v = row[j];
             all += v;
-            pre += j < g ? v : 0u;
+            pre += j < gs ? v : 0u;
         }
 #pragma unroll
         for (int o = 32; o > 0; o >>= 1) {
@@ -354,8 +356,33 @@ __global__ __launch_bounds__(1024) void k_coarse_scatter(PartArgs p) {
     __shared__ V s_val[kRound];
     const uint32_t g = blockIdx.x, C = p.C;
     const int cshift = p.tile_shift + kFineShift;
-    if (p.bstart_out) coarse_cursors_from_counts(p, g, cursor, hist, base, reinterpret_cast<uint32_t*>(s_idx), &tot);
-    else
+    if (p.bstart_out) {
+        coarse_cursors_from_counts(p, g, cursor, hist, base, reinterpret_cast<uint32_t*>(s_idx), &tot);
+        // tile totals of the region: block g folds every count row over its slice of tpb tiles
+        // (thread = (row group, tile); rows read in tpb-word segments), the fine pass turns them
+        // into tile starts; the slice's fill counters are cleared
+        const uint32_t rows = p.G * (p.csub ? p.csub : 1u);
+        const uint32_t tpb = (p.num_tiles + p.G - 1) / p.G;
+        const uint32_t t_lo = g * tpb, t_hi = min(t_lo + tpb, p.num_tiles);
+        uint32_t* part = reinterpret_cast<uint32_t*>(s_val);   // [1024] partial sums (LDS round buffer, free here)
+        for (uint32_t t0 = t_lo; t0 < t_hi; t0 += 1024) {
+            const uint32_t nt = min(1024u, t_hi - t0);
+            const uint32_t ng = 1024 / nt;                     // row groups
+            const uint32_t j = threadIdx.x % nt, rg = threadIdx.x / nt;
+            uint32_t x = 0;
+            if (rg < ng)
+                for (uint32_t b = rg; b < rows; b += ng) x += p.trows[uint64_t(b) * p.num_tiles + t0 + j];
+            part[threadIdx.x] = x;
+            __syncthreads();
+            if (threadIdx.x < nt) {
+                uint32_t sum = 0;
+                for (uint32_t r = 0; r < ng; r++) sum += part[r * nt + threadIdx.x];
+                p.ttot[t0 + threadIdx.x] = sum;
+                p.tfill[t0 + threadIdx.x] = 0;
+            }
+            __syncthreads();
+        }
+    } else
         for (uint32_t c = threadIdx.x; c < C; c += blockDim.x) cursor[c] = p.coarse_off[uint64_t(c) * p.G + g];
     const uint64_t lo = uint64_t(g) * p.chunk;
     const uint64_t hi = min(lo + p.chunk, p.n);
@@ -559,13 +586,14 @@ __host__ __device__ inline uint32_t seg_cap(uint32_t capc, uint32_t x) {
 }
 __device__ __forceinline__ uint32_t xcc_id() { return __builtin_amdgcn_s_getreg((3 << 11) | 20) & (kXcds - 1); }  // HW_REG_XCC_ID
 
-template <int IW, int VB, int RPT>
+template <int IW, int VB, int RPT, bool PAIRS>
 __global__ __launch_bounds__(1024) void k_coarse_free(PartArgs p) {
     using V = typename idx_t<VB>::I;
     constexpr uint32_t kRound = RPT * 1024;
     extern __shared__ uint32_t th[];                   // [num_tiles] this block's tile counts
     __shared__ uint32_t hist[kMaxCoarse], base[kMaxCoarse], tot;
     __shared__ uint32_t seg_a[kMaxCoarse], len_a[kMaxCoarse], seg_b[kMaxCoarse];   // a round's run: 2 pieces
+    __shared__ uint32_t s_spill;                      // this round has records past their bucket region
     __shared__ uint32_t s_idx[kRound];
     __shared__ V s_val[kRound];
     const uint32_t g = blockIdx.x, C = p.C;
@@ -581,31 +609,31 @@ __global__ __launch_bounds__(1024) void k_coarse_free(PartArgs p) {
     // pairs: two consecutive 8-B records per thread with one 16-B load of indices and one of
     // values (contiguous u64 indices and 8-B values, 16-B aligned); record j of a round is then
     // record 2 * ((j / 2) * 1024 + thread) + j % 2 (C2 coarse pass 1.585 -> 1.562 ms, same box)
-    const bool pairs = kCoarsePairs && IW == 8 && VB == 8 && (RPT % 2) == 0 && p.idx_stride == 8 && p.val &&
-                       p.val_stride == 8 && (p.chunk % 2) == 0 &&
-                       ((reinterpret_cast<uintptr_t>(p.idx) | reinterpret_cast<uintptr_t>(p.val)) & 15) == 0;
+    // PAIRS (compile time, chosen on the host: u64 indices and 8-B values, both contiguous and
+    // 16-B aligned, even chunks): without the one-at-a-time path in the same kernel, no dead
+    // path's pending loads make the compiler wait for the prefetch before the write-out
+    constexpr bool pairs = PAIRS;
+    // every pair is loaded from an even offset <= kl (the last record's pair): the aligned 16-B
+    // load of a valid 8-B record never leaves its page, and the half past the range is dropped
+    const uint64_t kl = lo < hi ? lo + ((hi - 1 - lo) & ~uint64_t(1)) : lo;
     auto kof = [&](uint64_t r0, int j) -> uint64_t {
         return pairs ? r0 + 2 * (uint64_t(j >> 1) * 1024 + threadIdx.x) + (j & 1) : r0 + uint64_t(j) * 1024 + threadIdx.x;
     };
     auto load_round = [&](uint64_t r0) {
         if (pairs) {
+            // branch-free from a clamped offset and used as loaded (the round masks the records
+            // past hi), so all RPT / 2 pairs are in flight at once: a guarded load per pair made
+            // the compiler wait for each pair before the next
 #pragma unroll
             for (int j = 0; j < RPT; j += 2) {
                 const uint64_t k = kof(r0, j);
-                if (k + 1 < hi) {
-                    const uint4 x = *reinterpret_cast<const uint4*>(p.idx + k * 8);
-                    const uint4 y = *reinterpret_cast<const uint4*>(p.val + k * 8);
-                    m_raw[j] = uint64_t(x.x) | (uint64_t(x.y) << 32);
-                    m_raw[j + 1] = uint64_t(x.z) | (uint64_t(x.w) << 32);
-                    m_val[j] = V(uint64_t(y.x) | (uint64_t(y.y) << 32));
-                    m_val[j + 1] = V(uint64_t(y.z) | (uint64_t(y.w) << 32));
-                } else {
-                    const bool in = k < hi;
-                    m_raw[j] = in ? load_idx<IW>(p.idx, 8, k) : ~uint64_t(0);
-                    m_val[j] = in ? *reinterpret_cast<const V*>(p.val + k * 8) : V(0);
-                    m_raw[j + 1] = ~uint64_t(0);
-                    m_val[j + 1] = V(0);
-                }
+                const uint64_t kc = k <= kl ? k : kl;
+                const ulonglong2 x = *reinterpret_cast<const ulonglong2*>(p.idx + kc * 8);
+                const ulonglong2 y = *reinterpret_cast<const ulonglong2*>(p.val + kc * 8);
+                m_raw[j] = x.x;
+                m_raw[j + 1] = x.y;
+                m_val[j] = V(y.x);
+                m_val[j + 1] = V(y.y);
             }
             return;
         }
@@ -617,7 +645,7 @@ __global__ __launch_bounds__(1024) void k_coarse_free(PartArgs p) {
             m_val[j] = !in ? V(0) : p.val ? *reinterpret_cast<const V*>(p.val + k * p.val_stride) : V(p.val_bits);
         }
     };
-    load_round(lo);
+    if (lo < hi) load_round(lo);
     for (uint64_t r0 = lo; r0 < hi; r0 += kRound) {
         for (uint32_t c = threadIdx.x; c < C; c += blockDim.x) hist[c] = 0;
         __syncthreads();
@@ -626,7 +654,7 @@ __global__ __launch_bounds__(1024) void k_coarse_free(PartArgs p) {
 #pragma unroll
         for (int j = 0; j < RPT; j++) {
             const uint64_t k = kof(r0, j);
-            m_ok[j] = m_raw[j] < p.shard_len;
+            m_ok[j] = k < hi && m_raw[j] < p.shard_len;
             if (!m_ok[j] && k < hi) oob = true;
             m_c[j] = m_ok[j] ? uint32_t(m_raw[j] >> cshift) : 0u;
             if (m_ok[j]) {
@@ -651,6 +679,7 @@ __global__ __launch_bounds__(1024) void k_coarse_free(PartArgs p) {
             s_idx[q] = uint32_t(m_raw[j]);
             s_val[q] = m_val[j];
         }
+        if (threadIdx.x == 0) s_spill = 0;
         if (threadIdx.x < C) {
             const uint32_t c = threadIdx.x;
             const uint32_t a = rsv >= capx ? 0u : min(cnt, capx - rsv);
@@ -661,11 +690,15 @@ __global__ __launch_bounds__(1024) void k_coarse_free(PartArgs p) {
         }
         if (r0 + kRound < hi) load_round(r0 + kRound);     // prefetch the next round
         __syncthreads();
-        // Records past the end of their bucket's region are applied to the shard with
-        // device atomics (the op is order-insensitive) and taken out of the tile counts.
+        if (threadIdx.x < C && len_a[threadIdx.x] < hist[threadIdx.x] &&
+            seg_b[threadIdx.x] + (hist[threadIdx.x] - len_a[threadIdx.x]) > caps)
+            s_spill = 1;
         const uint32_t nw = blockDim.x >> 6, wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
         const uint32_t wpb = C >= nw ? 1u : nw / C, bstep = nw / wpb;
         const uint32_t sb = seg_base(p.capc, kXcds);
+        // the write-out holds no device atomic (their returned values made the compiler wait
+        // for every outstanding load and store, the next round's prefetch included, at each
+        // iteration); records past their bucket region are handled by the loop after it
         for (uint32_t c = wave / wpb; c < C; c += bstep) {
             const uint32_t len = hist[c], b = base[c], la = len_a[c], da = seg_a[c], db = seg_b[c];
             const uint64_t reg = uint64_t(c) * p.capc;
@@ -676,15 +709,26 @@ __global__ __launch_bounds__(1024) void k_coarse_free(PartArgs p) {
                     const uint64_t d = reg + (i < la ? da + i : sb + db + j);
                     p.tmp_idx[d] = s_idx[q];
                     if (p.tmp_val) reinterpret_cast<V*>(p.tmp_val)[d] = s_val[q];
-                } else if (p.spill) {                       // not binned: out of the tile counts
+                }
+            }
+        }
+        __syncthreads();
+        // Records past the end of their bucket's region are applied to the shard with
+        // device atomics (the op is order-insensitive) and taken out of the tile counts.
+        if (s_spill && p.spill) {
+            for (uint32_t c = wave / wpb; c < C; c += bstep) {
+                const uint32_t len = hist[c], b = base[c], la = len_a[c], db = seg_b[c];
+                for (uint32_t i = (wave % wpb) * 64 + lane; i < len; i += wpb * 64) {
+                    const uint32_t q = b + i;
+                    if (i < la || db + (i - la) < caps) continue;
                     atomicSub(&th[s_idx[q] >> p.tile_shift], 1u);
                     uint8_t ok;
                     rmw_global<V>(reinterpret_cast<V*>(p.shard) + s_idx[q], p.op, LMR_KIND_NATIVE_ATOMIC, s_val[q],
                                   V(0), V(0), ok, p.err);
                 }
             }
+            __syncthreads();
         }
-        __syncthreads();
     }
     if (oob) raise_err(p.err, LMR_ERRBIT_OOB);
     __syncthreads();
@@ -854,30 +898,6 @@ __global__ __launch_bounds__(NT) void k_fine_free(PartArgs p) {
     }
 }
 
-// ---- tile work plan --------------------------------------------------------
-// Most tiles are one work item in "owner" mode (one workgroup stages the tile
-// in LDS, applies every record, writes the tile back). A tile with far more
-// records than average (skewed streams, e.g. Zipf 0.99: ~5 % of all records on
-// one element) is split into kSplit-record items in "delta" mode when the op
-// combines (add/sub/and/or/xor and their fetch forms): each workgroup combines
-// its records in an LDS delta tile (identity-initialised), then applies one
-// device-scope atomic per touched element; fetch results are the returned base
-// combined with the record's LDS prefix — a valid linearisation with each
-// workgroup's records applied as one block.
-constexpr uint32_t kSplit = 16 * 1024;     // records per delta item (16 per thread)
-#ifndef LMR_WAVE_COMBINE
-#define LMR_WAVE_COMBINE 1
-#endif
-constexpr bool kWaveCombine = LMR_WAVE_COMBINE != 0;   // lds_acc_wave in the delta pass (A/B builds: -DLMR_WAVE_COMBINE=0)
-
-struct TileItem { uint32_t tile, lo, hi, mode; };
-
-// a mixed staged session's per-region op (k_tile_owner applies region rg's records with rop[rg])
-struct RegionOp {
-    int32_t op, ret;
-    uint64_t cmp_bits, eps_bits;
-};
-
 // One block (T <= kMaxTiles): per-tile item counts, their scan and the fill in one launch
 // (the counts / scan / fill as three launches cost ~15 us per sweep). Mode 0 owner item,
 // mode 2 a skip marker (empty or split tile), delta pieces (mode 1) of split tiles listed
@@ -910,403 +930,6 @@ __global__ __launch_bounds__(1024) void k_tile_plan(const uint32_t* tile_start, 
     if (threadIdx.x == 0) *delta_count = carry;
 }
 
-struct TileArgs {
-    void* shard;
-    uint64_t shard_len;
-    int tile_shift;
-    int kind;
-    int op;
-    int ret;
-    uint64_t cmp_bits;
-    uint64_t eps_bits;
-    uint64_t val_bits;       // scalar value (SVMI)
-    bool scalar;
-    const TileItem* items;        // one per tile (owner kernel)
-    const TileItem* delta;        // delta pieces (delta kernel)
-    const uint32_t* delta_count;  // number of delta pieces (device)
-    uint32_t num_tiles;
-    const uint16_t* bin_lidx;
-    const uint8_t* bin_val;
-    void* results;           // binned order: [r] (un-partitioned by k_unpartition)
-    uint8_t* ok;             // binned order
-    uint32_t* err;
-    // staged apply: an owner item covers tile t of every region r, records
-    // [rts[r * rstride + t], rts[r * rstride + t + 1]); nreg == 0: the item's own [lo, hi)
-    const uint32_t* rts;
-    uint32_t nreg;
-    uint32_t rstride;
-    // mixed session (regions of different ops / operands): region rg applied with rop[rg], every
-    // region of the tile after the previous one (staging order per element)
-    int mixed;
-    RegionOp rop[kMaxRegions];
-};
-
-__host__ __device__ constexpr bool op_combines(int op) {
-    return op == LMR_OP_ADD || op == LMR_OP_FETCH_ADD || op == LMR_OP_SUB || op == LMR_OP_FETCH_SUB ||
-           op == LMR_OP_AND || op == LMR_OP_FETCH_AND || op == LMR_OP_OR || op == LMR_OP_FETCH_OR ||
-           op == LMR_OP_XOR || op == LMR_OP_FETCH_XOR;
-}
-
-// delta mode: how records accumulate in LDS, how the block's delta reaches
-// global memory, and how a record's old value is rebuilt from the base.
-__device__ __forceinline__ int delta_acc_op(int op) {
-    switch (op) {
-    case LMR_OP_ADD: case LMR_OP_FETCH_ADD: case LMR_OP_SUB: case LMR_OP_FETCH_SUB: return LMR_OP_FETCH_ADD;
-    case LMR_OP_AND: case LMR_OP_FETCH_AND: return LMR_OP_FETCH_AND;
-    case LMR_OP_OR: case LMR_OP_FETCH_OR: return LMR_OP_FETCH_OR;
-    default: return LMR_OP_FETCH_XOR;
-    }
-}
-__device__ __forceinline__ int delta_global_op(int op) {
-    switch (op) {
-    case LMR_OP_ADD: case LMR_OP_FETCH_ADD: return LMR_OP_FETCH_ADD;
-    case LMR_OP_SUB: case LMR_OP_FETCH_SUB: return LMR_OP_FETCH_SUB;
-    case LMR_OP_AND: case LMR_OP_FETCH_AND: return LMR_OP_FETCH_AND;
-    case LMR_OP_OR: case LMR_OP_FETCH_OR: return LMR_OP_FETCH_OR;
-    default: return LMR_OP_FETCH_XOR;
-    }
-}
-template <typename T>
-__device__ __forceinline__ T delta_finish(int op, T base, T prefix) {
-    using U = typename bits_of<T>::U;
-    switch (op) {
-    case LMR_OP_ADD: case LMR_OP_FETCH_ADD:
-        if constexpr (is_flt<T>::v) return base + prefix; else return T(U(U(base) + U(prefix)));
-    case LMR_OP_SUB: case LMR_OP_FETCH_SUB:
-        if constexpr (is_flt<T>::v) return base - prefix; else return T(U(U(base) - U(prefix)));
-    default: break;
-    }
-    if constexpr (!is_flt<T>::v) {
-        if (op == LMR_OP_AND || op == LMR_OP_FETCH_AND) return T(base & prefix);
-        if (op == LMR_OP_OR || op == LMR_OP_FETCH_OR) return T(base | prefix);
-        return T(base ^ prefix);
-    }
-    return base;
-}
-
-// a (+) b for the delta accumulation ops (FETCH_ADD / AND / OR / XOR), wrapping for integers
-template <typename T>
-__device__ __forceinline__ T acc_comb(int acc, T a, T b) {
-    using U = typename bits_of<T>::U;
-    if (acc == LMR_OP_FETCH_ADD) {
-        if constexpr (is_flt<T>::v) return a + b; else return T(U(U(a) + U(b)));
-    }
-    if constexpr (!is_flt<T>::v) {
-        if (acc == LMR_OP_FETCH_AND) return T(a & b);
-        if (acc == LMR_OP_FETCH_OR) return T(a | b);
-        return T(a ^ b);
-    }
-    return a;
-}
-template <typename T>
-__device__ __forceinline__ T shfl_t(T x, int src) {
-    using U = typename bits_of<T>::U;
-    if constexpr (sizeof(T) == 8) return from_bits<T>(U(__shfl((unsigned long long)U(to_bits(x)), src, 64)));
-    else return from_bits<T>(U(__shfl(uint32_t(U(to_bits(x))), src, 64)));
-}
-template <typename T>
-__device__ __forceinline__ T shfl_up_t(T x, int d) {
-    using U = typename bits_of<T>::U;
-    if constexpr (sizeof(T) == 8) return from_bits<T>(U(__shfl_up((unsigned long long)U(to_bits(x)), d, 64)));
-    else return from_bits<T>(U(__shfl_up(uint32_t(U(to_bits(x))), d, 64)));
-}
-
-// One record per active lane accumulated into an LDS delta tile with `acc`, returning the
-// element's previous delta. When many lanes of the wave name the first active lane's element
-// (a hot element: Zipf streams put most of a hot tile's records on it), those lanes combine
-// their values with a wave scan and one lane applies the sum: one LDS atomic instead of up to
-// 64 serialised ones; lane j of the group gets base (+) the values of the group's lanes before j
-// (the group applied in lane order, as one step). Called by every lane of the wave.
-template <typename T>
-__device__ __forceinline__ T lds_acc_wave(typename word_of<T>::W* tile, uint32_t l, T v, bool active, int acc,
-                                          T ident, int kind, uint32_t* err) {
-    const int lane = threadIdx.x & 63;
-    const uint64_t act = __ballot(active);
-    T res = ident;
-    bool done = false;
-    uint8_t ok = 0;
-    if (act) {
-        const int f = __ffsll((unsigned long long)act) - 1;
-        const uint32_t l0 = __shfl(l, f, 64);
-        const bool in = active && l == l0;
-        const uint64_t m = __ballot(in);
-        if (__popcll(m) >= 8) {
-            T x = in ? v : ident;
-#pragma unroll
-            for (int d = 1; d < 64; d <<= 1) {
-                const T y = shfl_up_t(x, d);
-                if (lane >= d) x = acc_comb(acc, y, x);
-            }
-            T excl = shfl_up_t(x, 1);
-            if (lane == 0) excl = ident;
-            const T total = shfl_t(x, 63);
-            T base = ident;
-            if (lane == f) base = rmw_lds<T>(tile + l0, acc, kind, total, ident, ident, ok, err);
-            base = shfl_t(base, f);
-            if (in) {
-                res = acc_comb(acc, base, excl);
-                done = true;
-            }
-        }
-    }
-    if (active && !done) res = rmw_lds<T>(tile + l, acc, kind, v, ident, ident, ok, err);
-    return res;
-}
-
-// OPT >= 0 fixes the op at compile time (hot paths); -1 reads it from the args.
-// Owner mode: one block per tile — load the tile into LDS, apply the tile's
-// records with LDS atomics, write it back. Kept free of the delta path's
-// register arrays so two 1024-thread blocks (2 x 64 KiB LDS) fit per CU.
-template <typename T, int OPT>
-__global__ __launch_bounds__(1024, 8) void k_tile_owner(TileArgs a) {
-    using U = typename bits_of<T>::U;
-    using W = typename word_of<T>::W;
-    extern __shared__ __align__(16) uint8_t lds_raw[];
-    W* tile = reinterpret_cast<W*>(lds_raw);
-    const TileItem w = a.items[blockIdx.x];
-    if (w.mode != 0) return;
-    const uint16_t* bin_lidx = a.bin_lidx;
-    const T* bin_val = reinterpret_cast<const T*>(a.bin_val);
-    int op = OPT >= 0 ? OPT : a.op;
-    T cmp = from_bits<T>(U(a.cmp_bits)), eps = from_bits<T>(U(a.eps_bits));
-    const T sv = from_bits<T>(U(a.val_bits));
-    int ret = a.ret;
-    const uint64_t base = uint64_t(w.tile) << a.tile_shift;
-    const uint32_t len = uint32_t(min(uint64_t(1) << a.tile_shift, a.shard_len - base));
-    T* shard = reinterpret_cast<T*>(a.shard) + base;
-    // 16 B per lane when the shard is 16-B aligned (sub-array views may not be)
-    const bool vec = sizeof(T) >= 4 && (reinterpret_cast<uintptr_t>(shard) & 15) == 0;
-    if constexpr (sizeof(T) >= 4) {
-        if (vec) {
-            constexpr uint32_t per = 16 / sizeof(T);
-            const uint32_t nv = len / per;
-            for (uint32_t v = threadIdx.x; v < nv; v += blockDim.x)
-                reinterpret_cast<uint4*>(tile)[v] = reinterpret_cast<const uint4*>(shard)[v];
-            for (uint32_t e = nv * per + threadIdx.x; e < len; e += blockDim.x) tile[e] = shard[e];
-        } else {
-            for (uint32_t e = threadIdx.x; e < len; e += blockDim.x) tile[e] = shard[e];   // W == T
-        }
-    } else {
-        for (uint32_t e = threadIdx.x; e < len; e += blockDim.x) tile[e] = W(U(shard[e]));   // widen the bits
-    }
-    __syncthreads();
-    // kOwnUnroll records per thread per round: all loads issued before the LDS atomics
-    constexpr int kOwnUnroll = 4;
-    constexpr bool kOwnVec = LMR_OWN_VEC != 0;
-    const uint32_t nrg = a.nreg ? a.nreg : 1u;
-    for (uint32_t rg = 0; rg < nrg; rg++) {
-    uint32_t lo = w.lo, hi = w.hi;
-    if (a.nreg) {
-        lo = a.rts[uint64_t(rg) * a.rstride + w.tile];
-        hi = a.rts[uint64_t(rg) * a.rstride + w.tile + 1];
-    }
-    if (OPT < 0 && a.mixed) {          // the region's op; its records after every earlier region's
-        op = a.rop[rg].op;
-        ret = a.rop[rg].ret;
-        cmp = from_bits<T>(U(a.rop[rg].cmp_bits));
-        eps = from_bits<T>(U(a.rop[rg].eps_bits));
-        if (rg) __syncthreads();
-    }
-    auto apply_one = [&](uint32_t r, uint32_t li, T vi) {
-        uint8_t ok = 0;
-        T old = rmw_lds<T>(tile + li, op, a.kind, vi, cmp, eps, ok, a.err);
-        if (ret != LMR_RET_NONE) {
-            reinterpret_cast<T*>(a.results)[r] = old;
-            if (ret == LMR_RET_RESULT) a.ok[r] = ok;
-        }
-    };
-    if constexpr (sizeof(T) == 4) {
-        // 4-byte values: 4 consecutive records per thread and iteration, one 8-B load of their
-        // offsets and one 16-B load of their values (fewer, wider memory instructions than a 2-B
-        // and a 4-B load per record); the unaligned head and the tail one record per thread.
-        // Measured: C5 tile sweep 0.378 -> 0.354 ms; for 8-byte values the same grouping lost
-        // (C2 tile 0.785 -> 0.80, C3 0.51 -> 0.54 ms), so they keep one record per load.
-        if (kOwnVec && !a.scalar && ((reinterpret_cast<uintptr_t>(bin_lidx) & 7) | (reinterpret_cast<uintptr_t>(bin_val) & 15)) == 0) {
-            const uint32_t a0 = min(hi, (lo + 3u) & ~3u);
-            const uint32_t a1 = a0 + ((hi - a0) & ~3u);
-            if (lo + threadIdx.x < a0) apply_one(lo + threadIdx.x, bin_lidx[lo + threadIdx.x], bin_val[lo + threadIdx.x]);
-            if (a1 + threadIdx.x < hi) apply_one(a1 + threadIdx.x, bin_lidx[a1 + threadIdx.x], bin_val[a1 + threadIdx.x]);
-            constexpr uint32_t kV = 2;           // groups of 4 records in flight per thread
-            const uint32_t g0 = a0 >> 2, g1 = a1 >> 2;
-            for (uint32_t q0 = g0 + threadIdx.x; q0 < g1; q0 += kV * 1024u) {
-                uint2 lw[kV];
-                T v[kV][4];
-#pragma unroll
-                for (uint32_t k = 0; k < kV; k++) {
-                    const uint32_t q = q0 + k * 1024u;
-                    if (q < g1) {
-                        lw[k] = reinterpret_cast<const uint2*>(bin_lidx)[q];
-                        const uint4 x = reinterpret_cast<const uint4*>(bin_val)[q];
-                        v[k][0] = from_bits<T>(U(x.x)); v[k][1] = from_bits<T>(U(x.y));
-                        v[k][2] = from_bits<T>(U(x.z)); v[k][3] = from_bits<T>(U(x.w));
-                    }
-                }
-#pragma unroll
-                for (uint32_t k = 0; k < kV; k++) {
-                    const uint32_t q = q0 + k * 1024u;
-                    if (q < g1) {
-                        apply_one(4 * q + 0, lw[k].x & 0xffffu, v[k][0]);
-                        apply_one(4 * q + 1, lw[k].x >> 16, v[k][1]);
-                        apply_one(4 * q + 2, lw[k].y & 0xffffu, v[k][2]);
-                        apply_one(4 * q + 3, lw[k].y >> 16, v[k][3]);
-                    }
-                }
-            }
-            continue;
-        }
-    }
-    for (uint32_t r0 = lo + threadIdx.x; r0 < hi; r0 += kOwnUnroll * 1024u) {
-        uint32_t l[kOwnUnroll];
-        T v[kOwnUnroll];
-#pragma unroll
-        for (int k = 0; k < kOwnUnroll; k++) {
-            const uint32_t r = r0 + uint32_t(k) * 1024u;
-            if (r < hi) {
-                l[k] = bin_lidx[r];
-                v[k] = a.scalar ? sv : bin_val[r];
-            }
-        }
-#pragma unroll
-        for (int k = 0; k < kOwnUnroll; k++) {
-            const uint32_t r = r0 + uint32_t(k) * 1024u;
-            if (r < hi) {
-                uint8_t ok = 0;
-                T old = rmw_lds<T>(tile + l[k], op, a.kind, v[k], cmp, eps, ok, a.err);
-                if (ret != LMR_RET_NONE) {
-                    reinterpret_cast<T*>(a.results)[r] = old;          // coalesced (binned order)
-                    if (ret == LMR_RET_RESULT) a.ok[r] = ok;
-                }
-            }
-        }
-    }
-    }
-    __syncthreads();
-    if (!op_is_read(op) || (OPT < 0 && a.mixed)) {
-        if constexpr (sizeof(T) >= 4) {
-            if (vec) {
-                constexpr uint32_t per = 16 / sizeof(T);
-                const uint32_t nv = len / per;
-                for (uint32_t v = threadIdx.x; v < nv; v += blockDim.x)
-                    reinterpret_cast<uint4*>(shard)[v] = reinterpret_cast<const uint4*>(tile)[v];
-                for (uint32_t e = nv * per + threadIdx.x; e < len; e += blockDim.x) shard[e] = tile[e];
-            } else {
-                for (uint32_t e = threadIdx.x; e < len; e += blockDim.x) shard[e] = tile[e];
-            }
-        } else {
-            for (uint32_t e = threadIdx.x; e < len; e += blockDim.x) shard[e] = T(U(tile[e]));
-        }
-    }
-}
-
-// Delta mode (combinable ops only; planned by k_tile_plan / k_stage_plan), persistent
-// over the delta list: combine kSplit records in an identity-initialised LDS
-// tile, push one device-scope atomic per touched element, rebuild fetch
-// results as base (+) the record's LDS prefix.
-template <typename T, int OPT>
-__global__ __launch_bounds__(1024) void k_tile_delta(TileArgs a) {
-    using U = typename bits_of<T>::U;
-    using W = typename word_of<T>::W;
-    extern __shared__ __align__(16) uint8_t lds_raw[];
-    W* tile = reinterpret_cast<W*>(lds_raw);
-    const int op = OPT >= 0 ? OPT : a.op;
-    const T cmp = from_bits<T>(U(a.cmp_bits)), eps = from_bits<T>(U(a.eps_bits));
-    const T sv = from_bits<T>(U(a.val_bits));
-    const int ret = a.ret;
-    const uint32_t nitems = *a.delta_count;
-    const uint16_t* bin_lidx = a.bin_lidx;
-    const T* bin_val = reinterpret_cast<const T*>(a.bin_val);
-    // floats: -0.0 is the identity of IEEE addition (-0.0 + x == x for every x, +0.0 and
-    // NaN included; +0.0 + -0.0 would be +0.0), and a - v is a + (-v) bit for bit, so a
-    // float sub piece accumulates -v and is applied as an add: base + (sum of its values)
-    // then keeps the sign of zero a serial chain of single RMWs gives
-    constexpr bool kFlt = is_flt<T>::v;
-    const bool fsub = kFlt && (op == LMR_OP_SUB || op == LMR_OP_FETCH_SUB);
-    const U ident_bits = (op == LMR_OP_AND || op == LMR_OP_FETCH_AND) ? ~U(0)
-                         : kFlt ? U(U(1) << (8 * sizeof(U) - 1)) : U(0);
-    W ident;
-    if constexpr (kFlt) ident = from_bits<T>(ident_bits);
-    else ident = W(ident_bits);
-    const int acc = delta_acc_op(op);
-    const int gop = fsub ? int(LMR_OP_FETCH_ADD) : delta_global_op(op);
-    const int fop = fsub ? int(LMR_OP_FETCH_ADD) : op;
-    // elements some record of the piece touched (fetch forms: only those need their base)
-    __shared__ uint32_t touched[16384 / 32];
-    for (uint32_t it = blockIdx.x; it < nitems; it += gridDim.x) {
-        const TileItem w = a.delta[it];
-        const uint64_t base = uint64_t(w.tile) << a.tile_shift;
-        const uint32_t len = uint32_t(min(uint64_t(1) << a.tile_shift, a.shard_len - base));
-        T* shard = reinterpret_cast<T*>(a.shard) + base;
-        for (uint32_t e = threadIdx.x; e < len; e += blockDim.x) tile[e] = ident;
-        if (ret != LMR_RET_NONE)
-            for (uint32_t e = threadIdx.x; e < (len + 31) / 32; e += blockDim.x) touched[e] = 0;
-        __syncthreads();
-        T pre[kSplit / 1024];
-#pragma unroll
-        for (int k = 0; k < int(kSplit / 1024); k++) {
-            const uint32_t r = w.lo + threadIdx.x + uint32_t(k) * 1024u;
-            const bool in = r < w.hi;
-            const uint32_t l = in ? bin_lidx[r] : 0u;
-            T v = !in ? T(0) : a.scalar ? sv : bin_val[r];
-            if (fsub) v = -v;
-            if (kWaveCombine) {
-                pre[k] = lds_acc_wave<T>(tile, l, v, in, acc, from_bits<T>(ident_bits), a.kind, a.err);
-            } else if (in) {
-                uint8_t ok = 0;
-                pre[k] = rmw_lds<T>(tile + l, acc, a.kind, v, cmp, eps, ok, a.err);
-            }
-            // the first record on an element sees the identity (later ones may too: harmless)
-            if (in && ret != LMR_RET_NONE && U(to_bits(pre[k])) == U(ident_bits)) atomicOr(&touched[l >> 5], 1u << (l & 31));
-        }
-        __syncthreads();
-        // one device-scope atomic per changed element, a load per touched unchanged one;
-        // every element's operation is issued before any result is waited for
-        constexpr int kPer = kTileBytes / int(sizeof(W)) / 1024;   // elements per thread (a tile's words / 1024)
-        T b[kPer];
-        bool need[kPer];
-#pragma unroll
-        for (int k = 0; k < kPer; k++) {
-            const uint32_t e = threadIdx.x + uint32_t(k) * 1024u;
-            need[k] = false;
-            if (e < len) {
-                T d;
-                if constexpr (sizeof(T) >= 4) d = tile[e];
-                else d = T(U(tile[e]));
-                uint8_t ok = 0;
-                if (U(to_bits(d)) != U(ident_bits)) {
-                    b[k] = rmw_global<T>(shard + e, gop, a.kind, d, cmp, eps, ok, a.err);
-                    need[k] = true;
-                } else if (ret != LMR_RET_NONE && ((touched[e >> 5] >> (e & 31)) & 1u)) {
-                    b[k] = rmw_global<T>(shard + e, LMR_OP_LOAD, a.kind, d, cmp, eps, ok, a.err);
-                    need[k] = true;
-                }
-            }
-        }
-        if (ret != LMR_RET_NONE) {
-#pragma unroll
-            for (int k = 0; k < kPer; k++) {
-                const uint32_t e = threadIdx.x + uint32_t(k) * 1024u;
-                if (need[k]) {
-                    if constexpr (sizeof(T) >= 4) tile[e] = b[k];
-                    else tile[e] = W(U(b[k]));
-                }
-            }
-            __syncthreads();
-#pragma unroll
-            for (int k = 0; k < int(kSplit / 1024); k++) {
-                const uint32_t r = w.lo + threadIdx.x + uint32_t(k) * 1024u;
-                if (r < w.hi) {
-                    const uint32_t l = bin_lidx[r];
-                    T bb;
-                    if constexpr (sizeof(T) >= 4) bb = tile[l];
-                    else bb = T(U(tile[l]));
-                    reinterpret_cast<T*>(a.results)[r] = delta_finish<T>(fop, bb, pre[k]);
-                }
-            }
-        }
-        __syncthreads();
-    }
-}
-
 // ---- un-partition of returned values ----------------------------------------
 // dst[k] = src[map[k]] over block-contiguous ranges of k (the forward pass's
 // chunks), so each block's reads stay within the runs its chunk produced and
@@ -1323,7 +946,9 @@ __device__ __forceinline__ void unpartition_range(const uint32_t* __restrict__ m
     const V* s = reinterpret_cast<const V*>(src);
     V* d = reinterpret_cast<V*>(dst);
     const uint32_t nt = blockDim.x;
-    // U records per thread per iteration: all U map loads, then all U gathers, then the stores
+    // U records per thread per iteration: all U map loads, then all U gathers, then the stores.
+    // Measured and not kept: a branch-free form (clamped loads, Ok flags gathered with the values,
+    // so every load stays in flight): C5 0.576 -> 0.572 ms, C3 0.619 -> 0.632 ms
     for (uint64_t k0 = lo + threadIdx.x; k0 < hi; k0 += uint64_t(U) * nt) {
         uint32_t p[U];
 #pragma unroll
@@ -1527,6 +1152,10 @@ static int coarse_rpt(int vb);
 // takes more than half the LDS (rounds of >= 8K records), two otherwise. G = 256
 // vs 512 on one box (tools/sweep_c2.sh): C2 4.40 -> 4.33 ms, C3 2.72 -> 2.47 ms
 // (larger producer chunks also keep the un-partition gathers local).
+static int ccount_split() {
+    static int v = env_int("LMR_CCOUNT_SPLIT", 1, 1, 16);   // (4: C5 count -0.027 ms, coarse +0.015)
+    return v;
+}
 static int bin_blocks_cap(int vb) {
     static int v = env_int("LMR_BIN_BLOCKS", 0, 0, kMaxBinBlocks);
     return v ? v : (coarse_rpt(vb) >= 8 ? 256 : 512);
@@ -1660,7 +1289,9 @@ static hipError_t launch_unpartition(int vb, const uint32_t* map, uint64_t n, co
 // split as launch_unpartition splits a single range
 static hipError_t launch_unpartition_multi(int vb, UnpartTable& t, hipStream_t s) {
     if (t.nr == 0) return hipSuccess;
-    const uint64_t sub = 32768 / uint64_t(vb);
+    static const int sub_env = env_int("LMR_UNPART_SUB", 0, 0, 1 << 20);   // records per block (A/B knob)
+    static const int uq = env_int("LMR_UNPART_U", 0, 0, 16);
+    const uint64_t sub = sub_env ? uint64_t(sub_env) : 32768 / uint64_t(vb);
     uint32_t blocks = 0;
     for (uint32_t i = 0; i < t.nr; i++) {
         UnpartRegion& g = t.r[i];
@@ -1672,10 +1303,15 @@ static hipError_t launch_unpartition_multi(int vb, UnpartTable& t, hipStream_t s
         g.block0 = blocks;
         blocks += uint32_t(Gu * split);
     }
+    const int u = uq ? uq : (vb >= 8 ? 4 : 16);
     auto go = [&](auto vbt) {
         constexpr int VB = decltype(vbt)::value;
-        constexpr int UU = VB >= 8 ? 4 : 16;
-        hipLaunchKernelGGL((k_unpartition_multi<VB, UU>), dim3(blocks), dim3(1024), 0, s, t);
+        auto with_u = [&](auto ut) {
+            hipLaunchKernelGGL((k_unpartition_multi<VB, decltype(ut)::value>), dim3(blocks), dim3(1024), 0, s, t);
+        };
+        if (u >= 16) with_u(std::integral_constant<int, 16>{});
+        else if (u >= 8) with_u(std::integral_constant<int, 8>{});
+        else with_u(std::integral_constant<int, 4>{});
     };
     switch (vb) {
     case 1: go(std::integral_constant<int, 1>{}); break;
@@ -1756,7 +1392,14 @@ static hipError_t launch_coarse_free(int index_size, int vb, int frpt, const Par
         constexpr int IW = decltype(iw)::value;
         dispatch_vb_rpt<4>(vb, frpt, [&](auto vbt, auto rpt) {
             constexpr int VBc = decltype(vbt)::value, R = decltype(rpt)::value;
-            hipLaunchKernelGGL((k_coarse_free<IW, VBc, R>), dim3(q.G), dim3(1024), size_t(q.num_tiles) * 4, s, q);
+            const bool pairs = kCoarsePairs && IW == 8 && VBc == 8 && (R % 2) == 0 && q.idx_stride == 8 && q.val &&
+                               q.val_stride == 8 && (q.chunk % 2) == 0 &&
+                               ((reinterpret_cast<uintptr_t>(q.idx) | reinterpret_cast<uintptr_t>(q.val)) & 15) == 0;
+            if (pairs)
+                hipLaunchKernelGGL((k_coarse_free<IW, VBc, R, (IW == 8 && VBc == 8 && R % 2 == 0)>), dim3(q.G), dim3(1024),
+                                   size_t(q.num_tiles) * 4, s, q);
+            else
+                hipLaunchKernelGGL((k_coarse_free<IW, VBc, R, false>), dim3(q.G), dim3(1024), size_t(q.num_tiles) * 4, s, q);
         });
         return hipGetLastError();
     });
@@ -1803,18 +1446,7 @@ static hipError_t launch_tile_sweep(int dtype, const ApplyArgs& a, const TiledWs
     t.rts = nullptr; t.nreg = 0; t.rstride = 0; t.mixed = 0;
     const bool delta = op_combines(a.op) && n > thresh;
     const unsigned dgrid = unsigned(std::min<uint64_t>(2 * ((n + kSplit - 1) / kSplit), uint64_t(tile_grid_cap())));
-    return dispatch_dtype(dtype, [&](auto tag) {
-        using Ty = decltype(tag);
-        auto go = [&](auto opt) {
-            constexpr int OPT = decltype(opt)::value;
-            hipLaunchKernelGGL((k_tile_owner<Ty, OPT>), dim3(T), dim3(1024), size_t(kTileBytes), s, t);
-            if (delta) hipLaunchKernelGGL((k_tile_delta<Ty, OPT>), dim3(dgrid), dim3(1024), size_t(kTileBytes), s, t);
-        };
-        if (a.op == LMR_OP_ADD) go(std::integral_constant<int, LMR_OP_ADD>{});
-        else if (a.op == LMR_OP_FETCH_ADD) go(std::integral_constant<int, LMR_OP_FETCH_ADD>{});
-        else go(std::integral_constant<int, -1>{});
-        return hipGetLastError();
-    });
+    return launch_tile_kernels(dtype, a.op, t, delta, dgrid, s);
 }
 
 // One tiled piece: a.n <= workspace capacity, a.n < 2^32.
@@ -1957,11 +1589,12 @@ hipError_t launch_apply_tiled(int dtype, int index_size, const ApplyArgs& a, con
 // instead each arriving record stream (a *region*) is partitioned into 64 KiB
 // shard tiles on arrival, inside its own slice of the workspace, and one tile
 // sweep at the end applies every region:
-//   per region : k_ccount (coarse histogram per producer block)
+//   per region : k_ccount (coarse histogram per producer block, tile totals)
 //                -> k_coarse_scatter (shared with the one-shot path; its blocks fold the
-//                   raw counts into their cursors, block 0 stores the bucket starts)
-//                -> k_piece_count (piece table) -> scan
-//                -> k_fine_piece (region tile starts; region now tile-sorted)
+//                   raw counts into their cursors, block 0 stores the bucket starts and
+//                   turns the tile totals into the region's tile starts)
+//                -> k_fine_piece (each round reserves its tile runs with one atomic per
+//                   tile; region now tile-sorted)
 //   finish     : k_stage_plan -> k_tile_owner over every region's
 //                range of its tile (+ k_tile_delta for hot tiles)
 //                -> k_unpartition_multi x 2 (every region's results back to arrival order)
@@ -1973,22 +1606,32 @@ hipError_t launch_apply_tiled(int dtype, int index_size, const ApplyArgs& a, con
 #define LMR_PIECE_RECORDS 16384                  // (variant builds for measurements: -DLMR_PIECE_RECORDS=...)
 #endif
 constexpr uint32_t kPiece = LMR_PIECE_RECORDS;   // records per fine-level piece (2 LDS rounds of 8K)
-constexpr int kStagePbase = 0;                   // sinfo words: pbase[kMaxCoarse + 1]
-constexpr int kStageBstart = 160;                //              bstart[kMaxCoarse + 1]
+constexpr int kStageBstart = 160;                // sinfo words: bstart[kMaxCoarse + 1]
 constexpr int kStageInb = 320;                   //              in-bounds records per region
 static_assert(kStageInb + kMaxRegions <= kStageInfoWords, "staged scratch");
 
 // per-(coarse bucket, producer block) record counts: coarse_off[c * G + g]
 // (16 lane-picked copies of the histogram, to spread the LDS atomics' address conflicts,
 // measured 0.35 -> 0.36 ms per C5 step: the pass is not bound by them)
+// Measured and dropped: per-thread private LDS counters instead of the shared histogram's
+// atomics (C5 count 0.33 -> 0.38 ms: 128 KB of LDS per block, zeroing and folding).
+// Every block also counts its records per tile (LDS atomics over T bins, few conflicts) into
+// its row of p.trows: k_coarse_scatter folds the rows into tile totals, k_fine_piece turns
+// them into tile starts and reserves each round's tile runs inside them.
 template <int IW>
 __global__ __launch_bounds__(1024) void k_ccount(PartArgs p) {
     constexpr int U = 8;              // loads in flight per thread (4: C5 count 0.347 -> 0.337 ms at 8)
     __shared__ uint32_t hist[kMaxCoarse];
+    extern __shared__ uint32_t thist[];   // [num_tiles]
     for (uint32_t c = threadIdx.x; c < p.C; c += blockDim.x) hist[c] = 0;
+    for (uint32_t t = threadIdx.x; t < p.num_tiles; t += blockDim.x) thist[t] = 0;
     __syncthreads();
-    const uint64_t lo = uint64_t(blockIdx.x) * p.chunk;
-    const uint64_t hi = min(lo + p.chunk, p.n);
+    // block b counts the sub-range b % csub of producer block b / csub's chunk
+    const uint32_t S = p.csub ? p.csub : 1u;
+    const uint64_t sub = (p.chunk + S - 1) / S;
+    const uint64_t g0 = uint64_t(blockIdx.x / S) * p.chunk;
+    const uint64_t lo = g0 + uint64_t(blockIdx.x % S) * sub;
+    const uint64_t hi = min(min(lo + sub, g0 + p.chunk), p.n);
     const int cshift = p.tile_shift + kFineShift;
     bool oob = false;
     for (uint64_t k0 = lo + threadIdx.x; k0 < hi; k0 += U * uint64_t(blockDim.x)) {
@@ -2004,12 +1647,15 @@ __global__ __launch_bounds__(1024) void k_ccount(PartArgs p) {
             if (k >= hi) continue;
             if (ix[j] >= p.shard_len) { oob = true; continue; }
             atomicAdd(&hist[uint32_t(ix[j] >> cshift)], 1u);
+            atomicAdd(&thist[uint32_t(ix[j] >> p.tile_shift)], 1u);
         }
     }
     if (oob) raise_err(p.err, LMR_ERRBIT_OOB);
     __syncthreads();
     for (uint32_t c = threadIdx.x; c < p.C; c += blockDim.x)
-        p.coarse_off[uint64_t(c) * p.G + blockIdx.x] = hist[c];
+        p.coarse_off[uint64_t(c) * p.G * S + blockIdx.x] = hist[c];
+    uint32_t* row = p.trows + uint64_t(blockIdx.x) * p.num_tiles;
+    for (uint32_t t = threadIdx.x; t < p.num_tiles; t += blockDim.x) row[t] = thist[t];
 }
 
 struct PieceArgs {
@@ -2019,18 +1665,18 @@ struct PieceArgs {
     int tile_shift;
     uint32_t num_tiles;
     uint32_t C;
-    uint32_t* pbase;            // [C + 1] first piece of bucket c; pbase[C] = pieces (k_piece_count writes it)
     uint32_t* bstart;           // [C + 1] first temp slot of bucket c; bstart[C] = in-bounds records
-    uint32_t* cnt;              // (c, f, p) tile counts at pbase[c]*kFine + f*np_c + p, then their scan
     uint16_t* bin_lidx;         // workspace bases (binned positions are absolute)
     uint8_t* bin_val;
     uint32_t* rpos;             // region temp slot -> binned position (null: nothing returned)
     uint32_t R;                 // the region's first workspace slot
     uint32_t* ts;               // out: the region's tile starts (absolute binned positions)
+    const uint32_t* ttot;       // the region's tile totals (k_coarse_scatter)
+    uint32_t* tfill;            // per-tile records placed so far (zeroed by k_coarse_scatter)
 };
 
 // bucket starts (k_coarse_scatter's) -> pieces of kPiece records, computed by every block
-// of k_piece_count into its LDS (C <= 128 loads); block 0 also stores pbase for k_fine_piece
+// of k_fine_piece into its LDS (C <= 128 loads)
 __device__ void piece_table(const uint32_t* bstart, uint32_t C, uint32_t* pb_s, uint32_t* bs_s, uint32_t* np_s,
                             uint32_t* tot) {
     const uint32_t c = threadIdx.x;
@@ -2070,58 +1716,6 @@ __device__ __forceinline__ PieceLoc piece_loc(const uint32_t* pbase, const uint3
     L.hi = min(L.lo + kPiece, bstart[lo_c + 1]);
     return L;
 }
-__device__ __forceinline__ PieceLoc piece_loc(const PieceArgs& a, uint32_t pid) {
-    return piece_loc(a.pbase, a.bstart, a.C, pid);
-}
-
-// per-piece tile histogram (one block per piece; grid = upper bound of pieces). The
-// count entries of pieces past the table's end are never read (the scan folds them in
-// after every live entry), so nothing clears them.
-__global__ __launch_bounds__(1024) void k_piece_count(PieceArgs a) {
-    __shared__ uint32_t hist[kFine];
-    __shared__ uint32_t s_pb[kMaxCoarse + 1], s_bs[kMaxCoarse + 1], s_np[kMaxCoarse], s_tot;
-    piece_table(a.bstart, a.C, s_pb, s_bs, s_np, &s_tot);
-    if (blockIdx.x == 0)
-        for (uint32_t c = threadIdx.x; c <= a.C; c += blockDim.x) a.pbase[c] = s_pb[c];
-    const uint32_t pid = blockIdx.x;
-    if (pid >= s_pb[a.C]) return;
-    const PieceLoc L = piece_loc(s_pb, s_bs, a.C, pid);
-    const uint32_t t0 = L.c * kFine;
-    if (threadIdx.x < kFine) hist[threadIdx.x] = 0;
-    __syncthreads();
-    constexpr int U = 4;
-    for (uint32_t k0 = L.lo + threadIdx.x; k0 < L.hi; k0 += U * 1024u) {
-        uint32_t ix[U];
-#pragma unroll
-        for (int j = 0; j < U; j++) {
-            const uint32_t k = k0 + uint32_t(j) * 1024u;
-            ix[j] = k < L.hi ? a.tmp_idx[k] : 0u;
-        }
-#pragma unroll
-        for (int j = 0; j < U; j++)
-            if (k0 + uint32_t(j) * 1024u < L.hi) atomicAdd(&hist[(ix[j] >> a.tile_shift) - t0], 1u);
-    }
-    __syncthreads();
-    const uint32_t nf = min(uint32_t(kFine), a.num_tiles - t0);
-    if (threadIdx.x < nf)
-        a.cnt[uint64_t(s_pb[L.c]) * kFine + uint64_t(threadIdx.x) * L.np + L.p] = hist[threadIdx.x];
-}
-
-// the region's tile starts (absolute binned positions) from the scanned piece counts;
-// pb / bs: the piece table (k_fine_piece's LDS copy)
-__device__ __forceinline__ void region_starts(const PieceArgs& a, const uint32_t* pb, const uint32_t* bs) {
-    const uint32_t inb = bs[a.C];
-    for (uint32_t t = blockIdx.x * blockDim.x + threadIdx.x; t <= a.num_tiles; t += gridDim.x * blockDim.x) {
-        if (t == a.num_tiles) {
-            a.ts[t] = a.R + inb;
-            continue;
-        }
-        const uint32_t c = t >> kFineShift, f = t & (kFine - 1);
-        const uint32_t np = pb[c + 1] - pb[c];
-        const uint64_t e = uint64_t(pb[c]) * kFine + uint64_t(f) * np;
-        a.ts[t] = a.R + (e < uint64_t(pb[a.C]) * kFine ? a.cnt[e] : inb);
-    }
-}
 
 // fine level: each piece counting-sorted by tile in LDS rounds, written at its
 // final binned positions (persistent over pieces)
@@ -2130,23 +1724,27 @@ __global__ __launch_bounds__(1024) void k_fine_piece(PieceArgs a) {
     using V = typename idx_t<VB>::I;
     constexpr uint32_t kRound = RPT * 1024;
     __shared__ uint32_t hist[kFine], base[kFine], cursor[kFine], tot;
-    __shared__ uint32_t s_pb[kMaxCoarse + 1], s_bs[kMaxCoarse + 1];   // the piece table, for piece_loc
+    __shared__ uint32_t s_pb[kMaxCoarse + 1], s_bs[kMaxCoarse + 1], s_np[kMaxCoarse], s_tot;   // piece table
     __shared__ uint16_t s_l[kRound];
     __shared__ V s_val[kRound];
-    for (uint32_t c = threadIdx.x; c <= a.C; c += blockDim.x) {
-        s_pb[c] = a.pbase[c];
-        s_bs[c] = a.bstart[c];
-    }
-    __syncthreads();
-    region_starts(a, s_pb, s_bs);
+    __shared__ uint32_t s_tt[kFine], s_start[kFine];
+    piece_table(a.bstart, a.C, s_pb, s_bs, s_np, &s_tot);
     const uint32_t npieces = s_pb[a.C];
+    // tile starts of buckets with no piece (all their tiles empty) and the region's end
+    if (blockIdx.x == 0) {
+        for (uint32_t t = threadIdx.x; t < a.num_tiles; t += blockDim.x) {
+            const uint32_t c = t >> kFineShift;
+            if (s_pb[c + 1] == s_pb[c]) a.ts[t] = a.R + s_bs[c];
+        }
+        if (threadIdx.x == 0) a.ts[a.num_tiles] = a.R + s_bs[a.C];
+    }
     const uint32_t lmask = (1u << a.tile_shift) - 1u;
     const V sv = V(a.scalar_bits);
-    // the next round's records and the next piece's tile cursors are loaded into
-    // registers while the current round is ranked and written out
+    // the next round's records are loaded into registers while the current round is
+    // ranked and written out; each round reserves its tile runs with one atomic per tile
+    // (positions within a tile follow no input order: the tile sweep applies them with atomics)
     uint32_t m_idx[RPT];
     V m_val[RPT];
-    uint32_t pf_cur = 0;
     auto load_round = [&](uint32_t r0, uint32_t hi) {
 #pragma unroll
         for (int j = 0; j < RPT; j++) {
@@ -2156,12 +1754,7 @@ __global__ __launch_bounds__(1024) void k_fine_piece(PieceArgs a) {
             m_val[j] = in ? (a.tmp_val ? reinterpret_cast<const V*>(a.tmp_val)[k] : sv) : V(0);
         }
     };
-    auto load_piece = [&](const PieceLoc& L) {
-        load_round(L.lo, L.hi);
-        const uint32_t nf = min(uint32_t(kFine), a.num_tiles - L.c * kFine);
-        if (threadIdx.x < nf)
-            pf_cur = a.R + a.cnt[uint64_t(s_pb[L.c]) * kFine + uint64_t(threadIdx.x) * L.np + L.p];
-    };
+    auto load_piece = [&](const PieceLoc& L) { load_round(L.lo, L.hi); };
     uint32_t pid = blockIdx.x;
     PieceLoc L{};
     if (pid < npieces) {
@@ -2171,7 +1764,16 @@ __global__ __launch_bounds__(1024) void k_fine_piece(PieceArgs a) {
     for (; pid < npieces; pid += gridDim.x) {
         const uint32_t t0 = L.c * kFine;
         const uint32_t nf = min(uint32_t(kFine), a.num_tiles - t0);
-        if (threadIdx.x < nf) cursor[threadIdx.x] = pf_cur;
+        // this bucket's tile starts: bucket start + the tile totals before each tile; the
+        // bucket's first piece publishes them as the region's tile starts
+        if (threadIdx.x < kFine) s_tt[threadIdx.x] = threadIdx.x < nf ? a.ttot[t0 + threadIdx.x] : 0u;
+        __syncthreads();
+        small_excl_scan(s_tt, s_start, nf, &tot);
+        __syncthreads();
+        if (threadIdx.x < nf) {
+            s_start[threadIdx.x] += a.R + s_bs[L.c];
+            if (L.p == 0) a.ts[t0 + threadIdx.x] = s_start[threadIdx.x];
+        }
         const uint32_t nxt = pid + gridDim.x;
         PieceLoc LN{};
         if (nxt < npieces) LN = piece_loc(s_pb, s_bs, a.C, nxt);
@@ -2185,6 +1787,10 @@ __global__ __launch_bounds__(1024) void k_fine_piece(PieceArgs a) {
                 if (r0 + uint32_t(j) * 1024 + threadIdx.x < L.hi) m_rank[j] = atomicAdd(&hist[m_f[j]], 1u);
             }
             __syncthreads();
+            if (threadIdx.x < nf) {
+                const uint32_t h = hist[threadIdx.x];
+                cursor[threadIdx.x] = h ? s_start[threadIdx.x] + atomicAdd(&a.tfill[t0 + threadIdx.x], h) : 0u;
+            }
             small_excl_scan(hist, base, nf, &tot);
             __syncthreads();
 #pragma unroll
@@ -2204,7 +1810,6 @@ __global__ __launch_bounds__(1024) void k_fine_piece(PieceArgs a) {
                 reinterpret_cast<V*>(a.bin_val)[dst] = s_val[q];
             });
             __syncthreads();
-            for (uint32_t f = threadIdx.x; f < nf; f += blockDim.x) cursor[f] += hist[f];
         }
         __syncthreads();
         L = LN;
@@ -2314,7 +1919,6 @@ hipError_t launch_stage_region(int dtype, int index_size, const ApplyArgs& a, co
     uint64_t G = (a.n + 65535) / 65536;
     if (G > uint64_t(bin_blocks_cap(vb))) G = bin_blocks_cap(vb);
     if (G < 1) G = 1;
-    uint32_t* pbase = w.sinfo + kStagePbase;
     uint32_t* bstart = w.sinfo + kStageBstart;
     uint32_t* inb = w.sinfo + kStageInb + r;
     PartArgs q{};
@@ -2327,11 +1931,18 @@ hipError_t launch_stage_region(int dtype, int index_size, const ApplyArgs& a, co
     q.qpos = has_res ? w.qpos + R : nullptr;
     q.err = a.err;
     q.bstart_out = bstart; q.total_out = inb;       // raw counts: k_coarse_scatter derives its offsets
+    // the count pass runs csub blocks per producer block: one 1024-thread block per CU leaves
+    // the read-only pass at half occupancy
+    q.csub = uint32_t(std::max<uint64_t>(1, std::min<uint64_t>(ccount_split(), uint64_t(kMaxBinBlocks) / G)));
+    q.trows = w.counts;                             // G * csub rows of T counts (<= kMaxBinBlocks x kMaxTiles)
+    q.ttot = w.tile_items;
+    q.tfill = w.ff + 64 + size_t(kMaxCoarse) * kSegs;
     hipError_t e;
     {
         ProfScope ps(a.prof, LMR_STAGE_BIN_COUNT, st, a.n);
         e = dispatch_iw(index_size, [&](auto iw) {
-            hipLaunchKernelGGL((k_ccount<decltype(iw)::value>), dim3(unsigned(G)), dim3(1024), 0, st, q);
+            constexpr int IW = decltype(iw)::value;
+            hipLaunchKernelGGL((k_ccount<IW>), dim3(unsigned(G * q.csub)), dim3(1024), size_t(T) * 4, st, q);
             return hipGetLastError();
         });
     }
@@ -2350,16 +1961,13 @@ hipError_t launch_stage_region(int dtype, int index_size, const ApplyArgs& a, co
     if (e != hipSuccess) return e;
     PieceArgs pa;
     pa.tmp_idx = q.tmp_idx; pa.tmp_val = q.tmp_val; pa.scalar_bits = a.val_bits;
-    pa.tile_shift = shift; pa.num_tiles = T; pa.C = C; pa.pbase = pbase; pa.bstart = bstart;
-    pa.cnt = w.counts; pa.bin_lidx = w.bin_lidx; pa.bin_val = w.bin_val;
+    pa.tile_shift = shift; pa.num_tiles = T; pa.C = C; pa.bstart = bstart;
+    pa.bin_lidx = w.bin_lidx; pa.bin_val = w.bin_val;
     pa.rpos = has_res ? w.rpos + R : nullptr; pa.R = R;
-    pa.ts = w.rts + uint64_t(r) * (kMaxTiles + 1);
+    pa.ts = w.rts + uint64_t(r) * (kMaxTiles + 1); pa.ttot = q.ttot; pa.tfill = q.tfill;
     const uint64_t max_pieces = (a.n + kPiece - 1) / kPiece + C;
     {
         ProfScope ps(a.prof, LMR_STAGE_FINE_SCATTER, st, a.n);
-        hipLaunchKernelGGL(k_piece_count, dim3(unsigned(max_pieces)), dim3(1024), 0, st, pa);
-        e = scan_exclusive_u32(w.counts, max_pieces * kFine, w.partials, nullptr, st);
-        if (e != hipSuccess) return e;
         const unsigned fgrid = unsigned(std::min<uint64_t>(max_pieces, uint64_t(fine_blocks_cap())));
         dispatch_vb_rpt<2>(vb, piece_fine_rpt(vb), [&](auto vbt, auto rpt) {
             constexpr int VBc = decltype(vbt)::value, RP = decltype(rpt)::value;
@@ -2419,22 +2027,14 @@ hipError_t launch_stage_finish(const TiledWs& w, StageSession& s, hipStream_t st
         const bool delta = !mixed && op_combines(a.op) && s.staged > thresh;
         const unsigned dgrid = unsigned(std::min<uint64_t>(2 * ((s.staged + kSplit - 1) / kSplit) + 2 * uint64_t(s.nreg),
                                                            uint64_t(tile_grid_cap())));
-        e = dispatch_dtype(dtype, [&](auto tag) {
-            using Ty = decltype(tag);
-            auto go = [&](auto opt) {
-                constexpr int OPT = decltype(opt)::value;
-                hipLaunchKernelGGL((k_tile_owner<Ty, OPT>), dim3(T), dim3(1024), size_t(kTileBytes), st, t);
-                if (delta) hipLaunchKernelGGL((k_tile_delta<Ty, OPT>), dim3(dgrid), dim3(1024), size_t(kTileBytes), st, t);
-            };
-            if (!mixed && a.op == LMR_OP_ADD) go(std::integral_constant<int, LMR_OP_ADD>{});
-            else if (!mixed && a.op == LMR_OP_FETCH_ADD) go(std::integral_constant<int, LMR_OP_FETCH_ADD>{});
-            else go(std::integral_constant<int, -1>{});
-            return hipGetLastError();
-        });
+        e = launch_tile_kernels(dtype, mixed ? -1 : a.op, t, delta, dgrid, st);
     }
     if (e == hipSuccess && has_res) {
         // binned -> temp slot (in-bounds slots of each region) -> arrival order
-        ProfScope pu(a.prof, LMR_STAGE_UNPARTITION, st, s.staged);
+        uint64_t n_ret = 0;                                       // records whose op returns a value
+        for (int r = 0; r < s.nreg; r++)
+            if (s.reg[r].results && s.reg[r].ret != LMR_RET_NONE) n_ret += s.reg[r].n;
+        ProfScope pu(a.prof, LMR_STAGE_UNPARTITION, st, n_ret);
         uint8_t* tmpres = w.bin_val;                              // bins are free after the tile sweep
         uint8_t* ok_tmp_all = (a.ret == LMR_RET_RESULT) ? reinterpret_cast<uint8_t*>(w.bin_lidx) : nullptr;
         const uint8_t* ok_src_all = (a.ret == LMR_RET_RESULT) ? ok_bin : nullptr;

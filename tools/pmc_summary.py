@@ -22,9 +22,8 @@ STAGES = {
                     ("k_coarse_free", "k_coarse_scatter", "k_coarse_offsets", "k_bin_scatter")),
     "fine_scatter": (("k_fine_free", "k_fine_scatter", "k_fine_piece"),
                      ("k_fine_free", "k_fine_scatter", "k_fine_piece", "k_piece_count", "k_free_tile_totals")),
-    "tile_apply": (("k_tile_owner",), ("k_tile_owner", "k_tile_delta", "k_tile_plan_count", "k_stage_plan_count",
-                                       "k_tile_plan_fill", "k_stage_plan_fill")),
-    "unpartition": (("k_tile_owner",), ("k_unpartition",)),
+    "tile_apply": (("k_tile_owner",), ("k_tile_owner", "k_tile_delta", "k_tile_plan", "k_stage_plan")),
+    "unpartition": (("k_tile_owner",), ("k_unpartition", "k_unpartition_multi")),
     "direct": (("k_apply_direct",), ("k_apply_direct",)),
     "pack": (("k_pack_count", "k_pack_stage"), ("k_pack_count", "k_pack_scatter", "k_pack_stage", "k_dest_offsets",
                                                  "k_fill_counts")),
