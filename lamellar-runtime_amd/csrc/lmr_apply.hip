@@ -1634,6 +1634,8 @@ __global__ __launch_bounds__(1024) void k_ccount(PartArgs p) {
     const uint64_t hi = min(min(lo + sub, g0 + p.chunk), p.n);
     const int cshift = p.tile_shift + kFineShift;
     bool oob = false;
+    // (measured and not kept: the next U indices loaded before the current ones are counted,
+    // C5 count 0.371 -> 0.366-0.387 ms)
     for (uint64_t k0 = lo + threadIdx.x; k0 < hi; k0 += U * uint64_t(blockDim.x)) {
         uint64_t ix[U];
 #pragma unroll
@@ -1787,6 +1789,8 @@ __global__ __launch_bounds__(1024) void k_fine_piece(PieceArgs a) {
                 if (r0 + uint32_t(j) * 1024 + threadIdx.x < L.hi) m_rank[j] = atomicAdd(&hist[m_f[j]], 1u);
             }
             __syncthreads();
+            // (measured and not kept: the reservations' results consumed after the LDS staging,
+            // rpos written after a barrier: C5 fine 0.613 -> 0.63 ms, C3 0.443 -> 0.47 ms)
             if (threadIdx.x < nf) {
                 const uint32_t h = hist[threadIdx.x];
                 cursor[threadIdx.x] = h ? s_start[threadIdx.x] + atomicAdd(&a.tfill[t0 + threadIdx.x], h) : 0u;
