@@ -593,6 +593,9 @@ def e2e(lam, team, W, args):
     return out
 
 
+_PINNED_KEEP = []
+
+
 def e2e_wire(lam, team, W, args):
     """The reference's own op-buffer bytes in host memory: IdxVal<u32,u64> records
     (16 B, repr(C)), applied by lmr_apply_mvmi_host (pieces uploaded / applied /
@@ -612,6 +615,7 @@ def e2e_wire(lam, team, W, args):
     olds = np.empty(W.n, dtype=np.uint64)
     k.host_register(buf)
     k.host_register(olds)
+    _PINNED_KEEP.extend([buf, olds])      # registered ranges stay allocated (see tests/test_gpu_host.py)
     try:
         shard, slen = W.arr.local_shard(), W.arr.num_elems_local()
         kind = int(W.arr.kind)

@@ -21,6 +21,13 @@ def to_dev(a):
     return torch.from_numpy(np.ascontiguousarray(a).view(np.uint8).copy()).cuda()
 
 
+# Host ranges that were registered stay allocated for the rest of the process: after
+# hipHostUnregister the runtime may still map the range, and a later pageable copy from memory
+# that reuses those addresses (a freed numpy buffer handed out again) then faulted on the device
+# ("illegal memory access" at the next test's first host-to-device copy, twice in round 3).
+_KEEP = []
+
+
 @pytest.mark.parametrize("dt,op,register", [("u64", ADD, True), ("u64", FETCH_ADD, True), ("u32", XOR, False),
                                             ("i64", FETCH_ADD, False), ("u32", CAS, True), ("f64", FETCH_ADD, True)])
 def test_apply_mvmi_host_matches_oracle(world, orc, lam, dt, op, register):
@@ -48,8 +55,10 @@ def test_apply_mvmi_host_matches_oracle(world, orc, lam, dt, op, register):
     h_ok = np.zeros(n, dtype=np.uint8) if rk == 2 else None
     if register:
         k.host_register(buf)
+        _KEEP.append(buf)
         if h_res is not None:
             k.host_register(h_res)
+            _KEEP.append(h_res)
     try:
         cb = dt_obj.to_bits(cur) if cur is not None else 0
         k.apply_mvmi_host(d_shard, shard_len, kind, dt_obj, op, buf, iw, h_res, h_ok, cb, 0)
