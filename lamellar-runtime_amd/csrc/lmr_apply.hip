@@ -265,6 +265,11 @@ struct PartArgs {
     uint32_t* trows;              // staged regions: [G * csub][num_tiles] per-count-block tile counts (k_ccount)
     uint32_t* ttot;               // staged regions: [num_tiles] tile totals (k_coarse_scatter folds the rows)
     uint32_t* tfill;              // staged regions: [num_tiles] fine-pass fill counters (zeroed by k_coarse_scatter)
+    // staged returning regions, round-wise second un-partition gather (crt non-null): qpos[k] is
+    // record k's position in its coarse round's LDS staging, and each round's bucket runs are
+    // recorded, crt[g * rpb + round][c] = {temp start, length}
+    uint32_t* crt;
+    uint32_t rpb;                 // rounds per producer block
 };
 
 __device__ __forceinline__ void small_excl_scan(const uint32_t* hist, uint32_t* base, uint32_t m, uint32_t* tot);
@@ -422,7 +427,13 @@ __global__ __launch_bounds__(1024) void k_coarse_scatter(PartArgs p) {
             const uint32_t q = base[m_c[j]] + m_rank[j];
             s_idx[q] = uint32_t(m_raw[j]);
             s_val[q] = m_val[j];
-            if (p.qpos) p.qpos[k] = cursor[m_c[j]] + m_rank[j];   // coalesced in k
+            if (p.qpos) p.qpos[k] = p.crt ? q : cursor[m_c[j]] + m_rank[j];   // coalesced in k
+        }
+        if (p.crt && threadIdx.x < kMaxCoarse) {
+            uint32_t* rr = p.crt + (uint64_t(g) * p.rpb + (r0 - lo) / kRound) * (2 * kMaxCoarse) + 2 * threadIdx.x;
+            const bool in = threadIdx.x < C;
+            rr[0] = in ? cursor[threadIdx.x] : 0u;
+            rr[1] = in ? hist[threadIdx.x] : 0u;
         }
         if (r0 + kRound < hi) load_round(r0 + kRound);     // prefetch the next round
         __syncthreads();
@@ -1092,6 +1103,11 @@ uint64_t max_rec_cap() {
     return (uint64_t(0xFFFFFFFFull) - uint64_t(kMaxCoarse) * 8192) / 9 * 4;
 }
 
+// fine rounds of staged regions (>= 4K records each, up to 4 partial rounds per bucket and region)
+static uint64_t rt_rounds_for(uint64_t cap) { return cap / 4096 + uint64_t(kMaxRegions) * (kMaxCoarse + 2) * 4; }
+// coarse rounds of staged regions (>= 4K records each, one partial round per producer block of <= 64K)
+static uint64_t crt_rounds_for(uint64_t cap) { return cap / 4096 + cap / 65536 + uint64_t(kMaxRegions) * 2; }
+
 size_t tiled_ws_bytes(uint64_t cap) {
     size_t b = 0;
     auto al = [](size_t x) { return (x + 255) & ~size_t(255); };
@@ -1106,6 +1122,9 @@ size_t tiled_ws_bytes(uint64_t cap) {
     b += al(size_t(kMaxRegions) * (kMaxTiles + 1) * 4);             // staged regions' tile starts
     b += al(size_t(kStageInfoWords) * 4);                            // staged piece table / totals
     b += al(ff_words() * 4);                                         // count-free fill counters
+    b += al(rt_rounds_for(cap) * 256 * 4);                           // staged run tables
+    b += al(size_t(kMaxRegions) * 2 * (kMaxCoarse + 1) * 4);         // staged piece tables
+    b += al(crt_rounds_for(cap) * 256 * 4);                          // staged coarse run tables
     return b;
 }
 
@@ -1133,7 +1152,13 @@ TiledWs carve_tiled_ws(uint8_t* base, uint64_t cap) {
     p += al((size_t(kMaxTiles) + 2 * (cap / kSplit) + 2) * 16);
     w.rts = reinterpret_cast<uint32_t*>(p); p += al(size_t(kMaxRegions) * (kMaxTiles + 1) * 4);
     w.sinfo = reinterpret_cast<uint32_t*>(p); p += al(size_t(kStageInfoWords) * 4);
-    w.ff = reinterpret_cast<uint32_t*>(p);
+    w.ff = reinterpret_cast<uint32_t*>(p); p += al(ff_words() * 4);
+    w.runtab = reinterpret_cast<uint32_t*>(p); p += al(rt_rounds_for(cap) * 256 * 4);
+    w.ptab = reinterpret_cast<uint32_t*>(p);
+    w.rt_rounds = rt_rounds_for(cap);
+    p += al(size_t(kMaxRegions) * 2 * (kMaxCoarse + 1) * 4);
+    w.crtab = reinterpret_cast<uint32_t*>(p);
+    w.crt_rounds = crt_rounds_for(cap);
     w.cap = cap;
     w.tmp_cap = tmp_cap_for(cap);
     return w;
@@ -1152,6 +1177,14 @@ static int coarse_rpt(int vb);
 // takes more than half the LDS (rounds of >= 8K records), two otherwise. G = 256
 // vs 512 on one box (tools/sweep_c2.sh): C2 4.40 -> 4.33 ms, C3 2.72 -> 2.47 ms
 // (larger producer chunks also keep the un-partition gathers local).
+// Staged regions' un-partition gathers round-wise through LDS (LMR_UNPART_ROUNDS bits): 1 = the
+// first gather (k_unpart_rounds, fine rounds), 2 = the second (k_unpart_crounds, coarse rounds)
+// for values of <= 4 bytes, 4 = the second for 8-byte values. The coarse round gather of 8-byte
+// values holds a 12K-record round (108 KB of LDS, one block per CU): C3 0.52 -> 0.64 ms
+static int unpart_rounds() {
+    static int v = env_int("LMR_UNPART_ROUNDS", 3, 0, 7);
+    return v;
+}
 static int ccount_split() {
     static int v = env_int("LMR_CCOUNT_SPLIT", 1, 1, 16);   // (4: C5 count -0.027 ms, coarse +0.015)
     return v;
@@ -1620,7 +1653,10 @@ static_assert(kStageInb + kMaxRegions <= kStageInfoWords, "staged scratch");
 // them into tile starts and reserves each round's tile runs inside them.
 template <int IW>
 __global__ __launch_bounds__(1024) void k_ccount(PartArgs p) {
-    constexpr int U = 8;              // loads in flight per thread (4: C5 count 0.347 -> 0.337 ms at 8)
+    // loads in flight per thread (4: C5 count 0.347 -> 0.337 ms at 8; 16: 0.380 -> 0.398 ms)
+    constexpr int U = 8;
+    // the bucket counts derived from the tile counts after the loop (one LDS atomic per record)
+    constexpr bool kDerive = true;
     __shared__ uint32_t hist[kMaxCoarse];
     extern __shared__ uint32_t thist[];   // [num_tiles]
     for (uint32_t c = threadIdx.x; c < p.C; c += blockDim.x) hist[c] = 0;
@@ -1648,12 +1684,24 @@ __global__ __launch_bounds__(1024) void k_ccount(PartArgs p) {
             const uint64_t k = k0 + uint64_t(j) * blockDim.x;
             if (k >= hi) continue;
             if (ix[j] >= p.shard_len) { oob = true; continue; }
-            atomicAdd(&hist[uint32_t(ix[j] >> cshift)], 1u);
+            if (!kDerive) atomicAdd(&hist[uint32_t(ix[j] >> cshift)], 1u);
             atomicAdd(&thist[uint32_t(ix[j] >> p.tile_shift)], 1u);
         }
     }
     if (oob) raise_err(p.err, LMR_ERRBIT_OOB);
     __syncthreads();
+    if (kDerive) {
+        // bucket c's count = its 128 tiles' counts: wave w sums buckets w, w + 16, ...
+        const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+        for (uint32_t c = wv; c < p.C; c += blockDim.x >> 6) {
+            const uint32_t t0 = c * kFine + 2 * lane;
+            uint32_t x = (t0 < p.num_tiles ? thist[t0] : 0u) + (t0 + 1 < p.num_tiles ? thist[t0 + 1] : 0u);
+#pragma unroll
+            for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o, 64);
+            if (lane == 0) hist[c] = x;
+        }
+        __syncthreads();
+    }
     for (uint32_t c = threadIdx.x; c < p.C; c += blockDim.x)
         p.coarse_off[uint64_t(c) * p.G * S + blockIdx.x] = hist[c];
     uint32_t* row = p.trows + uint64_t(blockIdx.x) * p.num_tiles;
@@ -1675,6 +1723,13 @@ struct PieceArgs {
     uint32_t* ts;               // out: the region's tile starts (absolute binned positions)
     const uint32_t* ttot;       // the region's tile totals (k_coarse_scatter)
     uint32_t* tfill;            // per-tile records placed so far (zeroed by k_coarse_scatter)
+    // round-wise un-partition (rt non-null): rpos[k] is slot k's position in its round's LDS
+    // staging, and each round's tile runs are recorded, rt[round][f] = {binned start, length}
+    // (round = piece * rpp + the round within the piece), with the piece table in ptab
+    // (pbase[C + 1], bstart[C + 1]): k_unpart_rounds reads each round's runs back whole
+    uint32_t* rt;
+    uint32_t* ptab;
+    uint32_t rpp;               // rounds per piece
 };
 
 // bucket starts (k_coarse_scatter's) -> pieces of kPiece records, computed by every block
@@ -1732,6 +1787,11 @@ __global__ __launch_bounds__(1024) void k_fine_piece(PieceArgs a) {
     __shared__ uint32_t s_tt[kFine], s_start[kFine];
     piece_table(a.bstart, a.C, s_pb, s_bs, s_np, &s_tot);
     const uint32_t npieces = s_pb[a.C];
+    if (a.rt && blockIdx.x == 0)
+        for (uint32_t c = threadIdx.x; c <= a.C; c += blockDim.x) {
+            a.ptab[c] = s_pb[c];
+            a.ptab[a.C + 1 + c] = s_bs[c];
+        }
     // tile starts of buckets with no piece (all their tiles empty) and the region's end
     if (blockIdx.x == 0) {
         for (uint32_t t = threadIdx.x; t < a.num_tiles; t += blockDim.x) {
@@ -1804,7 +1864,13 @@ __global__ __launch_bounds__(1024) void k_fine_piece(PieceArgs a) {
                 const uint32_t q = base[m_f[j]] + m_rank[j];
                 s_l[q] = uint16_t(m_idx[j] & lmask);
                 s_val[q] = m_val[j];
-                if (a.rpos) a.rpos[k] = cursor[m_f[j]] + m_rank[j];
+                if (a.rpos) a.rpos[k] = a.rt ? q : cursor[m_f[j]] + m_rank[j];
+            }
+            if (a.rt && threadIdx.x < kFine) {
+                uint32_t* rr = a.rt + (uint64_t(pid) * a.rpp + (r0 - L.lo) / kRound) * (2 * kFine) + 2 * threadIdx.x;
+                const bool in = threadIdx.x < nf;
+                rr[0] = in ? cursor[threadIdx.x] : 0u;
+                rr[1] = in ? hist[threadIdx.x] : 0u;
             }
             if (r0 + kRound < L.hi) load_round(r0 + kRound, L.hi);
             else if (nxt < npieces) load_piece(LN);
@@ -1818,6 +1884,168 @@ __global__ __launch_bounds__(1024) void k_fine_piece(PieceArgs a) {
         __syncthreads();
         L = LN;
     }
+}
+
+// Round-wise first gather of a staged region's un-partition: one block per fine-pass round. The
+// round's tile runs of binned results (recorded by k_fine_piece) are read whole into LDS in the
+// round's staging order, then every slot of the round takes its value from its staging position
+// (rpos). Each run is read once, contiguously; the per-slot gather of binned positions it
+// replaces read 1.7-1.8x its bytes (a partial line at every run end, runs of ~2-4 records).
+// runs[0..nr) of src (start s_cur[f], length s_len[f], staging base s_base[f], nr <= 128,
+// total tot) copied into LDS in staging order: staging position x lies in the last run starting at
+// or before it (empty runs start where the next one does); every thread takes consecutive
+// positions, U loads in flight (a wave per run left Zipf-hot runs to one wave)
+static_assert(kFine == 128 && kMaxCoarse == 128, "runs_to_lds searches 128 runs");
+template <typename V>
+__device__ __forceinline__ void runs_to_lds(const uint32_t* s_cur, const uint32_t* s_base, uint32_t tot,
+                                            const V* __restrict__ src, const uint8_t* __restrict__ oks, V* s_v,
+                                            uint8_t* s_ok) {
+    constexpr int U = 4;
+    for (uint32_t x0 = threadIdx.x; x0 < tot; x0 += U * 1024) {
+        uint32_t sp[U];
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            const uint32_t x = min(x0 + uint32_t(u) * 1024, tot - 1);
+            uint32_t lo_f = 0, hi_f = 128;
+#pragma unroll
+            for (int it = 0; it < 7; it++) {
+                const uint32_t m = (lo_f + hi_f) >> 1;
+                if (s_base[m] <= x) lo_f = m; else hi_f = m;
+            }
+            sp[u] = s_cur[lo_f] + (x - s_base[lo_f]);
+        }
+        V v[U];
+        uint8_t o[U];
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            v[u] = src[sp[u]];
+            o[u] = oks ? oks[sp[u]] : uint8_t(0);
+        }
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            const uint32_t x = x0 + uint32_t(u) * 1024;
+            if (x < tot) {
+                s_v[x] = v[u];
+                s_ok[x] = o[u];
+            }
+        }
+    }
+}
+
+struct RoundRegion {
+    const uint32_t* rt;         // the region's run tables
+    const uint32_t* ptab;       // pbase[C + 1], bstart[C + 1]
+    const uint32_t* lpos;       // slot -> staging position in its round
+    const uint8_t* src;         // binned results
+    uint8_t* dst;               // results by slot
+    const uint8_t* oks;
+    uint8_t* okd;
+    uint32_t C, rpp, block0;
+};
+struct RoundTable {
+    RoundRegion r[kMaxRegions];
+    uint32_t nr;
+};
+
+template <int VB, int RPT>
+__global__ __launch_bounds__(1024) void k_unpart_rounds(RoundTable t) {
+    using V = typename idx_t<VB>::I;
+    constexpr uint32_t kRound = RPT * 1024;
+    __shared__ V s_v[kRound];
+    __shared__ uint8_t s_ok[kRound];
+    __shared__ uint32_t s_cur[kFine], s_len[kFine], s_base[kFine], s_tot;
+    uint32_t i = 0;
+    while (i + 1 < t.nr && t.r[i + 1].block0 <= blockIdx.x) i++;
+    const RoundRegion& g = t.r[i];
+    const uint32_t b = blockIdx.x - g.block0;
+    const uint32_t pid = b / g.rpp, j = b % g.rpp;
+    const uint32_t* pbase = g.ptab;
+    const uint32_t* bstart = g.ptab + g.C + 1;
+    if (pid >= pbase[g.C]) return;                        // block-uniform
+    const PieceLoc L = piece_loc(pbase, bstart, g.C, pid);
+    const uint32_t lo = L.lo + j * kRound;
+    if (lo >= L.hi) return;
+    const uint32_t hi = min(lo + kRound, L.hi);
+    if (threadIdx.x < kFine) {
+        const uint32_t* rr = g.rt + uint64_t(b) * (2 * kFine) + 2 * threadIdx.x;
+        s_cur[threadIdx.x] = rr[0];
+        s_len[threadIdx.x] = rr[1];
+    }
+    __syncthreads();
+    small_excl_scan(s_len, s_base, kFine, &s_tot);
+    __syncthreads();
+    runs_to_lds(s_cur, s_base, s_tot, reinterpret_cast<const V*>(g.src), g.oks, s_v, s_ok);
+    __syncthreads();
+    V* dst = reinterpret_cast<V*>(g.dst);
+    for (uint32_t k = lo + threadIdx.x; k < hi; k += blockDim.x) {
+        const uint32_t q = g.lpos[k];
+        dst[k] = s_v[q];
+        if (g.oks) g.okd[k] = s_ok[q];
+    }
+}
+
+// Round-wise second gather: one block per (region, producer block, coarse round). The round's
+// bucket runs of temp-slot results are read whole into LDS in the round's staging order, then
+// every record of the round takes its value from its staging position (qpos; ~0 = out of bounds).
+struct CRoundRegion {
+    const uint32_t* crt;        // the region's coarse run tables
+    const uint32_t* qpos;       // record -> staging position in its round
+    const uint8_t* src;         // results by temp slot
+    uint8_t* dst;               // caller's results (arrival order)
+    const uint8_t* oks;
+    uint8_t* okd;
+    uint64_t n, chunk;
+    uint32_t rpb, block0;
+};
+struct CRoundTable {
+    CRoundRegion r[kMaxRegions];
+    uint32_t nr;
+};
+
+template <int VB, int RPT>
+__global__ __launch_bounds__(1024) void k_unpart_crounds(CRoundTable t) {
+    using V = typename idx_t<VB>::I;
+    constexpr uint32_t kRound = RPT * 1024;
+    __shared__ V s_v[kRound];
+    __shared__ uint8_t s_ok[kRound];
+    __shared__ uint32_t s_cur[kMaxCoarse], s_len[kMaxCoarse], s_base[kMaxCoarse], s_tot;
+    uint32_t i = 0;
+    while (i + 1 < t.nr && t.r[i + 1].block0 <= blockIdx.x) i++;
+    const CRoundRegion& g = t.r[i];
+    const uint32_t b = blockIdx.x - g.block0;
+    const uint64_t lo = uint64_t(b / g.rpb) * g.chunk + uint64_t(b % g.rpb) * kRound;
+    const uint64_t hi = min(min(uint64_t(b / g.rpb) * g.chunk + g.chunk, g.n), lo + kRound);
+    if (lo >= hi) return;                                 // block-uniform
+    if (threadIdx.x < kMaxCoarse) {
+        const uint32_t* rr = g.crt + uint64_t(b) * (2 * kMaxCoarse) + 2 * threadIdx.x;
+        s_cur[threadIdx.x] = rr[0];
+        s_len[threadIdx.x] = rr[1];
+    }
+    __syncthreads();
+    small_excl_scan(s_len, s_base, kMaxCoarse, &s_tot);
+    __syncthreads();
+    runs_to_lds(s_cur, s_base, s_tot, reinterpret_cast<const V*>(g.src), g.oks, s_v, s_ok);
+    __syncthreads();
+    V* dst = reinterpret_cast<V*>(g.dst);
+    for (uint64_t k = lo + threadIdx.x; k < hi; k += blockDim.x) {
+        const uint32_t q = g.qpos[k];
+        if (q == 0xFFFFFFFFu) continue;
+        dst[k] = s_v[q];
+        if (g.okd) g.okd[k] = s_ok[q];
+    }
+}
+
+// work plan when no tile splits (mixed sessions, ops that do not combine): an owner item per
+// touched tile, one thread per tile over the whole grid (the one-block plan below took 14 us
+// for C5's 4096 tiles x 5 regions)
+__global__ void k_stage_plan_owner(const uint32_t* rts, uint32_t nreg, uint32_t stride, uint32_t num_tiles,
+                                   TileItem* items, uint32_t* delta_count) {
+    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t == 0) *delta_count = 0;
+    if (t >= num_tiles) return;
+    uint32_t all = 0;
+    for (uint32_t r = 0; r < nreg; r++) all += rts[uint64_t(r) * stride + t + 1] - rts[uint64_t(r) * stride + t];
+    items[t] = TileItem{t, 0u, 0u, all ? 0u : 2u};
 }
 
 // work plan over all regions, one block: owner item per touched tile; a hot tile of a
@@ -1941,6 +2169,14 @@ hipError_t launch_stage_region(int dtype, int index_size, const ApplyArgs& a, co
     q.trows = w.counts;                             // G * csub rows of T counts (<= kMaxBinBlocks x kMaxTiles)
     q.ttot = w.tile_items;
     q.tfill = w.ff + 64 + size_t(kMaxCoarse) * kSegs;
+    // coarse run tables for the round-wise second un-partition gather
+    uint32_t kcround = 0;
+    dispatch_vb_rpt<4>(vb, coarse_rpt(vb), [&](auto, auto rpt) { kcround = uint32_t(decltype(rpt)::value) * 1024; });
+    const uint32_t rpb = uint32_t((q.chunk + kcround - 1) / kcround);
+    const uint64_t ncr = G * rpb;
+    const bool crounds = has_res && (unpart_rounds() & (vb == 8 ? 4 : 2)) && s.crounds + ncr <= w.crt_rounds;
+    q.crt = crounds ? w.crtab + s.crounds * (2 * kMaxCoarse) : nullptr;
+    q.rpb = rpb;
     hipError_t e;
     {
         ProfScope ps(a.prof, LMR_STAGE_BIN_COUNT, st, a.n);
@@ -1970,6 +2206,15 @@ hipError_t launch_stage_region(int dtype, int index_size, const ApplyArgs& a, co
     pa.rpos = has_res ? w.rpos + R : nullptr; pa.R = R;
     pa.ts = w.rts + uint64_t(r) * (kMaxTiles + 1); pa.ttot = q.ttot; pa.tfill = q.tfill;
     const uint64_t max_pieces = (a.n + kPiece - 1) / kPiece + C;
+    // run tables for the round-wise un-partition: rpp rounds per piece, max_pieces * rpp per region
+    uint32_t kround = 0;
+    dispatch_vb_rpt<2>(vb, piece_fine_rpt(vb), [&](auto, auto rpt) { kround = uint32_t(decltype(rpt)::value) * 1024; });
+    const uint32_t rpp = (kPiece + kround - 1) / kround;
+    const uint64_t nrounds = max_pieces * rpp;
+    const bool rounds = has_res && (unpart_rounds() & 1) && s.rounds + nrounds <= w.rt_rounds;
+    pa.rt = rounds ? w.runtab + s.rounds * (2 * kFine) : nullptr;
+    pa.ptab = w.ptab + size_t(r) * 2 * (kMaxCoarse + 1);
+    pa.rpp = rpp;
     {
         ProfScope ps(a.prof, LMR_STAGE_FINE_SCATTER, st, a.n);
         const unsigned fgrid = unsigned(std::min<uint64_t>(max_pieces, uint64_t(fine_blocks_cap())));
@@ -1980,7 +2225,11 @@ hipError_t launch_stage_region(int dtype, int index_size, const ApplyArgs& a, co
         e = hipGetLastError();
     }
     if (e != hipSuccess) return e;
-    s.reg[r] = StageRegion{uint64_t(R), a.n, a.results, a.ok, a.op, a.ret, a.cmp_bits, a.eps_bits};
+    s.reg[r] = StageRegion{uint64_t(R), a.n, a.results, a.ok, a.op, a.ret, a.cmp_bits, a.eps_bits,
+                           uint32_t(s.rounds), kround, rounds ? uint32_t(nrounds) : 0u,
+                           uint32_t(s.crounds), crounds ? uint32_t(ncr) : 0u, rpb, kcround, q.chunk};
+    if (rounds) s.rounds += nrounds;
+    if (crounds) s.crounds += ncr;
     s.nreg = r + 1;
     s.staged += a.n;
     return hipSuccess;
@@ -2012,8 +2261,12 @@ hipError_t launch_stage_finish(const TiledWs& w, StageSession& s, hipStream_t st
         const uint64_t avg = (s.staged + T - 1) / T;
         const uint32_t thresh = uint32_t(std::min<uint64_t>(0xFFFFFFFFull, std::max<uint64_t>(delta_mul() * avg, delta_min())));
         TileItem* items = reinterpret_cast<TileItem*>(w.items);
-        hipLaunchKernelGGL(k_stage_plan, dim3(1), dim3(1024), 0, st, w.rts, uint32_t(s.nreg), stride, T, thresh,
-                           (!mixed && op_combines(a.op)) ? 1 : 0, items, items + kMaxTiles, w.item_count);
+        if (!mixed && op_combines(a.op))
+            hipLaunchKernelGGL(k_stage_plan, dim3(1), dim3(1024), 0, st, w.rts, uint32_t(s.nreg), stride, T, thresh,
+                               1, items, items + kMaxTiles, w.item_count);
+        else
+            hipLaunchKernelGGL(k_stage_plan_owner, dim3((T + 255) / 256), dim3(256), 0, st, w.rts, uint32_t(s.nreg),
+                               stride, T, items, w.item_count);
         TileArgs t;
         t.shard = a.shard; t.shard_len = a.shard_len; t.tile_shift = shift;
         t.kind = a.kind; t.op = a.op; t.ret = a.ret;
@@ -2042,25 +2295,62 @@ hipError_t launch_stage_finish(const TiledWs& w, StageSession& s, hipStream_t st
         uint8_t* tmpres = w.bin_val;                              // bins are free after the tile sweep
         uint8_t* ok_tmp_all = (a.ret == LMR_RET_RESULT) ? reinterpret_cast<uint8_t*>(w.bin_lidx) : nullptr;
         const uint8_t* ok_src_all = (a.ret == LMR_RET_RESULT) ? ok_bin : nullptr;
-        // every returning region's first gather in one launch, then every second gather
+        // every returning region's first gather in one launch (round-wise for the regions with run
+        // tables, per slot for the rest), then every second gather
         UnpartTable t1{}, t2{};
+        RoundTable tr{};
+        CRoundTable tc{};
+        uint32_t rblocks = 0, kround = 0, cblocks = 0, kcround = 0;
         for (int r = 0; r < s.nreg; r++) {
             const StageRegion& g = s.reg[r];
             if (!g.results || g.ret == LMR_RET_NONE) continue;
             uint8_t* ok_tmp = g.ret == LMR_RET_RESULT ? ok_tmp_all : nullptr;
             const uint8_t* ok_src = g.ret == LMR_RET_RESULT ? ok_src_all : nullptr;
             const bool want_ok = ok_tmp && g.ok;
-            t1.r[t1.nr++] = UnpartRegion{w.rpos + g.base, w.sinfo + kStageInb + r, g.n, 0, res_bin,
-                                         tmpres + g.base * vb, ok_src, ok_tmp ? ok_tmp + g.base : nullptr, 0};
-            t2.r[t2.nr++] = UnpartRegion{w.qpos + g.base, nullptr, g.n, 0, tmpres + g.base * vb,
-                                         reinterpret_cast<uint8_t*>(g.results), want_ok ? ok_tmp + g.base : nullptr,
-                                         want_ok ? g.ok : nullptr, 0};
+            if (g.nrounds) {
+                const uint32_t C = (T + kFine - 1) / kFine;
+                tr.r[tr.nr++] = RoundRegion{w.runtab + uint64_t(g.round_base) * (2 * kFine),
+                                            w.ptab + size_t(r) * 2 * (kMaxCoarse + 1), w.rpos + g.base, res_bin,
+                                            tmpres + g.base * vb, ok_src, ok_tmp ? ok_tmp + g.base : nullptr, C,
+                                            (kPiece + g.kround - 1) / g.kround, rblocks};
+                rblocks += g.nrounds;
+                kround = g.kround;
+            } else
+                t1.r[t1.nr++] = UnpartRegion{w.rpos + g.base, w.sinfo + kStageInb + r, g.n, 0, res_bin,
+                                             tmpres + g.base * vb, ok_src, ok_tmp ? ok_tmp + g.base : nullptr, 0};
+            if (g.ncrounds) {
+                tc.r[tc.nr++] = CRoundRegion{w.crtab + uint64_t(g.cround_base) * (2 * kMaxCoarse), w.qpos + g.base,
+                                             tmpres + g.base * vb, reinterpret_cast<uint8_t*>(g.results),
+                                             want_ok ? ok_tmp + g.base : nullptr, want_ok ? g.ok : nullptr, g.n,
+                                             g.chunk, g.rpb, cblocks};
+                cblocks += g.ncrounds;
+                kcround = g.kcround;
+            } else
+                t2.r[t2.nr++] = UnpartRegion{w.qpos + g.base, nullptr, g.n, 0, tmpres + g.base * vb,
+                                             reinterpret_cast<uint8_t*>(g.results), want_ok ? ok_tmp + g.base : nullptr,
+                                             want_ok ? g.ok : nullptr, 0};
         }
-        e = launch_unpartition_multi(vb, t1, st);
-        if (e == hipSuccess) e = launch_unpartition_multi(vb, t2, st);
+        if (tr.nr) {
+            dispatch_vb_rpt<2>(vb, int(kround / 1024), [&](auto vbt, auto rpt) {
+                constexpr int VBc = decltype(vbt)::value, RP = decltype(rpt)::value;
+                hipLaunchKernelGGL((k_unpart_rounds<VBc, RP>), dim3(rblocks), dim3(1024), 0, st, tr);
+            });
+            e = hipGetLastError();
+        }
+        if (e == hipSuccess && t1.nr) e = launch_unpartition_multi(vb, t1, st);
+        if (e == hipSuccess && tc.nr) {
+            dispatch_vb_rpt<4>(vb, int(kcround / 1024), [&](auto vbt, auto rpt) {
+                constexpr int VBc = decltype(vbt)::value, RP = decltype(rpt)::value;
+                hipLaunchKernelGGL((k_unpart_crounds<VBc, RP>), dim3(cblocks), dim3(1024), 0, st, tc);
+            });
+            e = hipGetLastError();
+        }
+        if (e == hipSuccess && t2.nr) e = launch_unpartition_multi(vb, t2, st);
     }
     s.nreg = 0;
     s.staged = 0;
+    s.rounds = 0;
+    s.crounds = 0;
     return e;
 }
 

@@ -81,6 +81,11 @@ struct TiledWs {
     uint32_t* rts;         // staged apply: [kMaxRegions][kMaxTiles + 1] tile starts of each region
     uint32_t* sinfo;       // staged apply: piece table (pbase, bstart) + per-region in-bounds totals
     uint32_t* ff;          // count-free partition: bucket and tile fill counters
+    uint32_t* runtab;      // staged apply: per fine round, per tile (binned run start, length)
+    uint32_t* ptab;        // staged apply: [kMaxRegions][2 * (kMaxCoarse + 1)] piece tables
+    uint64_t rt_rounds;    // rounds runtab holds
+    uint32_t* crtab;       // staged apply: per coarse round, per bucket (temp run start, length)
+    uint64_t crt_rounds;   // rounds crtab holds
     uint64_t cap;          // records of one tiled piece (bin arrays, position maps)
     uint64_t tmp_cap;      // records the temp arrays (tmp_idx / tmp_val) hold, > cap
 };
@@ -156,12 +161,22 @@ struct StageRegion {
     int ret;             // regions with equal op / operands, applied in staging order)
     uint64_t cmp_bits;
     uint64_t eps_bits;
+    uint32_t round_base = 0;   // first runtab round of the region (returning regions)
+    uint32_t kround = 0;       // the fine pass's LDS round (records)
+    uint32_t nrounds = 0;      // runtab rounds reserved for the region (0: no run table)
+    uint32_t cround_base = 0;  // first crtab round of the region
+    uint32_t ncrounds = 0;     // crtab rounds reserved (producer blocks x rounds per block; 0: none)
+    uint32_t rpb = 0;          // coarse rounds per producer block
+    uint32_t kcround = 0;      // the coarse pass's LDS round (records)
+    uint64_t chunk = 0;        // records per producer block
 };
 struct StageSession {
     ApplyArgs a;         // op / kind / shard / ret of the session's current op (record fields unused)
     int dtype = 0;
     int nreg = 0;
     uint64_t staged = 0; // workspace slots in use
+    uint64_t rounds = 0; // runtab rounds in use
+    uint64_t crounds = 0;  // crtab rounds in use
     bool free = false;   // count-free regions (stage_free_applies): shared bucket regions, one fine pass
     bool free_armed = false;
     bool switched = false;  // the op changed with records staged (lmr_stage_op): later phases counted
