@@ -1647,7 +1647,8 @@ static_assert(kStageInb + kMaxRegions <= kStageInfoWords, "staged scratch");
 // (16 lane-picked copies of the histogram, to spread the LDS atomics' address conflicts,
 // measured 0.35 -> 0.36 ms per C5 step: the pass is not bound by them)
 // Measured and dropped: per-thread private LDS counters instead of the shared histogram's
-// atomics (C5 count 0.33 -> 0.38 ms: 128 KB of LDS per block, zeroing and folding).
+// atomics (C5 count 0.33 -> 0.38 ms: 128 KB of LDS per block, zeroing and folding); the bucket
+// counts summed from the tile counts after the loop, one LDS atomic per record (0.371 -> 0.383 ms).
 // Every block also counts its records per tile (LDS atomics over T bins, few conflicts) into
 // its row of p.trows: k_coarse_scatter folds the rows into tile totals, k_fine_piece turns
 // them into tile starts and reserves each round's tile runs inside them.
@@ -1655,8 +1656,6 @@ template <int IW>
 __global__ __launch_bounds__(1024) void k_ccount(PartArgs p) {
     // loads in flight per thread (4: C5 count 0.347 -> 0.337 ms at 8; 16: 0.380 -> 0.398 ms)
     constexpr int U = 8;
-    // the bucket counts derived from the tile counts after the loop (one LDS atomic per record)
-    constexpr bool kDerive = true;
     __shared__ uint32_t hist[kMaxCoarse];
     extern __shared__ uint32_t thist[];   // [num_tiles]
     for (uint32_t c = threadIdx.x; c < p.C; c += blockDim.x) hist[c] = 0;
@@ -1684,24 +1683,12 @@ __global__ __launch_bounds__(1024) void k_ccount(PartArgs p) {
             const uint64_t k = k0 + uint64_t(j) * blockDim.x;
             if (k >= hi) continue;
             if (ix[j] >= p.shard_len) { oob = true; continue; }
-            if (!kDerive) atomicAdd(&hist[uint32_t(ix[j] >> cshift)], 1u);
+            atomicAdd(&hist[uint32_t(ix[j] >> cshift)], 1u);
             atomicAdd(&thist[uint32_t(ix[j] >> p.tile_shift)], 1u);
         }
     }
     if (oob) raise_err(p.err, LMR_ERRBIT_OOB);
     __syncthreads();
-    if (kDerive) {
-        // bucket c's count = its 128 tiles' counts: wave w sums buckets w, w + 16, ...
-        const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-        for (uint32_t c = wv; c < p.C; c += blockDim.x >> 6) {
-            const uint32_t t0 = c * kFine + 2 * lane;
-            uint32_t x = (t0 < p.num_tiles ? thist[t0] : 0u) + (t0 + 1 < p.num_tiles ? thist[t0 + 1] : 0u);
-#pragma unroll
-            for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o, 64);
-            if (lane == 0) hist[c] = x;
-        }
-        __syncthreads();
-    }
     for (uint32_t c = threadIdx.x; c < p.C; c += blockDim.x)
         p.coarse_off[uint64_t(c) * p.G * S + blockIdx.x] = hist[c];
     uint32_t* row = p.trows + uint64_t(blockIdx.x) * p.num_tiles;

@@ -23,7 +23,8 @@ STAGES = {
     "fine_scatter": (("k_fine_free", "k_fine_scatter", "k_fine_piece"),
                      ("k_fine_free", "k_fine_scatter", "k_fine_piece", "k_piece_count", "k_free_tile_totals")),
     "tile_apply": (("k_tile_owner",), ("k_tile_owner", "k_tile_delta", "k_tile_plan", "k_stage_plan")),
-    "unpartition": (("k_tile_owner",), ("k_unpartition", "k_unpartition_multi")),
+    "unpartition": (("k_tile_owner",), ("k_unpartition", "k_unpartition_multi", "k_unpart_rounds",
+                                        "k_unpart_crounds")),
     "direct": (("k_apply_direct",), ("k_apply_direct",)),
     "pack": (("k_pack_count", "k_pack_stage"), ("k_pack_count", "k_pack_scatter", "k_pack_stage", "k_dest_offsets",
                                                  "k_fill_counts")),
