@@ -75,6 +75,7 @@ class lmr_transport_t(Structure):
 
 
 XHDR_WORDS = 5     # LMR_XHDR_WORDS
+XHDR_SCALAR, XHDR_ORDERED = 1, 2   # LMR_XHDR_SCALAR, LMR_XHDR_ORDERED (flags word of a header row)
 
 
 # ---- AM wire format (include/lamellar_gpu_ops.h, "AM wire format")

@@ -309,6 +309,7 @@ lmr_status_t lmr_ctx_create(int device, lmr_ctx_t** out) {
     c->d_err = reinterpret_cast<uint32_t*>(p);
     // the error word and the pack scan's look-back scratch start zeroed
     if (hipMemset(p, 0, pack_scratch_bytes()) != hipSuccess) { (void)hipFree(p); delete c; return LMR_E_HIP; }
+    if (ord_reserve(c, kOrderedMinPiece) != hipSuccess) { lmr_ctx_destroy(c); return LMR_E_HIP; }
     *out = c;
     return LMR_OK;
 }
@@ -339,6 +340,7 @@ lmr_status_t lmr_ctx_reserve(lmr_ctx_t* ctx, uint64_t max_records) {
     (void)hipSetDevice(ctx->device);
     if (ctx->ws) { (void)hipFree(ctx->ws); ctx->ws = nullptr; ctx->ws_bytes = 0; ctx->rec_cap = 0; }
     if (max_records == 0) return LMR_OK;
+    if (ord_reserve(ctx, max_records) != hipSuccess) return LMR_E_HIP;
     size_t b = tiled_ws_bytes(max_records);
     void* p = nullptr;
     if (hipMalloc(&p, b) != hipSuccess) return LMR_E_HIP;

@@ -10,10 +10,12 @@
 // exec_am (registered_active_message.rs:443-497), and fetch results come back as
 // AM data (:307-359) into the handle's reorder (operations/handle.rs:315-317).
 // Here, per chunk of the batch:
-//   pack stream : lmr_pack_unordered -> header all-to-all (per PE: count, MVSI local
-//                 index, scalar flag + bits, chunk count) -> [host waits for the
-//                 headers: RCCL's all-to-all-v takes host counts] -> all-to-all-v of
-//                 local indices and values
+//   pack stream : pack by owner PE (count-free regions / lmr_pack_unordered; the stable
+//                 lmr_pack for a batch that is one reference AM per destination) and the
+//                 chunk's header rows (count, MVSI local index, flags, scalar bits, chunk
+//                 count); chunk j+1's pack runs while the host waits for chunk j's headers
+//   exchange    : header all-to-all -> [host reads the rows: RCCL's all-to-all-v takes
+//                 host counts] -> all-to-all-v of local indices and values
 //   apply stream: waits for the chunk's exchange, stages every source's records
 //                 (lmr_stage_soa; MVSI sources lmr_apply_mvsi) -> after the last
 //                 chunk one shard sweep (lmr_stage_finish) -> reverse all-to-all-v of
@@ -33,16 +35,19 @@
 
 namespace lmr {
 
+hipError_t xstate_drain(const XState* x);
+
 namespace {
 
 struct DevBuf {
     void* p = nullptr;
     size_t cap = 0;
-    // grow-only: a larger request waits for the device (the old buffer may be in use)
-    hipError_t need(size_t bytes) {
+    // grow-only: a larger request first waits for the exchange's internal streams (the old
+    // buffer may be in use there; the library uses these buffers on no other stream)
+    hipError_t need(size_t bytes, const lmr::XState* owner) {
         if (bytes <= cap) return hipSuccess;
         if (p) {
-            hipError_t e = hipDeviceSynchronize();
+            hipError_t e = xstate_drain(owner);
             if (e != hipSuccess) return e;
             (void)hipFree(p);
             p = nullptr;
@@ -79,40 +84,50 @@ struct HostBuf {
 }  // namespace
 
 // Exchange state of a context: internal streams, events, grow-only buffers.
-// Streams: sp packs, sx runs every forward collective, sa stages and applies. Send and
-// receive buffers are double-buffered, so chunk j+1's pack overlaps chunk j's all-to-all-v
-// and chunk j-1's staging.
+// Streams: sp packs, sx runs every forward collective, sa stages and applies. Send buffers,
+// header rows and receive buffers are double-buffered by chunk parity, so chunk j+1's pack
+// runs while the host waits for chunk j's header rows, and chunk j+1's all-to-all-v
+// overlaps chunk j's staging.
 struct XState {
     hipStream_t sp = nullptr, sx = nullptr, sa = nullptr;
-    hipEvent_t ev_begin = nullptr, ev_hdr = nullptr, ev_x = nullptr, ev_pack_done = nullptr, ev_apply_done = nullptr,
-               ev_x_done = nullptr;
+    hipEvent_t ev_begin = nullptr, ev_pack_done = nullptr, ev_apply_done = nullptr, ev_x_done = nullptr;
+    hipEvent_t ev_hdr[2] = {nullptr, nullptr}, ev_x[2] = {nullptr, nullptr};
     hipEvent_t ev_recv_free[2] = {nullptr, nullptr}, ev_send_free[2] = {nullptr, nullptr},
                ev_packed[2] = {nullptr, nullptr};
     bool recv_used[2] = {false, false}, send_used[2] = {false, false};
-    DevBuf hdr_recv, counts, offsets, one_idx, fill;
-    DevBuf hdr_send[2], send_idx[2], send_vals[2];
+    DevBuf counts, offsets, one_idx, fill;
+    DevBuf hdr_send[2], hdr_recv[2], send_idx[2], send_vals[2];
     DevBuf recv_idx[2], recv_vals[2];
     std::vector<DevBuf> pos, res, rok;   // per chunk (returning ops)
     DevBuf back, back_ok;
-    HostBuf h_hdr;                       // [send rows | recv rows] int64
+    HostBuf h_hdr;                       // per chunk parity: [send rows | recv rows] int64
     HostBuf h_send, h_recv;              // host-buffer transports
+    // waits for the three internal streams (not the whole device: other work may share it)
+    hipError_t drain() const {
+        hipError_t e = hipSuccess, r;
+        for (hipStream_t s : {sp, sx, sa})
+            if (s && (r = hipStreamSynchronize(s)) != hipSuccess && e == hipSuccess) e = r;
+        return e;
+    }
 };
+
+hipError_t xstate_drain(const XState* x) { return x->drain(); }
 
 void xstate_free(XState* x) {
     if (!x) return;
-    (void)hipDeviceSynchronize();
-    for (DevBuf* b : {&x->hdr_send[0], &x->hdr_send[1], &x->hdr_recv, &x->counts, &x->offsets, &x->one_idx, &x->fill,
-                      &x->send_idx[0], &x->send_idx[1], &x->send_vals[0], &x->send_vals[1], &x->recv_idx[0],
-                      &x->recv_idx[1], &x->recv_vals[0], &x->recv_vals[1], &x->back, &x->back_ok})
+    (void)x->drain();
+    for (DevBuf* b : {&x->hdr_send[0], &x->hdr_send[1], &x->hdr_recv[0], &x->hdr_recv[1], &x->counts, &x->offsets,
+                      &x->one_idx, &x->fill, &x->send_idx[0], &x->send_idx[1], &x->send_vals[0], &x->send_vals[1],
+                      &x->recv_idx[0], &x->recv_idx[1], &x->recv_vals[0], &x->recv_vals[1], &x->back, &x->back_ok})
         b->release();
     for (auto* v : {&x->pos, &x->res, &x->rok})
         for (DevBuf& b : *v) b.release();
     x->h_hdr.release();
     x->h_send.release();
     x->h_recv.release();
-    for (hipEvent_t e : {x->ev_begin, x->ev_hdr, x->ev_x, x->ev_pack_done, x->ev_apply_done, x->ev_x_done,
-                         x->ev_recv_free[0], x->ev_recv_free[1], x->ev_send_free[0], x->ev_send_free[1],
-                         x->ev_packed[0], x->ev_packed[1]})
+    for (hipEvent_t e : {x->ev_begin, x->ev_pack_done, x->ev_apply_done, x->ev_x_done, x->ev_hdr[0], x->ev_hdr[1],
+                         x->ev_x[0], x->ev_x[1], x->ev_recv_free[0], x->ev_recv_free[1], x->ev_send_free[0],
+                         x->ev_send_free[1], x->ev_packed[0], x->ev_packed[1]})
         if (e) (void)hipEventDestroy(e);
     if (x->sp) (void)hipStreamDestroy(x->sp);
     if (x->sx) (void)hipStreamDestroy(x->sx);
@@ -125,23 +140,24 @@ static hipError_t xstate_init(XState* x) {
     hipError_t e = hipStreamCreateWithFlags(&x->sp, hipStreamNonBlocking);
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&x->sx, hipStreamNonBlocking);
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&x->sa, hipStreamNonBlocking);
-    for (hipEvent_t* ev : {&x->ev_begin, &x->ev_hdr, &x->ev_x, &x->ev_pack_done, &x->ev_apply_done, &x->ev_x_done,
-                           &x->ev_recv_free[0], &x->ev_recv_free[1], &x->ev_send_free[0], &x->ev_send_free[1],
-                           &x->ev_packed[0], &x->ev_packed[1]})
+    for (hipEvent_t* ev : {&x->ev_begin, &x->ev_pack_done, &x->ev_apply_done, &x->ev_x_done, &x->ev_hdr[0],
+                           &x->ev_hdr[1], &x->ev_x[0], &x->ev_x[1], &x->ev_recv_free[0], &x->ev_recv_free[1],
+                           &x->ev_send_free[0], &x->ev_send_free[1], &x->ev_packed[0], &x->ev_packed[1]})
         if (e == hipSuccess) e = hipEventCreateWithFlags(ev, hipEventDisableTiming);
     return e;
 }
 
-// per-PE header rows of one chunk: [count, MVSI local index or -1, scalar flag, scalar bits, chunk count]
+// per-PE header rows of one chunk: [count, MVSI local index or -1, flags (LMR_XHDR_SCALAR |
+// LMR_XHDR_ORDERED), scalar bits, chunk count]
 __global__ void k_xhdr(const uint64_t* counts, uint32_t npes, int64_t mvsi_pe, int64_t mvsi_off, int64_t mvsi_n,
-                       int64_t scalar, uint64_t sbits, int64_t my_k, int64_t* hdr) {
+                       int64_t flags, uint64_t sbits, int64_t my_k, int64_t* hdr) {
     const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
     if (p >= npes) return;
     int64_t* r = hdr + uint64_t(p) * LMR_XHDR_WORDS;
     const bool mv = mvsi_pe >= 0 && int64_t(p) == mvsi_pe;
     r[0] = mvsi_pe >= 0 ? (mv ? mvsi_n : 0) : (counts ? int64_t(counts[p]) : 0);
     r[1] = mv ? mvsi_off : -1;
-    r[2] = scalar;
+    r[2] = flags;
     r[3] = int64_t(sbits);
     r[4] = my_k;
 }
@@ -236,8 +252,10 @@ const RcclApi& rccl() {
         api.send = reinterpret_cast<decltype(api.send)>(dlsym(h, "ncclSend"));
         api.recv = reinterpret_cast<decltype(api.recv)>(dlsym(h, "ncclRecv"));
         api.comm_abort = reinterpret_cast<decltype(api.comm_abort)>(dlsym(h, "ncclCommAbort"));
+        // ncclCommAbort is required: after a failed call it is the only way to end queued peer
+        // send / recv kernels, so an RCCL without it is not used (the caller gets LMR_E_UNSUPPORTED)
         api.ok = api.get_unique_id && api.comm_init_rank && api.comm_destroy && api.group_start &&
-                 api.group_end && api.send && api.recv;
+                 api.group_end && api.send && api.recv && api.comm_abort;
     });
     return api;
 }
@@ -303,7 +321,7 @@ lmr_status_t rccl_alltoallv(void* self, const void* send, const uint64_t* sb, co
 void transport_abort(const lmr_transport_t* tp) {
     if (!tp || tp->alltoall != rccl_alltoall) return;
     RcclTransport* t = static_cast<RcclTransport*>(tp->self);
-    if (t->comm && rccl().comm_abort) rccl().comm_abort(t->comm);
+    if (t->comm) rccl().comm_abort(t->comm);
     t->comm = nullptr;
 }
 
@@ -351,8 +369,8 @@ uint64_t lmr_exchange_plan(uint32_t npes, uint32_t iw, uint32_t eb, const int64_
         const uint64_t sc = uint64_t(s[0] > 0 ? s[0] : 0), rc = uint64_t(r[0] > 0 ? r[0] : 0);
         idx_sb[p] = s[1] < 0 ? sc * iw : 0;            // MVSI senders name their index in the header
         idx_rb[p] = r[1] < 0 ? rc * iw : 0;
-        val_sb[p] = s[2] ? 0 : sc * eb;                // one scalar value travels in the header
-        val_rb[p] = r[2] ? 0 : rc * eb;
+        val_sb[p] = (s[2] & LMR_XHDR_SCALAR) ? 0 : sc * eb;   // one scalar value travels in the header
+        val_rb[p] = (r[2] & LMR_XHDR_SCALAR) ? 0 : rc * eb;
         idx_so[p] = a; a += idx_sb[p];
         idx_ro[p] = b; b += idx_rb[p];
         val_so[p] = c; c += val_sb[p];
@@ -413,7 +431,8 @@ lmr_status_t lmr_batch_exchange(lmr_ctx_t* ctx, const lmr_transport_t* tp, const
     if (!ctx || !tp || !valid_layout(layout) || !desc || tp->num_pes != layout->num_pes ||
         tp->my_pe != layout->my_pe || layout->num_pes > uint32_t(kMaxPackPes))
         return LMR_E_INVALID;
-    if (desc->dtype >= LMR_NUM_DTYPES || desc->op >= LMR_NUM_OPS) return LMR_E_INVALID;
+    if (desc->dtype >= LMR_NUM_DTYPES || desc->op >= LMR_NUM_OPS || desc->strategy > LMR_STRATEGY_ORDERED)
+        return LMR_E_INVALID;
     if (!lmr_op_supported(desc->kind, desc->dtype, desc->op)) return LMR_E_UNSUPPORTED;
     if (i_len > 1 && v_len > 1 && i_len != v_len) return LMR_E_LENGTH;
     if ((i_len > 1 && !d_gidx) || (v_len > 1 && !d_vals) || (v_len == 1 && !h_val)) return LMR_E_INVALID;
@@ -430,6 +449,17 @@ lmr_status_t lmr_batch_exchange(lmr_ctx_t* ctx, const lmr_transport_t* tp, const
     const bool scalar = v_len == 1 && !mvsi;
     uint64_t sbits = 0;
     if (scalar) memcpy(&sbits, h_val, eb);
+    // A batch that is one reference AM per destination keeps its input order per owner: in the
+    // reference a batch below 1000 records is one OpInput chunk (src/array/operations.rs:462-469),
+    // so its pack appends each destination's records in input order into one buffer
+    // (unsafe/operations.rs:709-758) and the owner's AM applies them sequentially
+    // (impl/src/array_ops.rs:203-250; own records through the local shortcut,
+    // registered_active_message.rs:150-154). Such a sender packs stably and flags its header
+    // rows; the owner applies each flagged source's stream in order (LMR_STRATEGY_ORDERED).
+    // LMR_STRATEGY_ORDERED asks for the same at any size.
+    const bool ordered = !mvsi && n > 0 &&
+                         (desc->strategy == LMR_STRATEGY_ORDERED ||
+                          (desc->strategy == LMR_STRATEGY_AUTO && n < kOrderedAuto));
     (void)hipSetDevice(ctx->device);
     if (!ctx->xch) ctx->xch = new XState();
     XState* x = ctx->xch;
@@ -445,23 +475,24 @@ lmr_status_t lmr_batch_exchange(lmr_ctx_t* ctx, const lmr_transport_t* tp, const
         mvsi_pe = int64_t(pe);
         mvsi_off = int64_t(off);
     } else if (n > 0 && i_len == 1) {                  // one index (1 x 1): a one-record batch
-        if (x->one_idx.need(8) != hipSuccess) return LMR_E_HIP;
+        if (x->one_idx.need(8, x) != hipSuccess) return LMR_E_HIP;
         if (hipMemcpyAsync(x->one_idx.p, &h_index, 8, hipMemcpyHostToDevice, s0) != hipSuccess) return LMR_E_HIP;
         gidx = x->one_idx.as<uint64_t>();
     }
     const uint64_t chunk = exchange_chunk();
     const uint64_t my_k = mvsi ? 1 : std::max<uint64_t>(1, (m + chunk - 1) / chunk);
     // --- buffers that do not depend on the chunk
-    if (x->hdr_send[0].need(size_t(npes) * LMR_XHDR_WORDS * 8) != hipSuccess ||
-        x->hdr_send[1].need(size_t(npes) * LMR_XHDR_WORDS * 8) != hipSuccess ||
-        x->hdr_recv.need(size_t(npes) * LMR_XHDR_WORDS * 8) != hipSuccess ||
-        x->counts.need(size_t(npes) * 8) != hipSuccess || x->offsets.need(size_t(npes + 1) * 8) != hipSuccess ||
-        x->h_hdr.need(size_t(2 * npes) * LMR_XHDR_WORDS * 8) != hipSuccess)
+    const size_t rows = size_t(npes) * LMR_XHDR_WORDS;
+    for (int b = 0; b < 2; b++)
+        if (x->hdr_send[b].need(rows * 8, x) != hipSuccess || x->hdr_recv[b].need(rows * 8, x) != hipSuccess)
+            return LMR_E_HIP;
+    if (x->counts.need(size_t(npes) * 8, x) != hipSuccess || x->offsets.need(size_t(npes + 1) * 8, x) != hipSuccess ||
+        x->h_hdr.need(4 * rows * 8) != hipSuccess)
         return LMR_E_HIP;
     const uint64_t cmax = std::min<uint64_t>(m, chunk);
     // nothing returned: the count-free pack (fixed per-PE regions, no count pass); a chunk
     // whose records overflow a region is packed again with the counted pack
-    const bool free_pack = !returning && npes <= 512 && free_pack_enabled();
+    const bool free_pack = !returning && !ordered && npes <= 512 && free_pack_enabled();
     const uint32_t me = layout->my_pe;
     const bool bypass = npes > 1 && self_bypass_enabled();
     auto region_cap = [&](uint64_t c) -> uint64_t {
@@ -469,11 +500,13 @@ lmr_status_t lmr_batch_exchange(lmr_ctx_t* ctx, const lmr_transport_t* tp, const
         return q + q / 8 + 4096;
     };
     const uint64_t send_recs = free_pack ? std::max<uint64_t>(cmax, uint64_t(npes) * region_cap(cmax)) : cmax;
-    if (free_pack && (send_recs > 0xFFFFFFFFull || x->fill.need(size_t(npes) * 4 + 8) != hipSuccess)) return LMR_E_HIP;
+    if (free_pack && (send_recs > 0xFFFFFFFFull || x->fill.need(size_t(npes) * 4 + 8, x) != hipSuccess))
+        return LMR_E_HIP;
     for (int b = 0; b < 2; b++)
-        if (x->send_idx[b].need(send_recs * iw + 8) != hipSuccess || x->send_vals[b].need(send_recs * eb + 8) != hipSuccess)
+        if (x->send_idx[b].need(send_recs * iw + 8, x) != hipSuccess ||
+            x->send_vals[b].need(send_recs * eb + 8, x) != hipSuccess)
             return LMR_E_HIP;
-    // --- both internal streams start after everything already on the caller's stream
+    // --- the internal streams start after everything already on the caller's stream
     if (hipEventRecord(x->ev_begin, s0) != hipSuccess || hipStreamWaitEvent(x->sp, x->ev_begin, 0) != hipSuccess ||
         hipStreamWaitEvent(x->sx, x->ev_begin, 0) != hipSuccess || hipStreamWaitEvent(x->sa, x->ev_begin, 0) != hipSuccess)
         return LMR_E_HIP;
@@ -481,17 +514,18 @@ lmr_status_t lmr_batch_exchange(lmr_ctx_t* ctx, const lmr_transport_t* tp, const
     x->send_used[0] = x->send_used[1] = false;
     lmr_status_t st = lmr_stage_begin(ctx, desc);
     if (st != LMR_OK) return st;
-    // a failed exchange closes the session (its staged records are dropped) so the
-    // context stays usable; the device work already enqueued drains first
+    // a failed exchange closes the session (its staged records are dropped) so the context
+    // stays usable; the work already enqueued on the internal streams drains first (after a
+    // transport failure the transport is aborted first: peers may never post their halves)
     struct SessionGuard {
         lmr_ctx_t* c;
         const lmr_transport_t* t;
         bool armed = true;
-        bool tp_failed = false;       // a transport call failed: abort it before draining
+        bool tp_failed = false;
         ~SessionGuard() {
             if (!armed) return;
             if (tp_failed) transport_abort(t);
-            (void)hipDeviceSynchronize();
+            (void)c->xch->drain();
             stage_abort(c->stage);
         }
     } guard{ctx, tp};
@@ -501,30 +535,34 @@ lmr_status_t lmr_batch_exchange(lmr_ctx_t* ctx, const lmr_transport_t* tp, const
     };
     std::vector<ChunkRec> chunks;
     std::vector<uint64_t> isb(npes), iso(npes), irb(npes), iro(npes), vsb(npes), vso(npes), vrb(npes), vro(npes);
-    const int64_t* h_send = static_cast<const int64_t*>(x->h_hdr.p);
-    const int64_t* h_recv = h_send + size_t(npes) * LMR_XHDR_WORDS;
-    uint64_t nchunks = my_k;
-    for (uint64_t j = 0; j < nchunks; j++) {
-        const uint64_t lo = std::min(m, j * chunk), hi = std::min(m, (j + 1) * chunk);
-        const uint64_t cnt = hi - lo;
-        if (returning && x->pos.size() <= j) x->pos.resize(j + 1);
+    auto h_send_rows = [&](int b) { return static_cast<const int64_t*>(x->h_hdr.p) + size_t(b) * 2 * rows; };
+    auto h_recv_rows = [&](int b) { return h_send_rows(b) + rows; };
+    auto chunk_lo = [&](uint64_t j) { return std::min(m, j * chunk); };
+    auto chunk_hi = [&](uint64_t j) { return std::min(m, (j + 1) * chunk); };
+    // ---- local part of chunk j (pack stream): pack by destination PE into send buffer j&1
+    // and write the chunk's header rows. No collective here, so chunk j+1's pack is enqueued
+    // before the host waits for chunk j's header exchange and runs while it waits.
+    auto counted_pack = [&](uint64_t j) -> lmr_status_t {
         const int b = int(j & 1);
-        // ---- pack this chunk by destination PE (pack stream) into send buffer b, once the
-        // all-to-all-v of chunk j-2 has read it
+        const uint64_t lo = chunk_lo(j), cnt = chunk_hi(j) - lo;
+        const uint8_t* v = scalar ? nullptr : static_cast<const uint8_t*>(d_vals) + lo * eb;
+        uint32_t* pos = returning ? x->pos[j].as<uint32_t>() : nullptr;
+        return (ordered ? lmr_pack : lmr_pack_unordered)(
+            ctx, layout, gidx + lo, cnt, v, desc->dtype, iw, x->send_idx[b].p, scalar ? nullptr : x->send_vals[b].p, pos,
+            x->counts.as<uint64_t>(), x->offsets.as<uint64_t>(), reinterpret_cast<lmr_stream_t>(x->sp));
+    };
+    auto pack_chunk = [&](uint64_t j) -> lmr_status_t {
+        const uint64_t lo = chunk_lo(j), cnt = chunk_hi(j) - lo;
+        const int b = int(j & 1);
         const bool packed = !mvsi && j < my_k && cnt > 0;
+        // send buffer b and its header rows: chunk j-2's all-to-all-v (and, for own records
+        // staged from the send buffer, chunk j-2's staging) must be done with them
         if (x->send_used[b] && hipStreamWaitEvent(x->sp, x->ev_send_free[b], 0) != hipSuccess) return LMR_E_HIP;
-        // (own records are staged from send buffer b on the apply stream: that must be done too)
         if (bypass && x->recv_used[b] && hipStreamWaitEvent(x->sp, x->ev_recv_free[b], 0) != hipSuccess)
             return LMR_E_HIP;
-        const uint32_t cap = uint32_t(free_pack ? region_cap(cnt) : 0);
-        auto counted_pack = [&]() -> lmr_status_t {
-            return lmr_pack_unordered(ctx, layout, gidx + lo, cnt, scalar ? nullptr : static_cast<const uint8_t*>(d_vals) + lo * eb,
-                                      desc->dtype, iw, x->send_idx[b].p, scalar ? nullptr : x->send_vals[b].p,
-                                      returning ? x->pos[j].as<uint32_t>() : nullptr, x->counts.as<uint64_t>(),
-                                      x->offsets.as<uint64_t>(), reinterpret_cast<lmr_stream_t>(x->sp));
-        };
+        if (returning && x->pos.size() <= j) x->pos.resize(j + 1);
         if (packed) {
-            if (returning && x->pos[j].need(cnt * 4 + 8) != hipSuccess) return LMR_E_HIP;
+            if (returning && x->pos[j].need(cnt * 4 + 8, x) != hipSuccess) return LMR_E_HIP;
             if (free_pack) {
                 PackArgs pa;
                 pa.layout = *layout;
@@ -541,38 +579,65 @@ lmr_status_t lmr_batch_exchange(lmr_ctx_t* ctx, const lmr_transport_t* tp, const
                 pa.err = ctx->d_err;
                 pa.prof = ctx->prof;
                 pa.stable = false;
-                if (launch_pack_free(pa, x->fill.as<uint32_t>(), cap, x->sp) != hipSuccess) return LMR_E_HIP;
+                if (launch_pack_free(pa, x->fill.as<uint32_t>(), uint32_t(region_cap(cnt)), x->sp) != hipSuccess)
+                    return LMR_E_HIP;
             } else {
-                st = counted_pack();
-                if (st != LMR_OK) return st;
+                const lmr_status_t e = counted_pack(j);
+                if (e != LMR_OK) return e;
             }
         }
+        const int64_t flags = (scalar ? LMR_XHDR_SCALAR : 0) | (ordered ? LMR_XHDR_ORDERED : 0);
         hipLaunchKernelGGL(k_xhdr, dim3((npes + 255) / 256), dim3(256), 0, x->sp, packed ? x->counts.as<uint64_t>() : nullptr,
-                           npes, mvsi && j == 0 ? mvsi_pe : -1, mvsi_off, int64_t(n), int64_t(scalar ? 1 : 0), sbits,
-                           int64_t(my_k), x->hdr_send[b].as<int64_t>());
+                           npes, mvsi && j == 0 ? mvsi_pe : -1, mvsi_off, int64_t(n), flags, sbits, int64_t(my_k),
+                           x->hdr_send[b].as<int64_t>());
         if (hipGetLastError() != hipSuccess) return LMR_E_HIP;
-        if (hipEventRecord(x->ev_packed[b], x->sp) != hipSuccess || hipStreamWaitEvent(x->sx, x->ev_packed[b], 0) != hipSuccess)
+        return hipEventRecord(x->ev_packed[b], x->sp) == hipSuccess ? LMR_OK : LMR_E_HIP;
+    };
+    uint64_t packed_upto = 0;                          // chunks [0, packed_upto) are enqueued on sp
+    auto pack_until = [&](uint64_t upto) -> lmr_status_t {
+        while (packed_upto < upto) {
+            const lmr_status_t e = pack_chunk(packed_upto);
+            if (e != LMR_OK) return e;
+            packed_upto++;
+        }
+        return LMR_OK;
+    };
+    // ---- the header all-to-all of chunk j (exchange stream) and its rows to the host
+    auto post_header = [&](uint64_t j) -> lmr_status_t {
+        const int b = int(j & 1);
+        if (hipStreamWaitEvent(x->sx, x->ev_packed[b], 0) != hipSuccess) return LMR_E_HIP;
+        lmr_status_t e = tp_alltoall(tp, x, x->hdr_send[b].p, x->hdr_recv[b].p, LMR_XHDR_WORDS * 8, x->sx);
+        if (e != LMR_OK) { guard.tp_failed = true; return e; }
+        int64_t* hs_ = const_cast<int64_t*>(h_send_rows(b));
+        if (hipMemcpyAsync(hs_, x->hdr_send[b].p, rows * 8, hipMemcpyDeviceToHost, x->sx) != hipSuccess ||
+            hipMemcpyAsync(hs_ + rows, x->hdr_recv[b].p, rows * 8, hipMemcpyDeviceToHost, x->sx) != hipSuccess ||
+            hipEventRecord(x->ev_hdr[b], x->sx) != hipSuccess)
             return LMR_E_HIP;
-        // ---- the exchange stream: header all-to-all, then the host reads this chunk's counts
-        // (one wait per chunk; the next chunk's pack is not enqueued yet, the previous
-        // chunk's staging runs meanwhile): sent rows, then received rows
-        st = tp_alltoall(tp, x, x->hdr_send[b].p, x->hdr_recv.p, LMR_XHDR_WORDS * 8, x->sx);
-        if (st != LMR_OK) { guard.tp_failed = true; return st; }
-        if (hipMemcpyAsync(x->h_hdr.p, x->hdr_send[b].p, size_t(npes) * LMR_XHDR_WORDS * 8, hipMemcpyDeviceToHost,
-                           x->sx) != hipSuccess)
-            return LMR_E_HIP;
-        if (hipMemcpyAsync(static_cast<int64_t*>(x->h_hdr.p) + size_t(npes) * LMR_XHDR_WORDS, x->hdr_recv.p,
-                           size_t(npes) * LMR_XHDR_WORDS * 8, hipMemcpyDeviceToHost, x->sx) != hipSuccess ||
-            hipEventRecord(x->ev_hdr, x->sx) != hipSuccess || hipEventSynchronize(x->ev_hdr) != hipSuccess)
-            return LMR_E_HIP;
+        return LMR_OK;
+    };
+    // chunk 0: pack, header exchange; chunk 1's pack (local work) runs during the wait
+    if ((st = pack_until(1)) != LMR_OK) return st;
+    if ((st = post_header(0)) != LMR_OK) return st;
+    if ((st = pack_until(std::min<uint64_t>(my_k, 2))) != LMR_OK) return st;
+    uint64_t nchunks = 1;
+    for (uint64_t j = 0; j < nchunks; j++) {
+        const int b = int(j & 1);
+        // ---- the host reads chunk j's header rows (one wait per chunk: RCCL's send / recv
+        // counts are host arguments); meanwhile the pack stream runs chunk j+1's pack and the
+        // apply stream chunk j-1's staging
+        if (hipEventSynchronize(x->ev_hdr[b]) != hipSuccess) return LMR_E_HIP;
+        const int64_t* h_send = h_send_rows(b);
+        const int64_t* h_recv = h_recv_rows(b);
         const uint64_t k = lmr_exchange_plan(npes, iw, eb, h_send, h_recv, isb.data(), iso.data(), irb.data(),
                                              iro.data(), vsb.data(), vso.data(), vrb.data(), vro.data());
         if (j == 0) nchunks = std::max<uint64_t>(k, 1);
-        if (packed && free_pack) {
+        const uint64_t lo = chunk_lo(j), hi = chunk_hi(j);
+        if (!mvsi && j < my_k && hi > lo && free_pack) {
+            const uint32_t cap = uint32_t(region_cap(hi - lo));
             bool over = false;
             for (uint32_t p = 0; p < npes; p++) over = over || h_send[p * LMR_XHDR_WORDS] > int64_t(cap);
             if (over) {                                 // same counts, contiguous layout: the plan's offsets
-                st = counted_pack();
+                st = counted_pack(j);
                 if (st != LMR_OK) return st;
                 if (hipEventRecord(x->ev_packed[b], x->sp) != hipSuccess ||
                     hipStreamWaitEvent(x->sx, x->ev_packed[b], 0) != hipSuccess)
@@ -601,12 +666,8 @@ lmr_status_t lmr_batch_exchange(lmr_ctx_t* ctx, const lmr_transport_t* tp, const
         // ---- receive buffers of this chunk (double-buffered against the apply stream)
         if (x->recv_used[b] && hipStreamWaitEvent(x->sx, x->ev_recv_free[b], 0) != hipSuccess) return LMR_E_HIP;
         const uint64_t ib = iro[npes - 1] + irb[npes - 1], vb = vro[npes - 1] + vrb[npes - 1];
-        if (x->recv_idx[b].cap < ib + 8 || x->recv_vals[b].cap < vb + 8) {
-            // growing frees the old buffer: nothing may still use it
-            if (hipStreamSynchronize(x->sa) != hipSuccess) return LMR_E_HIP;
-            if (x->recv_idx[b].need(ib + 8) != hipSuccess || x->recv_vals[b].need(vb + 8) != hipSuccess)
-                return LMR_E_HIP;
-        }
+        if (x->recv_idx[b].need(ib + 8, x) != hipSuccess || x->recv_vals[b].need(vb + 8, x) != hipSuccess)
+            return LMR_E_HIP;
         const uint8_t* send_vals = mvsi ? static_cast<const uint8_t*>(d_vals) : x->send_vals[b].as<uint8_t>();
         st = tp_alltoallv(tp, x, x->send_idx[b].p, isb.data(), iso.data(), x->recv_idx[b].p, irb.data(), iro.data(),
                           unit_for(iw), x->sx);
@@ -616,13 +677,13 @@ lmr_status_t lmr_batch_exchange(lmr_ctx_t* ctx, const lmr_transport_t* tp, const
         if (st != LMR_OK) { guard.tp_failed = true; return st; }
         if (hipEventRecord(x->ev_send_free[b], x->sx) != hipSuccess) return LMR_E_HIP;
         x->send_used[b] = true;
-        if (hipEventRecord(x->ev_x, x->sx) != hipSuccess || hipStreamWaitEvent(x->sa, x->ev_x, 0) != hipSuccess)
+        if (hipEventRecord(x->ev_x[b], x->sx) != hipSuccess || hipStreamWaitEvent(x->sa, x->ev_x[b], 0) != hipSuccess)
             return LMR_E_HIP;
         // ---- owner side: stage every source's records (apply stream)
         if (returning) {
             if (x->res.size() <= j) { x->res.resize(j + 1); x->rok.resize(j + 1); }
-            if (x->res[j].need(cr.total * eb + 8) != hipSuccess) return LMR_E_HIP;
-            if (want_ok && x->rok[j].need(cr.total + 8) != hipSuccess) return LMR_E_HIP;
+            if (x->res[j].need(cr.total * eb + 8, x) != hipSuccess) return LMR_E_HIP;
+            if (want_ok && x->rok[j].need(cr.total + 8, x) != hipSuccess) return LMR_E_HIP;
         }
         uint64_t io = 0, vo = 0, ro = 0;
         lmr_stream_t sa = reinterpret_cast<lmr_stream_t>(x->sa);
@@ -644,21 +705,29 @@ lmr_status_t lmr_batch_exchange(lmr_ctx_t* ctx, const lmr_transport_t* tp, const
                 p++;
                 continue;
             }
-            // consecutive sources with the same value form go in one stream
-            const int64_t sc = r[2], bits = r[3];
+            // consecutive sources with the same value form and order flag go in one stream (an
+            // ordered stream of several sources keeps each source's records in its order)
+            const int64_t fl = r[2], bits = r[3];
+            const bool sc = (fl & LMR_XHDR_SCALAR) != 0, ord = (fl & LMR_XHDR_ORDERED) != 0;
             uint32_t e = p;
             uint64_t tot = 0;
             while (e < npes) {
                 const int64_t* q = h_recv + uint64_t(e) * LMR_XHDR_WORDS;
                 if (cr.recv_cnt[e] == 0) { e++; continue; }
-                if (q[1] >= 0 || q[2] != sc || (sc && q[3] != bits)) break;
+                if (q[1] >= 0 || q[2] != fl || (sc && q[3] != bits)) break;
                 if (bypass && (e == me) != own) break;  // own records are a stream of their own
                 tot += cr.recv_cnt[e];
                 e++;
                 if (own) break;
             }
             const uint64_t ubits = uint64_t(bits);
-            st = lmr_stage_soa(ctx, src_i, iw, sc ? nullptr : src_v, sc ? &ubits : nullptr, tot, res, okp, sa);
+            if (ord) {                                  // applied now, each element's records in stream order
+                lmr_apply_desc_t d = *desc;
+                d.strategy = LMR_STRATEGY_ORDERED;
+                st = lmr_apply_soa(ctx, &d, src_i, iw, sc ? nullptr : src_v, sc ? &ubits : nullptr, tot, res, okp, sa);
+            } else {
+                st = lmr_stage_soa(ctx, src_i, iw, sc ? nullptr : src_v, sc ? &ubits : nullptr, tot, res, okp, sa);
+            }
             if (st != LMR_OK) return st;
             io += tot * iw;
             if (!sc) vo += tot * eb;
@@ -668,6 +737,14 @@ lmr_status_t lmr_batch_exchange(lmr_ctx_t* ctx, const lmr_transport_t* tp, const
         if (hipEventRecord(x->ev_recv_free[b], x->sa) != hipSuccess) return LMR_E_HIP;
         x->recv_used[b] = true;
         chunks.push_back(std::move(cr));
+        // ---- the next chunk's header exchange (after this chunk's all-to-all-v on the
+        // exchange stream: every PE posts the collectives in the same order), and the pack of
+        // the chunk after it, which runs while the host waits for that header
+        if (j + 1 < nchunks) {
+            if ((st = pack_until(j + 2)) != LMR_OK) return st;
+            if ((st = post_header(j + 1)) != LMR_OK) return st;
+            if ((st = pack_until(std::min<uint64_t>(j + 3, nchunks))) != LMR_OK) return st;
+        }
     }
     // ---- one shard sweep, then results back to their senders
     st = lmr_stage_finish(ctx, reinterpret_cast<lmr_stream_t>(x->sa));
@@ -685,11 +762,8 @@ lmr_status_t lmr_batch_exchange(lmr_ctx_t* ctx, const lmr_transport_t* tp, const
                 orb[p] = cr.send_cnt[p]; oro[p] = ro[p] / eb;
                 nsent += cr.send_cnt[p];
             }
-            if (x->back.cap < nsent * eb + 8 || (want_ok && x->back_ok.cap < nsent + 8)) {
-                if (hipStreamSynchronize(x->sa) != hipSuccess) return LMR_E_HIP;
-                if (x->back.need(nsent * eb + 8) != hipSuccess || (want_ok && x->back_ok.need(nsent + 8) != hipSuccess))
-                    return LMR_E_HIP;
-            }
+            if (x->back.need(nsent * eb + 8, x) != hipSuccess || (want_ok && x->back_ok.need(nsent + 8, x) != hipSuccess))
+                return LMR_E_HIP;
             if (bypass && cr.recv_cnt[me]) {           // own results: a device copy, not the transport
                 if (hipMemcpyAsync(static_cast<uint8_t*>(x->back.p) + ro[me], x->res[j].as<uint8_t>() + so[me], sb[me],
                                    hipMemcpyDeviceToDevice, x->sa) != hipSuccess ||
@@ -705,7 +779,7 @@ lmr_status_t lmr_batch_exchange(lmr_ctx_t* ctx, const lmr_transport_t* tp, const
                                   x->sa);
             if (st != LMR_OK) {                         // (the session is already applied)
                 transport_abort(tp);
-                (void)hipDeviceSynchronize();
+                (void)x->drain();
                 return st;
             }
             if (nsent == 0) continue;

@@ -30,7 +30,7 @@ struct lmr_ctx {
     lmr::XState* xch = nullptr;        // multi-PE exchange state (lmr_batch_exchange), lazily made
     lmr::WinState* win = nullptr;      // window partition of shards above one tiled window, lazily made
     lmr::WireBufs* wire = nullptr;     // staging of lmr_apply_msg (AM wire format), lazily made
-    lmr::OrdBufs* ord = nullptr;       // sort buffers of the ordered apply (n > 1024), lazily made
+    lmr::OrdBufs* ord = nullptr;       // sort buffers of the ordered apply (n > 1024), see ord_reserve
 };
 
 namespace lmr {
@@ -130,6 +130,11 @@ hipError_t launch_apply_mvsi(int dtype, const ApplyArgs& a, uint64_t index, hipS
 // LMR_STRATEGY_ORDERED (lmr_ordered.hip): per element in record order, one atomic block each
 hipError_t launch_apply_ordered(lmr_ctx* ctx, int dtype, int index_size, const ApplyArgs& a, hipStream_t s);
 constexpr uint64_t kOrderedAuto = 1000;   // AUTO: below this many records (one reference AM at 1 PE)
+// sort buffers of the ordered apply: one piece of records (lmr_ctx_create reserves the minimum,
+// lmr_ctx_reserve up to the maximum); larger calls run piece after piece
+constexpr uint64_t kOrderedMinPiece = uint64_t(1) << 16;
+constexpr uint64_t kOrderedMaxPiece = uint64_t(1) << 22;
+hipError_t ord_reserve(lmr_ctx* ctx, uint64_t recs);
 // tiled apply of SoA/AoS records; returns hipErrorNotSupported when the shard
 // is too large for the single-level tile histogram.
 hipError_t launch_apply_tiled(int dtype, int index_size, const ApplyArgs& a, const TiledWs& w,

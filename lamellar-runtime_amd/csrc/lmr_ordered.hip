@@ -17,18 +17,25 @@
 //   n <= 1024 : k_order_small -- one workgroup; the first record of each element (no earlier
 //               record names it: an LDS scan) walks the element's later records in order.
 //   n > 1024  : keys (local index, out-of-bounds last) sorted stably with their record
-//               positions (hipcub radix sort), then k_order_chains: the first record of every
-//               run of equal keys walks its run, i.e. the element's records in input order.
+//               positions (rocPRIM's onesweep radix sort), then k_order_chains: the first
+//               record of every run of equal keys walks its run, i.e. the element's records in
+//               input order.
+// Larger calls go in pieces of the reserved capacity, one after another on the stream: every
+// record of a piece is applied before any of the next, so each element still sees its records
+// in input order. The sort buffers are reserved with the context (lmr_ctx_create: 2^16
+// records; lmr_ctx_reserve: up to 2^22), so the ordered path never allocates.
 #include "lmr_internal.hpp"
 #include "lmr_device.hpp"
-#include <hipcub/hipcub.hpp>
+#include <rocprim/device/device_radix_sort.hpp>
 #include <algorithm>
 
 namespace lmr {
 
 struct OrdBufs {
     void* p = nullptr;
-    size_t cap = 0;
+    size_t bytes = 0;
+    uint64_t recs = 0;        // records of one sorted piece
+    size_t tmp = 0;           // rocPRIM temporary storage for a piece of `recs`
 };
 
 void ord_bufs_free(OrdBufs* b) {
@@ -195,12 +202,41 @@ hipError_t ord_iw(int iw, F&& f) {
 
 size_t al256(size_t b) { return (b + 255) & ~size_t(255); }
 
+hipError_t sort_storage(uint64_t n, int bits, size_t& tmp) {
+    tmp = 0;
+    return rocprim::radix_sort_pairs(nullptr, tmp, (const uint64_t*)nullptr, (uint64_t*)nullptr,
+                                     (const uint32_t*)nullptr, (uint32_t*)nullptr, size_t(n), 0u, unsigned(bits),
+                                     hipStream_t(0));
+}
+
+size_t piece_bytes(uint64_t recs, size_t tmp) { return 2 * al256(recs * 8) + 2 * al256(recs * 4) + al256(tmp); }
+
 }  // namespace
 
-hipError_t launch_apply_ordered(lmr_ctx* ctx, int dtype, int iw, const ApplyArgs& a, hipStream_t s) {
-    if (a.n == 0) return hipSuccess;
-    if (a.n > 0xFFFFFFFFull) return hipErrorInvalidValue;
-    ProfScope ps(a.prof, LMR_STAGE_ORDERED, s, a.n);
+hipError_t ord_reserve(lmr_ctx* ctx, uint64_t recs) {
+    recs = std::min<uint64_t>(std::max<uint64_t>(recs, kOrderedMinPiece), kOrderedMaxPiece);
+    if (!ctx->ord) ctx->ord = new OrdBufs();
+    OrdBufs* B = ctx->ord;
+    if (B->recs >= recs) return hipSuccess;
+    size_t tmp = 0;
+    hipError_t e = sort_storage(recs, 64, tmp);          // the widest key range: covers every shard
+    if (e != hipSuccess) return e;
+    void* p = nullptr;
+    if ((e = hipMalloc(&p, piece_bytes(recs, tmp))) != hipSuccess) return e;
+    if (B->p) {                                          // (outside the hot path: lmr_ctx_reserve)
+        (void)hipDeviceSynchronize();
+        (void)hipFree(B->p);
+    }
+    B->p = p;
+    B->bytes = piece_bytes(recs, tmp);
+    B->recs = recs;
+    B->tmp = tmp;
+    return hipSuccess;
+}
+
+namespace {
+
+hipError_t apply_ordered_piece(const OrdBufs* B, int dtype, int iw, const ApplyArgs& a, hipStream_t s) {
     if (a.n <= kSmall) {
         return ord_dtype(dtype, [&](auto tag) {
             using T = decltype(tag);
@@ -216,27 +252,14 @@ hipError_t launch_apply_ordered(lmr_ctx* ctx, int dtype, int iw, const ApplyArgs
     int bits = 1;
     while (bits < 64 && (a.shard_len >> bits) != 0) bits++;
     size_t tmp = 0;
-    hipError_t e = hipcub::DeviceRadixSort::SortPairs(nullptr, tmp, (const uint64_t*)nullptr, (uint64_t*)nullptr,
-                                                      (const uint32_t*)nullptr, (uint32_t*)nullptr, int(n), 0, bits, s);
+    hipError_t e = sort_storage(n, bits, tmp);
     if (e != hipSuccess) return e;
-    const size_t need = 2 * al256(n * 8) + 2 * al256(n * 4) + al256(tmp);
-    if (!ctx->ord) ctx->ord = new OrdBufs();
-    OrdBufs* B = ctx->ord;
-    if (B->cap < need) {                       // grows once; the ordered path is not the bulk path
-        if (B->p) {
-            if ((e = hipStreamSynchronize(s)) != hipSuccess) return e;
-            (void)hipFree(B->p);
-            B->p = nullptr;
-            B->cap = 0;
-        }
-        if ((e = hipMalloc(&B->p, need)) != hipSuccess) { B->p = nullptr; return e; }
-        B->cap = need;
-    }
+    if (tmp > B->tmp) return hipErrorInvalidValue;       // (never: storage grows with n and bits)
     uint8_t* q = static_cast<uint8_t*>(B->p);
-    uint64_t* k_in = reinterpret_cast<uint64_t*>(q);   q += al256(n * 8);
-    uint64_t* k_out = reinterpret_cast<uint64_t*>(q);  q += al256(n * 8);
-    uint32_t* p_in = reinterpret_cast<uint32_t*>(q);   q += al256(n * 4);
-    uint32_t* p_out = reinterpret_cast<uint32_t*>(q);  q += al256(n * 4);
+    uint64_t* k_in = reinterpret_cast<uint64_t*>(q);   q += al256(B->recs * 8);
+    uint64_t* k_out = reinterpret_cast<uint64_t*>(q);  q += al256(B->recs * 8);
+    uint32_t* p_in = reinterpret_cast<uint32_t*>(q);   q += al256(B->recs * 4);
+    uint32_t* p_out = reinterpret_cast<uint32_t*>(q);  q += al256(B->recs * 4);
     void* t = q;
     const unsigned grid = unsigned(std::min<uint64_t>((n + 255) / 256, 4096));
     e = ord_iw(iw, [&](auto w) {
@@ -245,13 +268,34 @@ hipError_t launch_apply_ordered(lmr_ctx* ctx, int dtype, int iw, const ApplyArgs
         return hipGetLastError();
     });
     if (e != hipSuccess) return e;
-    e = hipcub::DeviceRadixSort::SortPairs(t, tmp, k_in, k_out, p_in, p_out, int(n), 0, bits, s);
+    e = rocprim::radix_sort_pairs(t, tmp, k_in, k_out, p_in, p_out, size_t(n), 0u, unsigned(bits), s);
     if (e != hipSuccess) return e;
     return ord_dtype(dtype, [&](auto tag) {
         using T = decltype(tag);
         hipLaunchKernelGGL((k_order_chains<T>), dim3(grid), dim3(256), 0, s, a, k_out, p_out);
         return hipGetLastError();
     });
+}
+
+}  // namespace
+
+hipError_t launch_apply_ordered(lmr_ctx* ctx, int dtype, int iw, const ApplyArgs& a, hipStream_t s) {
+    if (a.n == 0) return hipSuccess;
+    const OrdBufs* B = ctx->ord;
+    if (!B || B->recs == 0) return hipErrorNotInitialized;
+    ProfScope ps(a.prof, LMR_STAGE_ORDERED, s, a.n);
+    const int eb = dtype_bytes(dtype);
+    for (uint64_t p0 = 0; p0 < a.n; p0 += B->recs) {
+        ApplyArgs b = a;
+        b.n = std::min<uint64_t>(a.n - p0, B->recs);
+        b.idx = a.idx + p0 * a.idx_stride;
+        if (a.val) b.val = a.val + p0 * a.val_stride;
+        if (a.results) b.results = static_cast<uint8_t*>(a.results) + p0 * uint64_t(eb);
+        if (a.ok) b.ok = a.ok + p0;
+        const hipError_t e = apply_ordered_piece(B, dtype, iw, b, s);
+        if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
 }
 
 }  // namespace lmr

@@ -8,6 +8,12 @@ lmr_batch_exchange, with indices that collide across PEs, and saves per case the
 global array before and after, this PE's records and what came back. The parent
 checks them with the oracle (tests/test_gpu_dist_ordered.py).
 
+LMR_MODE=small runs instead one-AM batches (fewer than 1000 records per PE, indices
+repeated within and across PEs): swap, store, compare_exchange, fetch_rem and f64
+fetch_add, whose outcome the reference fixes per source (each destination's records in
+input order, applied sequentially by the owner's AM); the parent replays them with the
+oracle (test_gpu_dist_small.py).
+
 LMR_XPORT=devptr replaces the transport by `DevPtrGlooTransport` below: a
 host_buffers = 0 transport (the library hands it device pointers, exactly as it
 hands them to RCCL) whose collectives run over gloo. It copies each PE's segment
@@ -112,7 +118,9 @@ class DevPtrGlooTransport:
 
 
 def main():
-    from opgen import CODE, NP, CAS, CAS_EPS, FETCH_ADD, FETCH_MUL, FETCH_XOR, SWAP, AND, OR, XOR
+    from opgen import CODE, NP, ADD, CAS, CAS_EPS, FETCH_ADD, FETCH_MUL, FETCH_XOR, SWAP, AND, OR, XOR
+    if os.environ.get("LMR_MODE") == "small":
+        return main_small()
     world = lam.LamellarWorldBuilder().build()
     team = world.team()
     me, ws = world.my_pe(), world.num_pes()
@@ -197,6 +205,10 @@ def main():
     case("fadd_f32", lam.AtomicArray, "f32", FETCH_ADD, lambda a, i, v: a.batch_fetch_add(i, v),
          lambda n, _t: rng.integers(-1000, 1000, n).astype(np.float32), pick(hot, nrec),
          rng.integers(-64, 64, nrec).astype(np.float32))
+    # C4's op: u64 batch_add (wrapping sums commute: the final array is bit-exact)
+    case("add_u64", lam.AtomicArray, "u64", ADD, lambda a, i, v: a.batch_add(i, v),
+         u_any(np.uint64), rng.integers(0, n_len, nrec).astype(np.uint64),
+         rng.integers(0, 2**64, nrec, dtype=np.uint64))
     # C5's mixed u32 sequence on one array: bit_and, bit_or, bit_xor, swap, compare_exchange(0)
     c5 = lam.AtomicArray(team, n_len, dist_kind, "u32")
     c5.local_data().copy_(_storage(rng.integers(0, 4, c5.num_elems_local()), c5))
@@ -227,6 +239,60 @@ def main():
     tp = team._transport
     out["xport"] = np.array([getattr(tp, "gapped_send", -1), getattr(tp, "gapped_recv", -1),
                              getattr(tp, "calls", -1)])
+    np.savez(os.path.join(os.environ["LMR_OUT"], f"pe{me}.npz"), **out)
+    world.barrier()
+    if ws > 1:
+        dist.destroy_process_group()
+
+
+def main_small():
+    """One-AM batches: every PE issues fewer than 1000 records per batch over a small hot set
+    that all PEs share, so elements are hit repeatedly by every source."""
+    from opgen import CODE, NP, CAS, FETCH_ADD, FETCH_REM, STORE, SWAP
+    world = lam.LamellarWorldBuilder().build()
+    team = world.team()
+    me, ws = world.my_pe(), world.num_pes()
+    if os.environ.get("LMR_XPORT") == "devptr":
+        team._transport = DevPtrGlooTransport(ws, me, team.group)
+    dist_kind = int(os.environ["LMR_DIST"])
+    n_len = int(os.environ["LMR_LEN"])
+    nrec = int(os.environ["LMR_NREC"])
+    assert nrec < 1000
+    rng = np.random.default_rng(5151 + 31 * me)
+    hot = np.random.default_rng(77).choice(n_len, 24, replace=False).astype(np.uint64)
+    out = {}
+
+    def case(name, cls, dt, op, fn, init, vals, cur=None):
+        arr = cls(team, n_len, dist_kind, dt)
+        t = NP[dt]
+        arr.local_data().copy_(_storage(init(arr.num_elems_local()).astype(t), arr))
+        world.barrier()
+        before = arr.to_numpy()
+        idx = hot[rng.integers(0, hot.size, nrec)]
+        r = fn(arr, idx, vals).block()
+        world.barrier()
+        out[name + ":before"], out[name + ":after"] = before, arr.to_numpy()
+        out[name + ":idx"], out[name + ":vals"] = idx, vals.astype(t)
+        out[name + ":meta"] = np.array([op, CODE[dt], arr.kind])
+        if r is not None:
+            if hasattr(r, "numpy") and not isinstance(r, torch.Tensor):
+                v, ok = r.numpy()
+                out[name + ":res"], out[name + ":ok"] = v, ok.astype(np.uint8)
+            else:
+                out[name + ":res"] = r.cpu().numpy().view(t)
+        if cur is not None:
+            out[name + ":cur"] = np.array([cur], dtype=t)
+
+    case("swap_u64", lam.AtomicArray, "u64", SWAP, lambda a, i, v: a.batch_swap(i, v),
+         lambda n: rng.integers(0, 2**63, n, dtype=np.uint64), rng.integers(0, 2**63, nrec, dtype=np.uint64))
+    case("store_u32", lam.AtomicArray, "u32", STORE, lambda a, i, v: a.batch_store(i, v),
+         lambda n: rng.integers(0, 2**32, n, dtype=np.uint64), rng.integers(0, 2**32, nrec, dtype=np.uint64))
+    case("cas_i64", lam.AtomicArray, "i64", CAS, lambda a, i, v: a.batch_compare_exchange(i, np.int64(1), v),
+         lambda n: rng.integers(0, 3, n), rng.integers(0, 3, nrec).astype(np.int64), cur=np.int64(1))
+    case("frem_u32", lam.AtomicArray, "u32", FETCH_REM, lambda a, i, v: a.batch_fetch_rem(i, v),
+         lambda n: rng.integers(2**20, 2**32, n, dtype=np.uint64), rng.integers(2, 1000, nrec).astype(np.uint32))
+    case("fadd_f64", lam.AtomicArray, "f64", FETCH_ADD, lambda a, i, v: a.batch_fetch_add(i, v),
+         lambda n: rng.random(n) * 1e3, rng.random(nrec) * 10.0 - 5.0)
     np.savez(os.path.join(os.environ["LMR_OUT"], f"pe{me}.npz"), **out)
     world.barrier()
     if ws > 1:

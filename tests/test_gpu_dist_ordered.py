@@ -9,8 +9,8 @@ Its op tests run every op at 2, 3 and 4 PEs (lamellar_run.sh:31-40, tests/add.rs
 tests/array/atomic_ops/{swap,compare_exchange}_test.rs).
 
 Checks, per case, over the records of every PE together (indices collide across PEs):
-* and / or / xor (C5's first three batches): the final global array bit-exact against
-  the oracle's sequential apply;
+* add (C4's u64 batch_add) and and / or / xor (C5's first three batches): the final global
+  array bit-exact against the oracle's sequential apply;
 * swap, compare_exchange (Result values and Ok flags), compare_exchange_epsilon
   (NativeAtomic, GenericAtomic, LocalLock), fetch_xor, fetch_mul, fetch_add on i16 and
   f32: per element, the returned values / Ok flags and the final value form one serial
@@ -31,7 +31,7 @@ import tempfile
 import numpy as np
 import pytest
 
-from opgen import AND, NP, OR, XOR
+from opgen import ADD, AND, NP, OR, XOR
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 WORKER = os.path.join(ROOT, "tests", "dist_ordered_worker.py")
@@ -45,9 +45,9 @@ CHUNK = 1 << 16
 
 def run_pes(ws, dist_kind, env_extra, outdir, port):
     env = dict(os.environ)
-    env.update(env_extra)
     env.update(LMR_ROOT=ROOT, LMR_OUT=outdir, LMR_DIST=str(dist_kind), LMR_LEN=str(LEN), LMR_NREC=str(NREC),
                LAMELLAR_EXCHANGE_CHUNK=str(CHUNK), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    env.update(env_extra)
     procs = [subprocess.Popen([sys.executable, "-u", WORKER],
                               env=dict(env, RANK=str(r), WORLD_SIZE=str(ws), LOCAL_RANK=str(r)))
              for r in range(ws)]
@@ -63,7 +63,7 @@ def run_pes(ws, dist_kind, env_extra, outdir, port):
 
 def check_cases(orc, pe):
     names = sorted({k.split(":")[0] for k in pe[0] if k.endswith(":meta")})
-    assert len(names) == 15, names
+    assert len(names) == 16, names
     for name in names:
         op, code, kind = (int(x) for x in pe[0][name + ":meta"])
         t = NP[DTN[code]]
@@ -73,7 +73,7 @@ def check_cases(orc, pe):
             assert np.array_equal(p[name + ":after"].view(np.uint8), after.view(np.uint8)), name
         idx = np.concatenate([p[name + ":idx"] for p in pe])
         vals = np.concatenate([p[name + ":vals"] for p in pe]).astype(t)
-        if op in (AND, OR, XOR):
+        if op in (ADD, AND, OR, XOR):
             ref = before.copy()
             L = orc.layout_new(ref.size, 1, 0, 0)
             st, _, _ = orc.batch_op(L, [ref], kind, code, t, op, idx, vals)
@@ -90,8 +90,8 @@ def check_cases(orc, pe):
         assert st == 0, (name, "status", st, "element", bad, "records", int((idx == bad).sum()))
 
 
-@pytest.mark.parametrize("ws,dist_kind", [(2, 0), (4, 1), (8, 0), (8, 1)],
-                         ids=["2pe-Block", "4pe-Cyclic", "8pe-Block", "8pe-Cyclic"])
+@pytest.mark.parametrize("ws,dist_kind", [(2, 0), (3, 0), (4, 1), (8, 0), (8, 1)],
+                         ids=["2pe-Block", "3pe-Block", "4pe-Cyclic", "8pe-Block", "8pe-Cyclic"])
 def test_ordered_ops_gloo_host_transport(orc, ws, dist_kind):
     with tempfile.TemporaryDirectory() as d:
         pe = run_pes(ws, dist_kind, {"LAMELLAR_COMM_BACKEND": "gloo"}, d, 29300 + 10 * ws + dist_kind)
