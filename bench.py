@@ -593,7 +593,6 @@ def e2e(lam, team, W, args):
     return out
 
 
-_PINNED_KEEP = []
 
 
 def e2e_wire(lam, team, W, args):
@@ -615,7 +614,6 @@ def e2e_wire(lam, team, W, args):
     olds = np.empty(W.n, dtype=np.uint64)
     k.host_register(buf)
     k.host_register(olds)
-    _PINNED_KEEP.extend([buf, olds])      # registered ranges stay allocated (see tests/test_gpu_host.py)
     try:
         shard, slen = W.arr.local_shard(), W.arr.num_elems_local()
         kind = int(W.arr.kind)

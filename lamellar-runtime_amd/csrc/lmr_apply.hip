@@ -353,13 +353,13 @@ __device__ __forceinline__ void small_excl_scan(const uint32_t* hist, uint32_t* 
 // in flight while the staged round is written out.
 // RPT records per thread per round (kRound = RPT * 1024 records staged in LDS).
 template <int IW, int VB, int RPT>
-__global__ __launch_bounds__(1024) void k_coarse_scatter(PartArgs p) {
+__device__ __forceinline__ void coarse_scatter_body(const PartArgs& p, const uint32_t g) {
     using V = typename idx_t<VB>::I;
     constexpr uint32_t kRound = RPT * 1024;
     __shared__ uint32_t hist[kMaxCoarse], base[kMaxCoarse], cursor[kMaxCoarse], tot;
     __shared__ uint32_t s_idx[kRound];
     __shared__ V s_val[kRound];
-    const uint32_t g = blockIdx.x, C = p.C;
+    const uint32_t C = p.C;
     const int cshift = p.tile_shift + kFineShift;
     if (p.bstart_out) {
         coarse_cursors_from_counts(p, g, cursor, hist, base, reinterpret_cast<uint32_t*>(s_idx), &tot);
@@ -447,6 +447,11 @@ __global__ __launch_bounds__(1024) void k_coarse_scatter(PartArgs p) {
         __syncthreads();
         for (uint32_t c = threadIdx.x; c < C; c += blockDim.x) cursor[c] += hist[c];
     }
+}
+
+template <int IW, int VB, int RPT>
+__global__ __launch_bounds__(1024) void k_coarse_scatter(PartArgs p) {
+    coarse_scatter_body<IW, VB, RPT>(p, blockIdx.x);
 }
 
 // Persistent over (coarse bucket c, producer block g) segments, a contiguous
@@ -1125,6 +1130,7 @@ size_t tiled_ws_bytes(uint64_t cap) {
     b += al(rt_rounds_for(cap) * 256 * 4);                           // staged run tables
     b += al(size_t(kMaxRegions) * 2 * (kMaxCoarse + 1) * 4);         // staged piece tables
     b += al(crt_rounds_for(cap) * 256 * 4);                          // staged coarse run tables
+    b += 2 * al(size_t(kMaxRegions) * kMaxTiles * 4);                // staged regions' tile totals, fills
     return b;
 }
 
@@ -1159,6 +1165,9 @@ TiledWs carve_tiled_ws(uint8_t* base, uint64_t cap) {
     p += al(size_t(kMaxRegions) * 2 * (kMaxCoarse + 1) * 4);
     w.crtab = reinterpret_cast<uint32_t*>(p);
     w.crt_rounds = crt_rounds_for(cap);
+    p += al(crt_rounds_for(cap) * 256 * 4);
+    w.rtot = reinterpret_cast<uint32_t*>(p); p += al(size_t(kMaxRegions) * kMaxTiles * 4);
+    w.rfill = reinterpret_cast<uint32_t*>(p);
     w.cap = cap;
     w.tmp_cap = tmp_cap_for(cap);
     return w;
@@ -1639,7 +1648,6 @@ hipError_t launch_apply_tiled(int dtype, int index_size, const ApplyArgs& a, con
 #define LMR_PIECE_RECORDS 16384                  // (variant builds for measurements: -DLMR_PIECE_RECORDS=...)
 #endif
 constexpr uint32_t kPiece = LMR_PIECE_RECORDS;   // records per fine-level piece (2 LDS rounds of 8K)
-constexpr int kStageBstart = 160;                // sinfo words: bstart[kMaxCoarse + 1]
 constexpr int kStageInb = 320;                   //              in-bounds records per region
 static_assert(kStageInb + kMaxRegions <= kStageInfoWords, "staged scratch");
 
@@ -1653,7 +1661,7 @@ static_assert(kStageInb + kMaxRegions <= kStageInfoWords, "staged scratch");
 // its row of p.trows: k_coarse_scatter folds the rows into tile totals, k_fine_piece turns
 // them into tile starts and reserves each round's tile runs inside them.
 template <int IW>
-__global__ __launch_bounds__(1024) void k_ccount(PartArgs p) {
+__device__ __forceinline__ void ccount_body(const PartArgs& p, const uint32_t bid) {
     // loads in flight per thread (4: C5 count 0.347 -> 0.337 ms at 8; 16: 0.380 -> 0.398 ms)
     constexpr int U = 8;
     __shared__ uint32_t hist[kMaxCoarse];
@@ -1664,8 +1672,8 @@ __global__ __launch_bounds__(1024) void k_ccount(PartArgs p) {
     // block b counts the sub-range b % csub of producer block b / csub's chunk
     const uint32_t S = p.csub ? p.csub : 1u;
     const uint64_t sub = (p.chunk + S - 1) / S;
-    const uint64_t g0 = uint64_t(blockIdx.x / S) * p.chunk;
-    const uint64_t lo = g0 + uint64_t(blockIdx.x % S) * sub;
+    const uint64_t g0 = uint64_t(bid / S) * p.chunk;
+    const uint64_t lo = g0 + uint64_t(bid % S) * sub;
     const uint64_t hi = min(min(lo + sub, g0 + p.chunk), p.n);
     const int cshift = p.tile_shift + kFineShift;
     bool oob = false;
@@ -1690,8 +1698,8 @@ __global__ __launch_bounds__(1024) void k_ccount(PartArgs p) {
     if (oob) raise_err(p.err, LMR_ERRBIT_OOB);
     __syncthreads();
     for (uint32_t c = threadIdx.x; c < p.C; c += blockDim.x)
-        p.coarse_off[uint64_t(c) * p.G * S + blockIdx.x] = hist[c];
-    uint32_t* row = p.trows + uint64_t(blockIdx.x) * p.num_tiles;
+        p.coarse_off[uint64_t(c) * p.G * S + bid] = hist[c];
+    uint32_t* row = p.trows + uint64_t(bid) * p.num_tiles;
     for (uint32_t t = threadIdx.x; t < p.num_tiles; t += blockDim.x) row[t] = thist[t];
 }
 
@@ -1764,7 +1772,7 @@ __device__ __forceinline__ PieceLoc piece_loc(const uint32_t* pbase, const uint3
 // fine level: each piece counting-sorted by tile in LDS rounds, written at its
 // final binned positions (persistent over pieces)
 template <int VB, int RPT>
-__global__ __launch_bounds__(1024) void k_fine_piece(PieceArgs a) {
+__device__ __forceinline__ void fine_piece_body(const PieceArgs& a, const uint32_t bid, const uint32_t nblk) {
     using V = typename idx_t<VB>::I;
     constexpr uint32_t kRound = RPT * 1024;
     __shared__ uint32_t hist[kFine], base[kFine], cursor[kFine], tot;
@@ -1774,13 +1782,13 @@ __global__ __launch_bounds__(1024) void k_fine_piece(PieceArgs a) {
     __shared__ uint32_t s_tt[kFine], s_start[kFine];
     piece_table(a.bstart, a.C, s_pb, s_bs, s_np, &s_tot);
     const uint32_t npieces = s_pb[a.C];
-    if (a.rt && blockIdx.x == 0)
+    if (a.rt && bid == 0)
         for (uint32_t c = threadIdx.x; c <= a.C; c += blockDim.x) {
             a.ptab[c] = s_pb[c];
             a.ptab[a.C + 1 + c] = s_bs[c];
         }
     // tile starts of buckets with no piece (all their tiles empty) and the region's end
-    if (blockIdx.x == 0) {
+    if (bid == 0) {
         for (uint32_t t = threadIdx.x; t < a.num_tiles; t += blockDim.x) {
             const uint32_t c = t >> kFineShift;
             if (s_pb[c + 1] == s_pb[c]) a.ts[t] = a.R + s_bs[c];
@@ -1804,13 +1812,13 @@ __global__ __launch_bounds__(1024) void k_fine_piece(PieceArgs a) {
         }
     };
     auto load_piece = [&](const PieceLoc& L) { load_round(L.lo, L.hi); };
-    uint32_t pid = blockIdx.x;
+    uint32_t pid = bid;
     PieceLoc L{};
     if (pid < npieces) {
         L = piece_loc(s_pb, s_bs, a.C, pid);
         load_piece(L);
     }
-    for (; pid < npieces; pid += gridDim.x) {
+    for (; pid < npieces; pid += nblk) {
         const uint32_t t0 = L.c * kFine;
         const uint32_t nf = min(uint32_t(kFine), a.num_tiles - t0);
         // this bucket's tile starts: bucket start + the tile totals before each tile; the
@@ -1823,7 +1831,7 @@ __global__ __launch_bounds__(1024) void k_fine_piece(PieceArgs a) {
             s_start[threadIdx.x] += a.R + s_bs[L.c];
             if (L.p == 0) a.ts[t0 + threadIdx.x] = s_start[threadIdx.x];
         }
-        const uint32_t nxt = pid + gridDim.x;
+        const uint32_t nxt = pid + nblk;
         PieceLoc LN{};
         if (nxt < npieces) LN = piece_loc(s_pb, s_bs, a.C, nxt);
         for (uint32_t r0 = L.lo; r0 < L.hi; r0 += kRound) {
@@ -1871,6 +1879,86 @@ __global__ __launch_bounds__(1024) void k_fine_piece(PieceArgs a) {
         __syncthreads();
         L = LN;
     }
+}
+
+// ---- fused staged partition. The regions a session has staged since its last partition are
+// partitioned together: one launch per pass (count, coarse, fine) for up to kFuse regions, each
+// region keeping its own block range, count rows, tile totals and tables. Separate launches per
+// region left most of each short launch to ramp and tail (C5: five 27M-record regions per step,
+// count 0.075 ms at ~2.9 TB/s per launch) and ran the coarse pass one block per CU.
+constexpr int kFuse = 8;
+struct CountRegion {
+    const uint8_t* idx;
+    uint64_t idx_stride, n, chunk;
+    uint32_t* coarse_off;       // the region's [C][G * csub] raw counts
+    uint32_t* trows;            // the region's [G * csub][num_tiles] tile-count rows
+    uint32_t G, csub, block0;
+};
+struct CountTable {
+    CountRegion r[kFuse];
+    uint32_t nr, num_tiles, C;
+    int tile_shift;
+    uint64_t shard_len;
+    uint32_t* err;
+};
+struct CoarseRegion {
+    const uint8_t* idx;
+    uint64_t idx_stride;
+    const uint8_t* val;
+    uint64_t val_stride, n, chunk;
+    uint32_t *coarse_off, *bstart_out, *total_out, *trows, *ttot, *tfill, *tmp_idx;
+    uint8_t* tmp_val;
+    uint32_t *qpos, *crt;
+    uint32_t G, csub, rpb, block0;
+};
+struct CoarseTable {
+    CoarseRegion r[kFuse];
+    uint32_t nr, num_tiles, C;
+    int tile_shift;
+    uint64_t shard_len;
+    uint32_t* err;
+};
+struct FineRegion {
+    PieceArgs a;
+    uint32_t block0, nblk;
+};
+struct FineTable {
+    FineRegion r[kFuse];
+    uint32_t nr;
+};
+
+template <int IW>
+__global__ __launch_bounds__(1024) void k_ccount_stage(CountTable t) {
+    uint32_t i = 0;
+    while (i + 1 < t.nr && t.r[i + 1].block0 <= blockIdx.x) i++;
+    const CountRegion& g = t.r[i];
+    PartArgs p{};
+    p.idx = g.idx; p.idx_stride = g.idx_stride; p.n = g.n; p.chunk = g.chunk;
+    p.shard_len = t.shard_len; p.tile_shift = t.tile_shift; p.num_tiles = t.num_tiles; p.C = t.C;
+    p.G = g.G; p.csub = g.csub; p.coarse_off = g.coarse_off; p.trows = g.trows; p.err = t.err;
+    ccount_body<IW>(p, blockIdx.x - g.block0);
+}
+
+template <int IW, int VB, int RPT>
+__global__ __launch_bounds__(1024) void k_coarse_stage(CoarseTable t) {
+    uint32_t i = 0;
+    while (i + 1 < t.nr && t.r[i + 1].block0 <= blockIdx.x) i++;
+    const CoarseRegion& g = t.r[i];
+    PartArgs p{};
+    p.idx = g.idx; p.idx_stride = g.idx_stride; p.val = g.val; p.val_stride = g.val_stride; p.n = g.n;
+    p.chunk = g.chunk; p.shard_len = t.shard_len; p.tile_shift = t.tile_shift; p.num_tiles = t.num_tiles;
+    p.C = t.C; p.G = g.G; p.csub = g.csub; p.coarse_off = g.coarse_off; p.bstart_out = g.bstart_out;
+    p.total_out = g.total_out; p.trows = g.trows; p.ttot = g.ttot; p.tfill = g.tfill; p.tmp_idx = g.tmp_idx;
+    p.tmp_val = g.tmp_val; p.qpos = g.qpos; p.crt = g.crt; p.rpb = g.rpb; p.err = t.err;
+    coarse_scatter_body<IW, VB, RPT>(p, blockIdx.x - g.block0);
+}
+
+template <int VB, int RPT>
+__global__ __launch_bounds__(1024) void k_fine_stage(FineTable t) {
+    uint32_t i = 0;
+    while (i + 1 < t.nr && t.r[i + 1].block0 <= blockIdx.x) i++;
+    const FineRegion& g = t.r[i];
+    fine_piece_body<VB, RPT>(g.a, blockIdx.x - g.block0, g.nblk);
 }
 
 // Round-wise first gather of a staged region's un-partition: one block per fine-pass round. The
@@ -2129,102 +2217,156 @@ hipError_t launch_stage_region(int dtype, int index_size, const ApplyArgs& a, co
     const uint64_t num_tiles = (a.shard_len + (uint64_t(1) << shift) - 1) >> shift;
     if (num_tiles == 0 || num_tiles > uint64_t(kMaxTiles) || a.n > kStageMaxRegion || s.nreg >= kMaxRegions)
         return hipErrorInvalidValue;
-    const uint32_t T = uint32_t(num_tiles);
-    const uint32_t C = uint32_t((num_tiles + kFine - 1) / kFine);
-    const int vb = dtype_bytes(dtype);
+    // the region takes workspace slots [staged, staged + n) now; its records are partitioned
+    // with the session's other pending regions (launch_stage_partition): the caller's record
+    // buffers must stay valid until then
     const int r = s.nreg;
-    const uint32_t R = uint32_t(s.staged);
-    const bool has_res = a.ret != LMR_RET_NONE;
-    uint64_t G = (a.n + 65535) / 65536;
-    if (G > uint64_t(bin_blocks_cap(vb))) G = bin_blocks_cap(vb);
-    if (G < 1) G = 1;
-    uint32_t* bstart = w.sinfo + kStageBstart;
-    uint32_t* inb = w.sinfo + kStageInb + r;
-    PartArgs q{};
-    q.idx = a.idx; q.idx_stride = a.idx_stride; q.val = a.val; q.val_stride = a.val_stride;
-    q.n = a.n; q.shard_len = a.shard_len; q.chunk = (a.n + G - 1) / G; q.tile_shift = shift;
-    q.num_tiles = T; q.G = uint32_t(G); q.C = C;
-    q.coarse_off = w.coarse_off;
-    q.tmp_idx = w.tmp_idx + R;
-    q.tmp_val = a.val ? w.tmp_val + uint64_t(R) * vb : nullptr;
-    q.qpos = has_res ? w.qpos + R : nullptr;
-    q.err = a.err;
-    q.bstart_out = bstart; q.total_out = inb;       // raw counts: k_coarse_scatter derives its offsets
-    // the count pass runs csub blocks per producer block: one 1024-thread block per CU leaves
-    // the read-only pass at half occupancy
-    q.csub = uint32_t(std::max<uint64_t>(1, std::min<uint64_t>(ccount_split(), uint64_t(kMaxBinBlocks) / G)));
-    q.trows = w.counts;                             // G * csub rows of T counts (<= kMaxBinBlocks x kMaxTiles)
-    q.ttot = w.tile_items;
-    q.tfill = w.ff + 64 + size_t(kMaxCoarse) * kSegs;
-    // coarse run tables for the round-wise second un-partition gather
-    uint32_t kcround = 0;
-    dispatch_vb_rpt<4>(vb, coarse_rpt(vb), [&](auto, auto rpt) { kcround = uint32_t(decltype(rpt)::value) * 1024; });
-    const uint32_t rpb = uint32_t((q.chunk + kcround - 1) / kcround);
-    const uint64_t ncr = G * rpb;
-    const bool crounds = has_res && (unpart_rounds() & (vb == 8 ? 4 : 2)) && s.crounds + ncr <= w.crt_rounds;
-    q.crt = crounds ? w.crtab + s.crounds * (2 * kMaxCoarse) : nullptr;
-    q.rpb = rpb;
-    hipError_t e;
-    {
-        ProfScope ps(a.prof, LMR_STAGE_BIN_COUNT, st, a.n);
-        e = dispatch_iw(index_size, [&](auto iw) {
-            constexpr int IW = decltype(iw)::value;
-            hipLaunchKernelGGL((k_ccount<IW>), dim3(unsigned(G * q.csub)), dim3(1024), size_t(T) * 4, st, q);
-            return hipGetLastError();
-        });
-    }
-    if (e != hipSuccess) return e;
-    {
-        ProfScope ps(a.prof, LMR_STAGE_BIN_SCATTER, st, a.n);
-        e = dispatch_iw(index_size, [&](auto iw) {
-            constexpr int IW = decltype(iw)::value;
-            dispatch_vb_rpt<4>(vb, coarse_rpt(vb), [&](auto vbt, auto rpt) {
-                constexpr int VBc = decltype(vbt)::value, RP = decltype(rpt)::value;
-                hipLaunchKernelGGL((k_coarse_scatter<IW, VBc, RP>), dim3(unsigned(G)), dim3(1024), 0, st, q);
-            });
-            return hipGetLastError();
-        });
-    }
-    if (e != hipSuccess) return e;
-    PieceArgs pa;
-    pa.tmp_idx = q.tmp_idx; pa.tmp_val = q.tmp_val; pa.scalar_bits = a.val_bits;
-    pa.tile_shift = shift; pa.num_tiles = T; pa.C = C; pa.bstart = bstart;
-    pa.bin_lidx = w.bin_lidx; pa.bin_val = w.bin_val;
-    pa.rpos = has_res ? w.rpos + R : nullptr; pa.R = R;
-    pa.ts = w.rts + uint64_t(r) * (kMaxTiles + 1); pa.ttot = q.ttot; pa.tfill = q.tfill;
-    const uint64_t max_pieces = (a.n + kPiece - 1) / kPiece + C;
-    // run tables for the round-wise un-partition: rpp rounds per piece, max_pieces * rpp per region
-    uint32_t kround = 0;
-    dispatch_vb_rpt<2>(vb, piece_fine_rpt(vb), [&](auto, auto rpt) { kround = uint32_t(decltype(rpt)::value) * 1024; });
-    const uint32_t rpp = (kPiece + kround - 1) / kround;
-    const uint64_t nrounds = max_pieces * rpp;
-    const bool rounds = has_res && (unpart_rounds() & 1) && s.rounds + nrounds <= w.rt_rounds;
-    pa.rt = rounds ? w.runtab + s.rounds * (2 * kFine) : nullptr;
-    pa.ptab = w.ptab + size_t(r) * 2 * (kMaxCoarse + 1);
-    pa.rpp = rpp;
-    {
-        ProfScope ps(a.prof, LMR_STAGE_FINE_SCATTER, st, a.n);
-        const unsigned fgrid = unsigned(std::min<uint64_t>(max_pieces, uint64_t(fine_blocks_cap())));
-        dispatch_vb_rpt<2>(vb, piece_fine_rpt(vb), [&](auto vbt, auto rpt) {
-            constexpr int VBc = decltype(vbt)::value, RP = decltype(rpt)::value;
-            hipLaunchKernelGGL((k_fine_piece<VBc, RP>), dim3(fgrid), dim3(1024), 0, st, pa);
-        });
-        e = hipGetLastError();
-    }
-    if (e != hipSuccess) return e;
-    s.reg[r] = StageRegion{uint64_t(R), a.n, a.results, a.ok, a.op, a.ret, a.cmp_bits, a.eps_bits,
-                           uint32_t(s.rounds), kround, rounds ? uint32_t(nrounds) : 0u,
-                           uint32_t(s.crounds), crounds ? uint32_t(ncr) : 0u, rpb, kcround, q.chunk};
-    if (rounds) s.rounds += nrounds;
-    if (crounds) s.crounds += ncr;
+    s.reg[r] = StageRegion{s.staged, a.n, a.results, a.ok, a.op, a.ret, a.cmp_bits, a.eps_bits};
+    s.pend[r] = PendingRegion{a, index_size};
     s.nreg = r + 1;
     s.staged += a.n;
+    return hipSuccess;
+}
+
+// the regions [s.parted, s.nreg): count, coarse and fine passes, fused over groups of up to kFuse
+// regions of one index width whose count rows fit the workspace
+hipError_t launch_stage_partition(const TiledWs& w, StageSession& s, hipStream_t st) {
+    const int dtype = s.dtype, vb = dtype_bytes(dtype);
+    const int shift = tile_shift_for(dtype);
+    while (s.parted < s.nreg) {
+        const ApplyArgs& a0 = s.pend[s.parted].a;
+        const int iw = s.pend[s.parted].iw;
+        const uint32_t T = uint32_t((a0.shard_len + (uint64_t(1) << shift) - 1) >> shift);
+        const uint32_t C = (T + kFine - 1) / kFine;
+        uint32_t kcround = 0, kround = 0;
+        dispatch_vb_rpt<4>(vb, coarse_rpt(vb), [&](auto, auto rpt) { kcround = uint32_t(decltype(rpt)::value) * 1024; });
+        dispatch_vb_rpt<2>(vb, piece_fine_rpt(vb), [&](auto, auto rpt) { kround = uint32_t(decltype(rpt)::value) * 1024; });
+        const uint32_t rpp = (kPiece + kround - 1) / kround;
+        CountTable ct{};
+        CoarseTable cs{};
+        FineTable ft{};
+        uint64_t rows = 0;                                  // count rows of the group so far
+        uint32_t cb = 0, gb = 0, fb = 0;
+        uint64_t n_all = 0;
+        int r = s.parted;
+        for (; r < s.nreg && r - s.parted < kFuse && s.pend[r].iw == iw; r++) {
+            const ApplyArgs& a = s.pend[r].a;
+            StageRegion& g = s.reg[r];
+            const bool has_res = a.ret != LMR_RET_NONE;
+            uint64_t G = (a.n + 65535) / 65536;
+            if (G > uint64_t(bin_blocks_cap(vb))) G = bin_blocks_cap(vb);
+            if (G < 1) G = 1;
+            // count blocks per producer block: one 1024-thread block per CU leaves a lone
+            // region's read-only count pass at half occupancy (LMR_CCOUNT_SPLIT)
+            const uint64_t csub = std::max<uint64_t>(1, std::min<uint64_t>(ccount_split(), uint64_t(kMaxBinBlocks) / G));
+            const uint64_t GS = G * csub;
+            if (r > s.parted && ((rows + GS) * T > uint64_t(kMaxTiles) * kMaxBinBlocks ||
+                                 (rows + GS) * C > uint64_t(kMaxCoarse) * kMaxBinBlocks))
+                break;                                      // the next group takes it
+            const uint64_t chunk = (a.n + G - 1) / G;
+            const uint32_t R = uint32_t(g.base);
+            const uint32_t k = uint32_t(r - s.parted);
+            uint32_t* coarse_off = w.coarse_off + rows * C;
+            uint32_t* trows = w.counts + rows * T;
+            uint32_t* ptab = w.ptab + size_t(r) * 2 * (kMaxCoarse + 1);
+            uint32_t* bstart = ptab + C + 1;                // the piece table's bucket starts
+            uint32_t* ttot = w.rtot + size_t(r) * kMaxTiles;
+            uint32_t* tfill = w.rfill + size_t(r) * kMaxTiles;
+            ct.r[k] = CountRegion{a.idx, a.idx_stride, a.n, chunk, coarse_off, trows, uint32_t(G), uint32_t(csub), cb};
+            cb += uint32_t(GS);
+            // coarse run tables for the round-wise second un-partition gather
+            const uint32_t rpb = uint32_t((chunk + kcround - 1) / kcround);
+            const uint64_t ncr = G * rpb;
+            const bool crounds = has_res && (unpart_rounds() & (vb == 8 ? 4 : 2)) && s.crounds + ncr <= w.crt_rounds;
+            cs.r[k] = CoarseRegion{a.idx, a.idx_stride, a.val, a.val_stride, a.n, chunk, coarse_off, bstart,
+                                   w.sinfo + kStageInb + r, trows, ttot, tfill, w.tmp_idx + R,
+                                   a.val ? w.tmp_val + uint64_t(R) * vb : nullptr, has_res ? w.qpos + R : nullptr,
+                                   crounds ? w.crtab + s.crounds * (2 * kMaxCoarse) : nullptr, uint32_t(G),
+                                   uint32_t(csub), rpb, gb};
+            gb += uint32_t(G);
+            // run tables for the round-wise first gather: rpp rounds per piece
+            const uint64_t max_pieces = (a.n + kPiece - 1) / kPiece + C;
+            const uint64_t nrounds = max_pieces * rpp;
+            const bool rounds = has_res && (unpart_rounds() & 1) && s.rounds + nrounds <= w.rt_rounds;
+            PieceArgs pa;
+            pa.tmp_idx = w.tmp_idx + R; pa.tmp_val = cs.r[k].tmp_val; pa.scalar_bits = a.val_bits;
+            pa.tile_shift = shift; pa.num_tiles = T; pa.C = C; pa.bstart = bstart;
+            pa.bin_lidx = w.bin_lidx; pa.bin_val = w.bin_val;
+            pa.rpos = has_res ? w.rpos + R : nullptr; pa.R = R;
+            pa.ts = w.rts + uint64_t(r) * (kMaxTiles + 1); pa.ttot = ttot; pa.tfill = tfill;
+            pa.rt = rounds ? w.runtab + s.rounds * (2 * kFine) : nullptr;
+            pa.ptab = ptab;
+            pa.rpp = rpp;
+            const uint32_t fgrid = uint32_t(std::min<uint64_t>(max_pieces, uint64_t(fine_blocks_cap())));
+            ft.r[k] = FineRegion{pa, fb, fgrid};
+            fb += fgrid;
+            g.round_base = uint32_t(s.rounds);
+            g.kround = kround;
+            g.nrounds = rounds ? uint32_t(nrounds) : 0u;
+            g.cround_base = uint32_t(s.crounds);
+            g.ncrounds = crounds ? uint32_t(ncr) : 0u;
+            g.rpb = rpb;
+            g.kcround = kcround;
+            g.chunk = chunk;
+            if (rounds) s.rounds += nrounds;
+            if (crounds) s.crounds += ncr;
+            rows += GS;
+            n_all += a.n;
+        }
+        const uint32_t nr = uint32_t(r - s.parted);
+        ct.nr = cs.nr = ft.nr = nr;
+        ct.num_tiles = cs.num_tiles = T;
+        ct.C = cs.C = C;
+        ct.tile_shift = cs.tile_shift = shift;
+        ct.shard_len = cs.shard_len = a0.shard_len;
+        ct.err = cs.err = a0.err;
+        hipError_t e;
+        {
+            ProfScope ps(a0.prof, LMR_STAGE_BIN_COUNT, st, n_all);
+            e = dispatch_iw(iw, [&](auto iwt) {
+                constexpr int IW = decltype(iwt)::value;
+                hipLaunchKernelGGL((k_ccount_stage<IW>), dim3(cb), dim3(1024), size_t(T) * 4, st, ct);
+                return hipGetLastError();
+            });
+        }
+        if (e != hipSuccess) return e;
+        {
+            ProfScope ps(a0.prof, LMR_STAGE_BIN_SCATTER, st, n_all);
+            e = dispatch_iw(iw, [&](auto iwt) {
+                constexpr int IW = decltype(iwt)::value;
+                dispatch_vb_rpt<4>(vb, coarse_rpt(vb), [&](auto vbt, auto rpt) {
+                    constexpr int VBc = decltype(vbt)::value, RP = decltype(rpt)::value;
+                    hipLaunchKernelGGL((k_coarse_stage<IW, VBc, RP>), dim3(gb), dim3(1024), 0, st, cs);
+                });
+                return hipGetLastError();
+            });
+        }
+        if (e != hipSuccess) return e;
+        {
+            ProfScope ps(a0.prof, LMR_STAGE_FINE_SCATTER, st, n_all);
+            dispatch_vb_rpt<2>(vb, piece_fine_rpt(vb), [&](auto vbt, auto rpt) {
+                constexpr int VBc = decltype(vbt)::value, RP = decltype(rpt)::value;
+                hipLaunchKernelGGL((k_fine_stage<VBc, RP>), dim3(fb), dim3(1024), 0, st, ft);
+            });
+            e = hipGetLastError();
+        }
+        if (e != hipSuccess) return e;
+        s.parted = r;
+    }
     return hipSuccess;
 }
 
 hipError_t launch_stage_finish(const TiledWs& w, StageSession& s, hipStream_t st) {
     if (s.nreg == 0) return hipSuccess;
     if (s.free) return stage_finish_free(w, s, st);
+    {
+        const hipError_t ep = launch_stage_partition(w, s, st);
+        if (ep != hipSuccess) {
+            s.nreg = s.parted = 0;
+            s.staged = s.rounds = s.crounds = 0;
+            return ep;
+        }
+    }
     // the regions' op: every region's, or per region (mixed: op phases in staging order)
     ApplyArgs a = s.a;
     a.op = s.reg[0].op; a.ret = s.reg[0].ret; a.cmp_bits = s.reg[0].cmp_bits; a.eps_bits = s.reg[0].eps_bits;
@@ -2335,6 +2477,7 @@ hipError_t launch_stage_finish(const TiledWs& w, StageSession& s, hipStream_t st
         if (e == hipSuccess && t2.nr) e = launch_unpartition_multi(vb, t2, st);
     }
     s.nreg = 0;
+    s.parted = 0;
     s.staged = 0;
     s.rounds = 0;
     s.crounds = 0;

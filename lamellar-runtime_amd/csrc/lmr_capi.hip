@@ -755,6 +755,14 @@ lmr_status_t lmr_stage_op(lmr_ctx_t* ctx, uint32_t op, uint64_t cmp_bits, uint64
     return LMR_OK;
 }
 
+lmr_status_t lmr_stage_flush(lmr_ctx_t* ctx, lmr_stream_t stream) {
+    if (!ctx || !ctx->stage || !ctx->stage->open) return LMR_E_INVALID;
+    StageSession& ss = ctx->stage->s;
+    if (ss.free || ss.parted == ss.nreg) return LMR_OK;
+    return hip_status(launch_stage_partition(carve_tiled_ws(ctx->ws, ctx->rec_cap), ss,
+                                             reinterpret_cast<hipStream_t>(stream)));
+}
+
 lmr_status_t lmr_stage_finish(lmr_ctx_t* ctx, lmr_stream_t stream) {
     if (!ctx || !ctx->stage || !ctx->stage->open) return LMR_E_INVALID;
     StageState* S = ctx->stage;

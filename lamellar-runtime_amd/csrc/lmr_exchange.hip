@@ -734,6 +734,8 @@ lmr_status_t lmr_batch_exchange(lmr_ctx_t* ctx, const lmr_transport_t* tp, const
             ro += tot;
             p = e;
         }
+        // this chunk's streams partitioned now (fused), before its receive buffers are reused
+        if ((st = lmr_stage_flush(ctx, sa)) != LMR_OK) return st;
         if (hipEventRecord(x->ev_recv_free[b], x->sa) != hipSuccess) return LMR_E_HIP;
         x->recv_used[b] = true;
         chunks.push_back(std::move(cr));

@@ -14,18 +14,59 @@
 // so piece i+1's upload and piece i-1's result download overlap piece i's
 // apply; PCIe (full duplex) is the bound. Registering the host buffer
 // (lmr_host_register = hipHostRegister of the lamellae heap) lets the DMA
-// engines read it in place, without a bounce through pageable staging.
+// engines read it in place.
+//
+// The library DMAs only between the device and host memory it knows is page-locked: ranges
+// registered through lmr_host_register (kept in a registry) and its own pinned bounce buffers.
+// Records in pageable memory are copied by the host into a pinned slot before their upload;
+// results / Ok flags bound for pageable memory land in a pinned slot and the host copies them
+// out (the call then returns once they are written). In round 3 the Ok flags of
+// compare_exchange went by an asynchronous copy into a pageable array next to a registered one,
+// leaving the runtime to pin pageable memory on the fly beside our registrations; the next
+// pageable host-to-device copy of the process faulted twice. tools/hostreg_probe.cpp (run on
+// the GPU box, profiles/r4/hostreg_probe.txt) showed that the runtime keeps no mapping of an
+// unregistered range (scenarios A-C, F, G), so the "stale registration" reading of those
+// faults was wrong; it also showed that hipHostUnregister with a pointer inside a registered
+// range aborts the process (E), which the registry now refuses with LMR_E_INVALID.
 #include "lmr_internal.hpp"
 #include "../../include/lamellar_gpu_ops.h"
 #include <stdlib.h>
+#include <string.h>
+#include <iterator>
+#include <map>
+#include <mutex>
 
 namespace lmr {
+
+// ranges registered through lmr_host_register: start -> end (bytes)
+std::mutex& reg_mu() {
+    static std::mutex m;
+    return m;
+}
+std::map<uintptr_t, uintptr_t>& regs() {
+    static std::map<uintptr_t, uintptr_t> r;
+    return r;
+}
+// true when [p, p + bytes) lies inside one registered range
+bool host_range_registered(const void* p, uint64_t bytes) {
+    if (!p || bytes == 0) return false;
+    const uintptr_t lo = reinterpret_cast<uintptr_t>(p), hi = lo + bytes;
+    std::lock_guard<std::mutex> g(reg_mu());
+    auto it = regs().upper_bound(lo);
+    if (it == regs().begin()) return false;
+    --it;
+    return it->first <= lo && hi <= it->second;
+}
 
 struct HostStage {
     hipStream_t h2d = nullptr, d2h = nullptr;
     uint8_t* d_rec[2] = {nullptr, nullptr};
     uint8_t* d_res[2] = {nullptr, nullptr};
     uint8_t* d_ok[2] = {nullptr, nullptr};
+    // pinned bounce slots for pageable host buffers (made on first use)
+    uint8_t* h_rec[2] = {nullptr, nullptr};
+    uint8_t* h_res[2] = {nullptr, nullptr};
+    uint8_t* h_ok[2] = {nullptr, nullptr};
     hipEvent_t copied[2] = {}, applied[2] = {}, drained[2] = {};
     uint64_t piece_recs = 0;
     uint64_t rec_bytes_cap = 0;   // bytes per record slot capacity (largest record size supported: 16)
@@ -39,6 +80,9 @@ void host_stage_free(HostStage* h) {
         if (h->d_rec[b]) (void)hipFree(h->d_rec[b]);
         if (h->d_res[b]) (void)hipFree(h->d_res[b]);
         if (h->d_ok[b]) (void)hipFree(h->d_ok[b]);
+        if (h->h_rec[b]) (void)hipHostFree(h->h_rec[b]);
+        if (h->h_res[b]) (void)hipHostFree(h->h_res[b]);
+        if (h->h_ok[b]) (void)hipHostFree(h->h_ok[b]);
         if (h->copied[b]) (void)hipEventDestroy(h->copied[b]);
         if (h->applied[b]) (void)hipEventDestroy(h->applied[b]);
         if (h->drained[b]) (void)hipEventDestroy(h->drained[b]);
@@ -77,6 +121,16 @@ static hipError_t host_stage_get(lmr_ctx* ctx, HostStage** out) {
     return hipSuccess;
 }
 
+static hipError_t host_bounce_get(HostStage* h) {
+    hipError_t e = hipSuccess;
+    for (int b = 0; b < 2 && e == hipSuccess; b++) {
+        if (!h->h_rec[b]) e = hipHostMalloc(&h->h_rec[b], h->piece_recs * h->rec_bytes_cap, hipHostMallocDefault);
+        if (e == hipSuccess && !h->h_res[b]) e = hipHostMalloc(&h->h_res[b], h->piece_recs * 8, hipHostMallocDefault);
+        if (e == hipSuccess && !h->h_ok[b]) e = hipHostMalloc(&h->h_ok[b], h->piece_recs, hipHostMallocDefault);
+    }
+    return e;
+}
+
 }  // namespace lmr
 
 using namespace lmr;
@@ -85,11 +139,22 @@ extern "C" {
 
 lmr_status_t lmr_host_register(void* ptr, uint64_t bytes) {
     if (!ptr || bytes == 0) return LMR_E_INVALID;
-    return hipHostRegister(ptr, bytes, hipHostRegisterDefault) == hipSuccess ? LMR_OK : LMR_E_HIP;
+    const uintptr_t lo = reinterpret_cast<uintptr_t>(ptr), hi = lo + bytes;
+    std::lock_guard<std::mutex> g(reg_mu());
+    auto it = regs().lower_bound(lo);                    // overlapping an earlier registration: refused
+    if (it != regs().end() && it->first < hi) return LMR_E_INVALID;
+    if (it != regs().begin() && std::prev(it)->second > lo) return LMR_E_INVALID;
+    if (hipHostRegister(ptr, bytes, hipHostRegisterDefault) != hipSuccess) return LMR_E_HIP;
+    regs()[lo] = hi;
+    return LMR_OK;
 }
 
 lmr_status_t lmr_host_unregister(void* ptr) {
     if (!ptr) return LMR_E_INVALID;
+    std::lock_guard<std::mutex> g(reg_mu());
+    auto it = regs().find(reinterpret_cast<uintptr_t>(ptr));
+    if (it == regs().end()) return LMR_E_INVALID;        // not the start of a registration
+    regs().erase(it);
     return hipHostUnregister(ptr) == hipSuccess ? LMR_OK : LMR_E_HIP;
 }
 
@@ -118,14 +183,37 @@ lmr_status_t lmr_apply_mvmi_host(lmr_ctx_t* ctx, const lmr_apply_desc_t* desc, c
     const uint32_t ret = lmr_op_ret_kind(desc->op);
     const bool want_res = h_results && ret != LMR_RET_NONE;
     const bool want_ok = h_ok && ret == LMR_RET_RESULT;
+    // pageable buffers go through the pinned bounce slots
+    const bool rec_pinned = host_range_registered(h_idx_vals, n * rb);
+    const bool res_pinned = !want_res || host_range_registered(h_results, n * eb);
+    const bool ok_pinned = !want_ok || host_range_registered(h_ok, n);
+    if ((!rec_pinned || !res_pinned || !ok_pinned) && host_bounce_get(h) != hipSuccess) return LMR_E_HIP;
     const uint8_t* src = reinterpret_cast<const uint8_t*>(h_idx_vals);
+    // results of a bounced piece are copied out by the host once its download is done
+    struct Out { bool live = false; uint64_t r0 = 0, m = 0; };
+    Out pend[2];
+    auto drain_out = [&](int b) -> lmr_status_t {
+        if (!pend[b].live) return LMR_OK;
+        if (hipEventSynchronize(h->drained[b]) != hipSuccess) return LMR_E_HIP;
+        if (want_res && !res_pinned)
+            memcpy(static_cast<uint8_t*>(h_results) + pend[b].r0 * eb, h->h_res[b], pend[b].m * eb);
+        if (want_ok && !ok_pinned) memcpy(h_ok + pend[b].r0, h->h_ok[b], pend[b].m);
+        pend[b].live = false;
+        return LMR_OK;
+    };
     uint64_t i = 0;
     for (uint64_t r0 = 0; r0 < n; r0 += P, i++) {
         const int b = int(i & 1);
         const uint64_t m = (n - r0 < P) ? n - r0 : P;
         // upload: the slot's previous apply must have consumed its records
         if (hipStreamWaitEvent(h->h2d, h->applied[b], 0) != hipSuccess) return LMR_E_HIP;
-        if (hipMemcpyAsync(h->d_rec[b], src + r0 * rb, m * rb, hipMemcpyHostToDevice, h->h2d) != hipSuccess)
+        const uint8_t* up = src + r0 * rb;
+        if (!rec_pinned) {                             // the bounce slot's previous upload is done
+            if (i >= 2 && hipEventSynchronize(h->copied[b]) != hipSuccess) return LMR_E_HIP;
+            memcpy(h->h_rec[b], up, m * rb);
+            up = h->h_rec[b];
+        }
+        if (hipMemcpyAsync(h->d_rec[b], up, m * rb, hipMemcpyHostToDevice, h->h2d) != hipSuccess)
             return LMR_E_HIP;
         if (hipEventRecord(h->copied[b], h->h2d) != hipSuccess) return LMR_E_HIP;
         // apply on the caller's stream (after the upload and the slot's previous download)
@@ -135,16 +223,23 @@ lmr_status_t lmr_apply_mvmi_host(lmr_ctx_t* ctx, const lmr_apply_desc_t* desc, c
                                          want_res ? h->d_res[b] : nullptr, want_ok ? h->d_ok[b] : nullptr, stream);
         if (st != LMR_OK) return st;
         if (hipEventRecord(h->applied[b], s) != hipSuccess) return LMR_E_HIP;
-        // download of the returned values
+        // download of the returned values (into the caller's registered memory or a bounce slot)
         if (want_res || want_ok) {
+            if ((st = drain_out(b)) != LMR_OK) return st;   // the slot's previous results are out
             if (hipStreamWaitEvent(h->d2h, h->applied[b], 0) != hipSuccess) return LMR_E_HIP;
-            if (want_res && hipMemcpyAsync(reinterpret_cast<uint8_t*>(h_results) + r0 * eb, h->d_res[b], m * eb,
-                                           hipMemcpyDeviceToHost, h->d2h) != hipSuccess)
+            uint8_t* res_dst = res_pinned ? static_cast<uint8_t*>(h_results) + r0 * eb : h->h_res[b];
+            uint8_t* ok_dst = ok_pinned ? h_ok + r0 : h->h_ok[b];
+            if (want_res && hipMemcpyAsync(res_dst, h->d_res[b], m * eb, hipMemcpyDeviceToHost, h->d2h) != hipSuccess)
                 return LMR_E_HIP;
-            if (want_ok && hipMemcpyAsync(h_ok + r0, h->d_ok[b], m, hipMemcpyDeviceToHost, h->d2h) != hipSuccess)
+            if (want_ok && hipMemcpyAsync(ok_dst, h->d_ok[b], m, hipMemcpyDeviceToHost, h->d2h) != hipSuccess)
                 return LMR_E_HIP;
             if (hipEventRecord(h->drained[b], h->d2h) != hipSuccess) return LMR_E_HIP;
+            pend[b] = Out{!(res_pinned && ok_pinned), r0, m};
         }
+    }
+    for (int b = 0; b < 2; b++) {
+        const lmr_status_t st = drain_out(b);
+        if (st != LMR_OK) return st;
     }
     // completion on the caller's stream covers the downloads too
     for (int b = 0; b < 2; b++)

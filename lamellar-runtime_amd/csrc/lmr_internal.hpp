@@ -86,6 +86,8 @@ struct TiledWs {
     uint64_t rt_rounds;    // rounds runtab holds
     uint32_t* crtab;       // staged apply: per coarse round, per bucket (temp run start, length)
     uint64_t crt_rounds;   // rounds crtab holds
+    uint32_t* rtot;        // staged apply: [kMaxRegions][kMaxTiles] each region's tile totals
+    uint32_t* rfill;       // staged apply: [kMaxRegions][kMaxTiles] each region's fine-pass tile fills
     uint64_t cap;          // records of one tiled piece (bin arrays, position maps)
     uint64_t tmp_cap;      // records the temp arrays (tmp_idx / tmp_val) hold, > cap
 };
@@ -175,10 +177,15 @@ struct StageRegion {
     uint32_t kcround = 0;      // the coarse pass's LDS round (records)
     uint64_t chunk = 0;        // records per producer block
 };
+struct PendingRegion {
+    ApplyArgs a;         // the region's records (caller buffers, valid until the region is partitioned)
+    int iw;
+};
 struct StageSession {
     ApplyArgs a;         // op / kind / shard / ret of the session's current op (record fields unused)
     int dtype = 0;
     int nreg = 0;
+    int parted = 0;      // regions [0, parted) are partitioned; [parted, nreg) wait in pend[]
     uint64_t staged = 0; // workspace slots in use
     uint64_t rounds = 0; // runtab rounds in use
     uint64_t crounds = 0;  // crtab rounds in use
@@ -186,15 +193,19 @@ struct StageSession {
     bool free_armed = false;
     bool switched = false;  // the op changed with records staged (lmr_stage_op): later phases counted
     StageRegion reg[kMaxRegions];
+    PendingRegion pend[kMaxRegions];
 };
 // true when a region staged under a different op / operands than `a`'s is pending
 bool stage_pending_other_op(const StageSession& s, const ApplyArgs& a);
 // true when a staged session of this op takes the count-free regions
 bool stage_free_applies(int dtype, int op, int ret, uint64_t shard_len, uint64_t cap);
-// partition the records of `a` into the next region (caller checks capacity:
-// s.staged + a.n <= workspace capacity, a.n <= kStageMaxRegion, s.nreg < kMaxRegions)
+// add the records of `a` as the next region (caller checks capacity: s.staged + a.n <= workspace
+// capacity, a.n <= kStageMaxRegion, s.nreg < kMaxRegions). Counted regions are only recorded:
+// launch_stage_partition partitions every pending region at once (the caller's buffers stay valid
+// until then); count-free regions are partitioned at once.
 hipError_t launch_stage_region(int dtype, int index_size, const ApplyArgs& a, const TiledWs& w,
                                StageSession& s, hipStream_t st);
+hipError_t launch_stage_partition(const TiledWs& w, StageSession& s, hipStream_t st);
 // apply every staged region in one tile sweep, results back to each region's caller
 hipError_t launch_stage_finish(const TiledWs& w, StageSession& s, hipStream_t st);
 

@@ -65,6 +65,8 @@ class DeviceKernels:
         # the open deferred session of asynchronous batches (defer_soa): [shard key, (op, cmp, eps),
         # tensors its kernels still write or read]; applied by flush()
         self._deferred = None
+        # record tensors of the open lmr_stage_* session, held until it is partitioned
+        self._staged_refs = []
 
     # ---------------------------------------------------------------- infra
     def stream(self):
@@ -202,8 +204,11 @@ class DeviceKernels:
         check(self.lib.lmr_stage_begin(self.ctx, byref(d)), "lmr_stage_begin")
 
     def stage_soa(self, idx, iw, vals, scalar_bits, n, results=None, ok=None):
-        """Partition n records (lmr_apply_soa's arguments) into the session; their
-        results / Ok flags are valid once stage_finish has run on this stream."""
+        """Stage n records (lmr_apply_soa's arguments) into the session; their
+        results / Ok flags are valid once stage_finish has run on this stream. The
+        records are partitioned at the next stage_flush / stage_finish: the tensors are
+        held until then."""
+        self._staged_refs.append((idx, vals))
         sv = c_uint64(int(scalar_bits) & 0xFFFFFFFFFFFFFFFF)
         st = self.lib.lmr_stage_soa(self.ctx, _p(idx), int(iw), _p(vals),
                                     None if vals is not None else ctypes.cast(byref(sv), c_void_p),
@@ -216,9 +221,15 @@ class DeviceKernels:
         check(self.lib.lmr_stage_op(self.ctx, int(op), c_uint64(int(cmp_bits) & 0xFFFFFFFFFFFFFFFF),
                                     c_uint64(int(eps_bits) & 0xFFFFFFFFFFFFFFFF), self.stream()), "lmr_stage_op")
 
+    def stage_flush(self):
+        """Partition the staged records now (lmr_stage_flush)."""
+        check(self.lib.lmr_stage_flush(self.ctx, self.stream()), "lmr_stage_flush")
+        self._staged_refs = []
+
     def stage_finish(self):
         """Apply every staged record in one sweep of the shard and close the session."""
         check(self.lib.lmr_stage_finish(self.ctx, self.stream()), "lmr_stage_finish")
+        self._staged_refs = []
 
     def apply_mvmi(self, shard, shard_len, kind, dt, op, idx_vals_bytes, nbytes, iw,
                    results=None, ok=None, cmp_bits=0, eps_bits=0):

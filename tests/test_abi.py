@@ -130,3 +130,14 @@ def test_pack_oracle_buffers_respect_am_threshold(orc):
     L1 = orc.layout_new(1 << 20, 1, 0, 0)
     st, ams = orc.pack(L1, 3, np.uint64, g, None, 4, threshold=100000, threads=1)
     assert max(a[1].size for a in ams) == 25000 * 4      # SVMI: 25000 u32 indices (:488-489)
+
+
+def test_host_unregister_refuses_unknown_ranges(capi):
+    """lmr_host_unregister only takes the start of a range lmr_host_register registered (a
+    pointer inside a registered range makes hipHostUnregister abort the process,
+    tools/hostreg_probe.cpp scenario E): anything else is LMR_E_INVALID, decided by the
+    library's registry before any runtime call (no GPU needed)."""
+    buf = np.zeros(4096, np.uint8)
+    assert capi.lmr_host_unregister(ctypes.c_void_p(buf.ctypes.data)) == 1
+    assert capi.lmr_host_unregister(ctypes.c_void_p(buf.ctypes.data + 64)) == 1
+    assert capi.lmr_host_unregister(None) == 1

@@ -3,7 +3,9 @@ buffer in host memory -> pieces uploaded / applied / results downloaded on
 three streams. Checked against the oracle's apply of the same bytes
 (bit-exact for integers), over several pieces (LMR_HOST_PIECE_RECORDS is set
 small here so both the tiled (>= 2^16 records) and the direct last piece run),
-with registered and pageable host buffers."""
+with registered and pageable host buffers (pageable ones go through the
+library's pinned bounce slots), and registered ranges unregistered and freed
+right after use, their memory reused by the next allocations."""
 import os
 
 import numpy as np
@@ -19,13 +21,6 @@ pytestmark = pytest.mark.gpu
 
 def to_dev(a):
     return torch.from_numpy(np.ascontiguousarray(a).view(np.uint8).copy()).cuda()
-
-
-# Host ranges that were registered stay allocated for the rest of the process: after
-# hipHostUnregister the runtime may still map the range, and a later pageable copy from memory
-# that reuses those addresses (a freed numpy buffer handed out again) then faulted on the device
-# ("illegal memory access" at the next test's first host-to-device copy, twice in round 3).
-_KEEP = []
 
 
 @pytest.mark.parametrize("dt,op,register", [("u64", ADD, True), ("u64", FETCH_ADD, True), ("u32", XOR, False),
@@ -55,10 +50,8 @@ def test_apply_mvmi_host_matches_oracle(world, orc, lam, dt, op, register):
     h_ok = np.zeros(n, dtype=np.uint8) if rk == 2 else None
     if register:
         k.host_register(buf)
-        _KEEP.append(buf)
         if h_res is not None:
             k.host_register(h_res)
-            _KEEP.append(h_res)
     try:
         cb = dt_obj.to_bits(cur) if cur is not None else 0
         k.apply_mvmi_host(d_shard, shard_len, kind, dt_obj, op, buf, iw, h_res, h_ok, cb, 0)
@@ -90,3 +83,49 @@ def test_apply_mvmi_host_collisions_sum(world, orc, lam):
     d_shard = torch.zeros(shard_len, dtype=torch.int64, device="cuda")
     k.apply_mvmi_host(d_shard, shard_len, 1, lam.dtype_of("u64"), ADD, buf, 2)
     assert np.array_equal(d_shard.cpu().numpy().view(np.uint64), ref)
+
+
+def test_registered_ranges_freed_and_reused(world, orc, lam):
+    """Registered op buffers and result arrays that share pages (slices of one host arena),
+    unregistered and freed right after each apply; the freed memory is reused by the next
+    arena and by pageable host-to-device copies in between. compare_exchange's Ok flags go to
+    a pageable array (the library's bounce slot) beside the registered results. Every round
+    is bit-exact against the oracle."""
+    k = world.team().kernels
+    dt = "u32"
+    shard_len, n = 300000, 2 * 65536 + 777
+    rb, vo = orc.record_bytes(4, CODE[dt]), orc.record_val_offset(4, CODE[dt])
+    for rnd in range(4):
+        rng = np.random.default_rng(900 + rnd)
+        shard0 = rand_elems(dt, shard_len, rng, CAS)
+        idx = rng.permutation(shard_len)[:n].astype(np.uint64)
+        vals = rand_vals(dt, n, rng, CAS)
+        cur, _, shard0 = cas_operands(dt, shard0, vals, rng)
+        recs = to_aos(idx, vals, 4, dt, rb, vo)
+        # one arena: records, then results 16 bytes later (the two ranges share a page)
+        arena = np.zeros(recs.nbytes + 16 + n * 4 + 64, np.uint8)
+        buf = arena[:recs.nbytes]
+        buf[:] = recs
+        h_res = arena[recs.nbytes + 16:recs.nbytes + 16 + n * 4].view(np.uint32)
+        h_ok = np.zeros(n, np.uint8)                        # pageable
+        ref = shard0.copy()
+        st_o, res_o, ok_o = orc.apply_mvmi(ref, 1, CODE[dt], NP[dt], CAS, recs, 4, cur, None)
+        assert st_o == 0
+        d_shard = to_dev(shard0)
+        k.host_register(buf)
+        k.host_register(h_res)
+        try:
+            k.apply_mvmi_host(d_shard, shard_len, 1, lam.dtype_of(dt), CAS, buf, 4, h_res, h_ok,
+                              lam.dtype_of(dt).to_bits(cur), 0)
+        finally:
+            k.host_unregister(buf)
+            k.host_unregister(h_res)
+        assert k.errors() == 0
+        assert bits_equal(d_shard.cpu().numpy().view(NP[dt])[:shard_len], ref)
+        assert bits_equal(h_res.copy(), res_o)
+        assert np.array_equal(h_ok, ok_o)
+        del buf, h_res, arena
+        # pageable copies of fresh allocations (the freed arena's memory is handed out again)
+        for _ in range(3):
+            x = rng.integers(0, 2**31, n, dtype=np.int64)
+            assert np.array_equal(torch.from_numpy(x).cuda().cpu().numpy(), x)
