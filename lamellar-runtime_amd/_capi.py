@@ -196,7 +196,10 @@ def lib():
             l = ctypes.CDLL(LIB_PATH)
         except OSError as e:  # pragma: no cover - environment specific
             raise LamellarLibraryError(f"failed to load {LIB_PATH}: {e}") from e
+        side = "LAMELLAR_GPU_OPS_LIB" in os.environ      # an earlier build for a same-box A/B
         for name, (res, args) in SIGNATURES.items():
+            if side and not hasattr(l, name):
+                continue                                   # (entry points added since that build)
             fn = getattr(l, name)
             fn.restype = res
             fn.argtypes = args

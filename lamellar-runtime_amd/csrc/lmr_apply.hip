@@ -265,8 +265,9 @@ struct PartArgs {
     uint32_t* trows;              // staged regions: [G * csub][num_tiles] per-count-block tile counts (k_ccount)
     uint32_t* ttot;               // staged regions: [num_tiles] tile totals (k_coarse_scatter folds the rows)
     uint32_t* tfill;              // staged regions: [num_tiles] fine-pass fill counters (zeroed by k_coarse_scatter)
-    // staged returning regions, round-wise second un-partition gather (crt non-null): qpos[k] is
-    // record k's position in its coarse round's LDS staging, and each round's bucket runs are
+    // staged returning regions, round-wise second un-partition gather (crt non-null): qpos holds
+    // as u16 record k's position in its coarse round's LDS staging (0xFFFF: out of bounds; the u16
+    // array starts where the region's u32 map would), and each round's bucket runs are
     // recorded, crt[g * rpb + round][c] = {temp start, length}
     uint32_t* crt;
     uint32_t rpb;                 // rounds per producer block
@@ -356,6 +357,7 @@ template <int IW, int VB, int RPT>
 __device__ __forceinline__ void coarse_scatter_body(const PartArgs& p, const uint32_t g) {
     using V = typename idx_t<VB>::I;
     constexpr uint32_t kRound = RPT * 1024;
+    static_assert(kRound < 0xFFFFu, "round staging positions are u16");
     __shared__ uint32_t hist[kMaxCoarse], base[kMaxCoarse], cursor[kMaxCoarse], tot;
     __shared__ uint32_t s_idx[kRound];
     __shared__ V s_val[kRound];
@@ -421,13 +423,19 @@ __device__ __forceinline__ void coarse_scatter_body(const PartArgs& p, const uin
         for (int j = 0; j < RPT; j++) {
             const uint64_t k = r0 + uint64_t(j) * 1024 + threadIdx.x;
             if (!m_ok[j]) {
-                if (p.qpos && k < hi) p.qpos[k] = 0xFFFFFFFFu;
+                if (p.qpos && k < hi) {
+                    if (p.crt) reinterpret_cast<uint16_t*>(p.qpos)[k] = 0xFFFFu;
+                    else p.qpos[k] = 0xFFFFFFFFu;
+                }
                 continue;
             }
             const uint32_t q = base[m_c[j]] + m_rank[j];
             s_idx[q] = uint32_t(m_raw[j]);
             s_val[q] = m_val[j];
-            if (p.qpos) p.qpos[k] = p.crt ? q : cursor[m_c[j]] + m_rank[j];   // coalesced in k
+            if (p.qpos) {                                  // coalesced in k
+                if (p.crt) reinterpret_cast<uint16_t*>(p.qpos)[k] = uint16_t(q);
+                else p.qpos[k] = cursor[m_c[j]] + m_rank[j];
+            }
         }
         if (p.crt && threadIdx.x < kMaxCoarse) {
             uint32_t* rr = p.crt + (uint64_t(g) * p.rpb + (r0 - lo) / kRound) * (2 * kMaxCoarse) + 2 * threadIdx.x;
@@ -629,8 +637,8 @@ __global__ __launch_bounds__(1024) void k_coarse_free(PartArgs p) {
     // 16-B aligned, even chunks): without the one-at-a-time path in the same kernel, no dead
     // path's pending loads make the compiler wait for the prefetch before the write-out
     constexpr bool pairs = PAIRS;
-    // every pair is loaded from an even offset <= kl (the last record's pair): the aligned 16-B
-    // load of a valid 8-B record never leaves its page, and the half past the range is dropped
+    // every pair is loaded from an even offset <= kl (the last record's pair); the host picks
+    // PAIRS only when every block's range holds whole pairs, so no load passes the range's end
     const uint64_t kl = lo < hi ? lo + ((hi - 1 - lo) & ~uint64_t(1)) : lo;
     auto kof = [&](uint64_t r0, int j) -> uint64_t {
         return pairs ? r0 + 2 * (uint64_t(j >> 1) * 1024 + threadIdx.x) + (j & 1) : r0 + uint64_t(j) * 1024 + threadIdx.x;
@@ -1434,8 +1442,10 @@ static hipError_t launch_coarse_free(int index_size, int vb, int frpt, const Par
         constexpr int IW = decltype(iw)::value;
         dispatch_vb_rpt<4>(vb, frpt, [&](auto vbt, auto rpt) {
             constexpr int VBc = decltype(vbt)::value, R = decltype(rpt)::value;
+            // (even chunks and an even n: every block's range is whole pairs, so no 16-B load
+            // reaches past the caller's last record)
             const bool pairs = kCoarsePairs && IW == 8 && VBc == 8 && (R % 2) == 0 && q.idx_stride == 8 && q.val &&
-                               q.val_stride == 8 && (q.chunk % 2) == 0 &&
+                               q.val_stride == 8 && (q.chunk % 2) == 0 && (q.n % 2) == 0 &&
                                ((reinterpret_cast<uintptr_t>(q.idx) | reinterpret_cast<uintptr_t>(q.val)) & 15) == 0;
             if (pairs)
                 hipLaunchKernelGGL((k_coarse_free<IW, VBc, R, (IW == 8 && VBc == 8 && R % 2 == 0)>), dim3(q.G), dim3(1024),
@@ -1718,7 +1728,7 @@ struct PieceArgs {
     uint32_t* ts;               // out: the region's tile starts (absolute binned positions)
     const uint32_t* ttot;       // the region's tile totals (k_coarse_scatter)
     uint32_t* tfill;            // per-tile records placed so far (zeroed by k_coarse_scatter)
-    // round-wise un-partition (rt non-null): rpos[k] is slot k's position in its round's LDS
+    // round-wise un-partition (rt non-null): rpos holds as u16 slot k's position in its round's LDS
     // staging, and each round's tile runs are recorded, rt[round][f] = {binned start, length}
     // (round = piece * rpp + the round within the piece), with the piece table in ptab
     // (pbase[C + 1], bstart[C + 1]): k_unpart_rounds reads each round's runs back whole
@@ -1775,6 +1785,7 @@ template <int VB, int RPT>
 __device__ __forceinline__ void fine_piece_body(const PieceArgs& a, const uint32_t bid, const uint32_t nblk) {
     using V = typename idx_t<VB>::I;
     constexpr uint32_t kRound = RPT * 1024;
+    static_assert(kRound < 0xFFFFu, "round staging positions are u16");
     __shared__ uint32_t hist[kFine], base[kFine], cursor[kFine], tot;
     __shared__ uint32_t s_pb[kMaxCoarse + 1], s_bs[kMaxCoarse + 1], s_np[kMaxCoarse], s_tot;   // piece table
     __shared__ uint16_t s_l[kRound];
@@ -1859,7 +1870,10 @@ __device__ __forceinline__ void fine_piece_body(const PieceArgs& a, const uint32
                 const uint32_t q = base[m_f[j]] + m_rank[j];
                 s_l[q] = uint16_t(m_idx[j] & lmask);
                 s_val[q] = m_val[j];
-                if (a.rpos) a.rpos[k] = a.rt ? q : cursor[m_f[j]] + m_rank[j];
+                if (a.rpos) {
+                    if (a.rt) reinterpret_cast<uint16_t*>(a.rpos)[k] = uint16_t(q);   // u16 map
+                    else a.rpos[k] = cursor[m_f[j]] + m_rank[j];
+                }
             }
             if (a.rt && threadIdx.x < kFine) {
                 uint32_t* rr = a.rt + (uint64_t(pid) * a.rpp + (r0 - L.lo) / kRound) * (2 * kFine) + 2 * threadIdx.x;
@@ -2010,7 +2024,7 @@ __device__ __forceinline__ void runs_to_lds(const uint32_t* s_cur, const uint32_
 struct RoundRegion {
     const uint32_t* rt;         // the region's run tables
     const uint32_t* ptab;       // pbase[C + 1], bstart[C + 1]
-    const uint32_t* lpos;       // slot -> staging position in its round
+    const uint16_t* lpos;       // slot -> staging position in its round (u16)
     const uint8_t* src;         // binned results
     uint8_t* dst;               // results by slot
     const uint8_t* oks;
@@ -2053,7 +2067,7 @@ __global__ __launch_bounds__(1024) void k_unpart_rounds(RoundTable t) {
     __syncthreads();
     V* dst = reinterpret_cast<V*>(g.dst);
     for (uint32_t k = lo + threadIdx.x; k < hi; k += blockDim.x) {
-        const uint32_t q = g.lpos[k];
+        const uint32_t q = g.lpos[k];                     // (u16 map)
         dst[k] = s_v[q];
         if (g.oks) g.okd[k] = s_ok[q];
     }
@@ -2064,7 +2078,7 @@ __global__ __launch_bounds__(1024) void k_unpart_rounds(RoundTable t) {
 // every record of the round takes its value from its staging position (qpos; ~0 = out of bounds).
 struct CRoundRegion {
     const uint32_t* crt;        // the region's coarse run tables
-    const uint32_t* qpos;       // record -> staging position in its round
+    const uint16_t* qpos;       // record -> staging position in its round (u16, 0xFFFF: out of bounds)
     const uint8_t* src;         // results by temp slot
     uint8_t* dst;               // caller's results (arrival order)
     const uint8_t* oks;
@@ -2104,7 +2118,7 @@ __global__ __launch_bounds__(1024) void k_unpart_crounds(CRoundTable t) {
     V* dst = reinterpret_cast<V*>(g.dst);
     for (uint64_t k = lo + threadIdx.x; k < hi; k += blockDim.x) {
         const uint32_t q = g.qpos[k];
-        if (q == 0xFFFFFFFFu) continue;
+        if (q == 0xFFFFu) continue;
         dst[k] = s_v[q];
         if (g.okd) g.okd[k] = s_ok[q];
     }
@@ -2439,7 +2453,8 @@ hipError_t launch_stage_finish(const TiledWs& w, StageSession& s, hipStream_t st
             if (g.nrounds) {
                 const uint32_t C = (T + kFine - 1) / kFine;
                 tr.r[tr.nr++] = RoundRegion{w.runtab + uint64_t(g.round_base) * (2 * kFine),
-                                            w.ptab + size_t(r) * 2 * (kMaxCoarse + 1), w.rpos + g.base, res_bin,
+                                            w.ptab + size_t(r) * 2 * (kMaxCoarse + 1),
+                                            reinterpret_cast<const uint16_t*>(w.rpos + g.base), res_bin,
                                             tmpres + g.base * vb, ok_src, ok_tmp ? ok_tmp + g.base : nullptr, C,
                                             (kPiece + g.kround - 1) / g.kround, rblocks};
                 rblocks += g.nrounds;
@@ -2448,7 +2463,8 @@ hipError_t launch_stage_finish(const TiledWs& w, StageSession& s, hipStream_t st
                 t1.r[t1.nr++] = UnpartRegion{w.rpos + g.base, w.sinfo + kStageInb + r, g.n, 0, res_bin,
                                              tmpres + g.base * vb, ok_src, ok_tmp ? ok_tmp + g.base : nullptr, 0};
             if (g.ncrounds) {
-                tc.r[tc.nr++] = CRoundRegion{w.crtab + uint64_t(g.cround_base) * (2 * kMaxCoarse), w.qpos + g.base,
+                tc.r[tc.nr++] = CRoundRegion{w.crtab + uint64_t(g.cround_base) * (2 * kMaxCoarse),
+                                             reinterpret_cast<const uint16_t*>(w.qpos + g.base),
                                              tmpres + g.base * vb, reinterpret_cast<uint8_t*>(g.results),
                                              want_ok ? ok_tmp + g.base : nullptr, want_ok ? g.ok : nullptr, g.n,
                                              g.chunk, g.rpb, cblocks};

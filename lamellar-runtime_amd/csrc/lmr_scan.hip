@@ -51,6 +51,10 @@ __global__ __launch_bounds__(1024) void k_scan_lookback(uint32_t* __restrict__ d
     if (threadIdx.x == 0) s_tile = atomicAdd(&ctl[0], 1u);
     __syncthreads();
     const uint32_t tile = s_tile;
+    // a ticket past the last tile means the scratch was not zero at launch (two scans sharing
+    // one context's scratch from different streams, which the C ABI rules out): write nothing
+    // outside the scratch sized for this m
+    if (tile >= nb) return;
     const uint64_t base = uint64_t(tile) * kScanItems + uint64_t(threadIdx.x) * 4;
     uint32_t v[4];
     uint32_t sum = 0;

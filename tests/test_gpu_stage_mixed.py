@@ -210,3 +210,42 @@ def test_small_stream_after_other_op_phase(world, lam):
     ref = np.full(1000, 7, np.uint32)
     np.add.at(ref, i0.astype(np.int64), 1)
     assert np.array_equal(got, ref)
+
+
+def test_fused_partition_groups(world, lam):
+    """Counted regions are partitioned together at the finish: one count / coarse / fine
+    launch per group of up to 8 pending regions of one index width (u64 global and u32
+    local indices here, 11 counted phases -> groups of 2, 3 and 6 regions: 3 launches per
+    pass), each region with its own count rows, tile totals and tables; the final shard is
+    the serial per-phase replay, bit for bit."""
+    k = world.team().kernels
+    dt = lam.dtype_of("u32")
+    rng = np.random.default_rng(31337)
+    hot = rng.choice(L, 20000, replace=False)
+    s0 = rng.integers(0, 2**32, L, dtype=np.uint64).astype(np.uint32)
+    widths = [8, 8, 4, 4, 4, 8, 8, 8, 8, 8, 8]
+    ops = [XOR] + [ADD if j % 2 == 0 else XOR for j in range(len(widths))]
+    n = N // 2
+    vals = [rng.integers(0, 2**32, n, dtype=np.uint64).astype(np.uint32) for _ in ops]
+    idxs = [_idx(rng, n, hot) for _ in ops]
+    k.reserve(16 * n)
+    shard = to_dev(s0)
+    k.profile(True)
+    k.profile_read(reset=True)
+    try:
+        k.stage_begin(shard, L, 1, dt, ops[0])
+        k.stage_soa(to_dev(idxs[0]), 8, to_dev(vals[0]), 0, n)       # count-free, applied at the switch
+        for j, w in enumerate(widths):
+            k.stage_op(ops[j + 1])
+            i = idxs[j + 1] if w == 8 else idxs[j + 1].astype(np.uint32)
+            k.stage_soa(to_dev(i), w, to_dev(vals[j + 1]), 0, n)
+        k.stage_finish()
+        stages = k.profile_read(reset=True)
+    finally:
+        k.profile(False)
+    assert k.errors() == 0
+    ref = s0.copy()
+    for op, v, i in zip(ops, vals, idxs):
+        ref = _fold(op, ref, i, v)
+    assert np.array_equal(shard.cpu().numpy().view(np.uint32), ref)
+    assert stages["bin_count"][1] == 3 and stages["fine_scatter"][1] == 4, stages   # (+1: the free phase)
