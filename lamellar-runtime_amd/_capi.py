@@ -67,7 +67,7 @@ class lmr_transport_t(Structure):
         ("num_pes", c_uint32),
         ("my_pe", c_uint32),
         ("host_buffers", c_uint32),
-        ("reserved_", c_uint32),
+        ("flags", c_uint32),          # LMR_TRANSPORT_SPLIT_HEADERS = 1
         ("self", c_void_p),
         ("alltoall", ALLTOALL_FN),
         ("alltoallv", ALLTOALLV_FN),

@@ -90,7 +90,9 @@ struct HostBuf {
 // overlaps chunk j's staging.
 struct XState {
     hipStream_t sp = nullptr, sx = nullptr, sa = nullptr;
-    hipEvent_t ev_begin = nullptr, ev_pack_done = nullptr, ev_apply_done = nullptr, ev_x_done = nullptr;
+    hipStream_t sh = nullptr;            // header exchanges of split-header transports
+    hipEvent_t ev_begin = nullptr, ev_pack_done = nullptr, ev_apply_done = nullptr, ev_x_done = nullptr,
+               ev_h_done = nullptr;
     hipEvent_t ev_hdr[2] = {nullptr, nullptr}, ev_x[2] = {nullptr, nullptr};
     hipEvent_t ev_recv_free[2] = {nullptr, nullptr}, ev_send_free[2] = {nullptr, nullptr},
                ev_packed[2] = {nullptr, nullptr};
@@ -105,7 +107,7 @@ struct XState {
     // waits for the three internal streams (not the whole device: other work may share it)
     hipError_t drain() const {
         hipError_t e = hipSuccess, r;
-        for (hipStream_t s : {sp, sx, sa})
+        for (hipStream_t s : {sp, sx, sa, sh})
             if (s && (r = hipStreamSynchronize(s)) != hipSuccess && e == hipSuccess) e = r;
         return e;
     }
@@ -125,13 +127,15 @@ void xstate_free(XState* x) {
     x->h_hdr.release();
     x->h_send.release();
     x->h_recv.release();
-    for (hipEvent_t e : {x->ev_begin, x->ev_pack_done, x->ev_apply_done, x->ev_x_done, x->ev_hdr[0], x->ev_hdr[1],
+    for (hipEvent_t e : {x->ev_begin, x->ev_pack_done, x->ev_apply_done, x->ev_x_done, x->ev_h_done, x->ev_hdr[0],
+                         x->ev_hdr[1],
                          x->ev_x[0], x->ev_x[1], x->ev_recv_free[0], x->ev_recv_free[1], x->ev_send_free[0],
                          x->ev_send_free[1], x->ev_packed[0], x->ev_packed[1]})
         if (e) (void)hipEventDestroy(e);
     if (x->sp) (void)hipStreamDestroy(x->sp);
     if (x->sx) (void)hipStreamDestroy(x->sx);
     if (x->sa) (void)hipStreamDestroy(x->sa);
+    if (x->sh) (void)hipStreamDestroy(x->sh);
     delete x;
 }
 
@@ -140,7 +144,9 @@ static hipError_t xstate_init(XState* x) {
     hipError_t e = hipStreamCreateWithFlags(&x->sp, hipStreamNonBlocking);
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&x->sx, hipStreamNonBlocking);
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&x->sa, hipStreamNonBlocking);
-    for (hipEvent_t* ev : {&x->ev_begin, &x->ev_pack_done, &x->ev_apply_done, &x->ev_x_done, &x->ev_hdr[0],
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&x->sh, hipStreamNonBlocking);
+    for (hipEvent_t* ev : {&x->ev_begin, &x->ev_pack_done, &x->ev_apply_done, &x->ev_x_done, &x->ev_h_done,
+                           &x->ev_hdr[0],
                            &x->ev_hdr[1], &x->ev_x[0], &x->ev_x[1], &x->ev_recv_free[0], &x->ev_recv_free[1],
                            &x->ev_send_free[0], &x->ev_send_free[1], &x->ev_packed[0], &x->ev_packed[1]})
         if (e == hipSuccess) e = hipEventCreateWithFlags(ev, hipEventDisableTiming);
@@ -181,7 +187,9 @@ lmr_status_t tp_alltoall(const lmr_transport_t* tp, XState* x, const void* send,
         return LMR_E_HIP;
     lmr_status_t st = tp->alltoall(tp->self, x->h_send.p, x->h_recv.p, bytes, reinterpret_cast<lmr_stream_t>(s));
     if (st != LMR_OK) return st;
-    return hs(hipMemcpyAsync(recv, x->h_recv.p, tot, hipMemcpyHostToDevice, s));
+    // (the staging is shared with calls on the other internal streams: nothing may still read it)
+    if (hipMemcpyAsync(recv, x->h_recv.p, tot, hipMemcpyHostToDevice, s) != hipSuccess) return LMR_E_HIP;
+    return hs(hipStreamSynchronize(s));
 }
 
 lmr_status_t tp_alltoallv(const lmr_transport_t* tp, XState* x, const void* send, const uint64_t* sb,
@@ -211,14 +219,18 @@ lmr_status_t tp_alltoallv(const lmr_transport_t* tp, XState* x, const void* send
     lmr_status_t st = tp->alltoallv(tp->self, x->h_send.p, sb, cso.data(), x->h_recv.p, rb, cro.data(), unit,
                                     reinterpret_cast<lmr_stream_t>(s));
     if (st != LMR_OK) return st;
-    if (rcontig) return rt_end ? hs(hipMemcpyAsync(static_cast<uint8_t*>(recv) + cro[0], x->h_recv.p, rt_end,
-                                                   hipMemcpyHostToDevice, s))
-                               : LMR_OK;
-    for (uint32_t p = 0; p < tp->num_pes; p++)
-        if (rb[p] && hipMemcpyAsync(static_cast<uint8_t*>(recv) + ro[p], static_cast<uint8_t*>(x->h_recv.p) + cro[p], rb[p],
-                                    hipMemcpyHostToDevice, s) != hipSuccess)
+    if (rcontig) {
+        if (rt_end && hipMemcpyAsync(static_cast<uint8_t*>(recv) + cro[0], x->h_recv.p, rt_end, hipMemcpyHostToDevice,
+                                     s) != hipSuccess)
             return LMR_E_HIP;
-    return LMR_OK;
+    } else {
+        for (uint32_t p = 0; p < tp->num_pes; p++)
+            if (rb[p] && hipMemcpyAsync(static_cast<uint8_t*>(recv) + ro[p], static_cast<uint8_t*>(x->h_recv.p) + cro[p],
+                                        rb[p], hipMemcpyHostToDevice, s) != hipSuccess)
+                return LMR_E_HIP;
+    }
+    // (the staging is shared with calls on the other internal streams: nothing may still read it)
+    return hs(hipStreamSynchronize(s));
 }
 
 // ---- the RCCL transport: grouped ncclSend / ncclRecv on the caller's stream.
@@ -233,6 +245,7 @@ struct RcclApi {
     decltype(&ncclSend) send = nullptr;
     decltype(&ncclRecv) recv = nullptr;
     decltype(&ncclCommAbort) comm_abort = nullptr;
+    decltype(&ncclCommSplit) comm_split = nullptr;   // optional: a header communicator
     bool ok = false;
 };
 
@@ -252,6 +265,7 @@ const RcclApi& rccl() {
         api.send = reinterpret_cast<decltype(api.send)>(dlsym(h, "ncclSend"));
         api.recv = reinterpret_cast<decltype(api.recv)>(dlsym(h, "ncclRecv"));
         api.comm_abort = reinterpret_cast<decltype(api.comm_abort)>(dlsym(h, "ncclCommAbort"));
+        api.comm_split = reinterpret_cast<decltype(api.comm_split)>(dlsym(h, "ncclCommSplit"));
         // ncclCommAbort is required: after a failed call it is the only way to end queued peer
         // send / recv kernels, so an RCCL without it is not used (the caller gets LMR_E_UNSUPPORTED)
         api.ok = api.get_unique_id && api.comm_init_rank && api.comm_destroy && api.group_start &&
@@ -263,6 +277,8 @@ const RcclApi& rccl() {
 struct RcclTransport {
     lmr_transport_t tp;
     ncclComm_t comm = nullptr;
+    ncclComm_t hcomm = nullptr;   // header rows (split off comm): their own stream, no false
+                                  // dependency on the previous chunk's records
     int device = 0;
 };
 
@@ -279,6 +295,7 @@ ncclDataType_t nccl_type(uint32_t unit) {
 lmr_status_t rccl_alltoall(void* self, const void* send, void* recv, uint64_t bytes, lmr_stream_t stream) {
     RcclTransport* t = static_cast<RcclTransport*>(self);
     if (!t->comm) return LMR_E_HIP;                  // aborted after an earlier failure
+    ncclComm_t comm = t->hcomm ? t->hcomm : t->comm;
     const uint32_t unit = (bytes % 8 == 0) ? 8 : (bytes % 4 == 0 ? 4 : 1);
     const size_t cnt = size_t(bytes / unit);
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
@@ -286,9 +303,9 @@ lmr_status_t rccl_alltoall(void* self, const void* send, void* recv, uint64_t by
     if (R.group_start() != ncclSuccess) return LMR_E_HIP;
     bool ok = true;
     for (uint32_t p = 0; p < t->tp.num_pes && ok; p++) {
-        ok = R.send(static_cast<const uint8_t*>(send) + uint64_t(p) * bytes, cnt, nccl_type(unit), int(p), t->comm, s) ==
+        ok = R.send(static_cast<const uint8_t*>(send) + uint64_t(p) * bytes, cnt, nccl_type(unit), int(p), comm, s) ==
                  ncclSuccess &&
-             R.recv(static_cast<uint8_t*>(recv) + uint64_t(p) * bytes, cnt, nccl_type(unit), int(p), t->comm, s) ==
+             R.recv(static_cast<uint8_t*>(recv) + uint64_t(p) * bytes, cnt, nccl_type(unit), int(p), comm, s) ==
                  ncclSuccess;
     }
     return (R.group_end() == ncclSuccess && ok) ? LMR_OK : LMR_E_HIP;
@@ -321,8 +338,9 @@ lmr_status_t rccl_alltoallv(void* self, const void* send, const uint64_t* sb, co
 void transport_abort(const lmr_transport_t* tp) {
     if (!tp || tp->alltoall != rccl_alltoall) return;
     RcclTransport* t = static_cast<RcclTransport*>(tp->self);
+    if (t->hcomm) rccl().comm_abort(t->hcomm);
     if (t->comm) rccl().comm_abort(t->comm);
-    t->comm = nullptr;
+    t->comm = t->hcomm = nullptr;
 }
 
 bool valid_layout(const lmr_layout_t* L) {
@@ -404,9 +422,14 @@ lmr_status_t lmr_transport_rccl_create(const uint8_t id[128], uint32_t num_pes, 
         return LMR_E_HIP;
     }
     t->device = device;
+    // the header communicator (collective like the init; without ncclCommSplit, or if the split
+    // fails, headers share the data communicator and its stream)
+    if (rccl().comm_split && rccl().comm_split(t->comm, 0, int(my_pe), &t->hcomm, nullptr) != ncclSuccess)
+        t->hcomm = nullptr;
     t->tp.num_pes = num_pes;
     t->tp.my_pe = my_pe;
     t->tp.host_buffers = 0;
+    t->tp.flags = t->hcomm ? LMR_TRANSPORT_SPLIT_HEADERS : 0u;
     t->tp.self = t;
     t->tp.alltoall = rccl_alltoall;
     t->tp.alltoallv = rccl_alltoallv;
@@ -419,6 +442,7 @@ lmr_status_t lmr_transport_rccl_destroy(lmr_transport_t* tp) {
     RcclTransport* t = static_cast<RcclTransport*>(tp->self);
     (void)hipSetDevice(t->device);
     (void)hipDeviceSynchronize();
+    if (t->hcomm) rccl().comm_destroy(t->hcomm);
     if (t->comm) rccl().comm_destroy(t->comm);       // (an aborted communicator is already gone)
     delete t;
     return LMR_OK;
@@ -508,8 +532,15 @@ lmr_status_t lmr_batch_exchange(lmr_ctx_t* ctx, const lmr_transport_t* tp, const
             return LMR_E_HIP;
     // --- the internal streams start after everything already on the caller's stream
     if (hipEventRecord(x->ev_begin, s0) != hipSuccess || hipStreamWaitEvent(x->sp, x->ev_begin, 0) != hipSuccess ||
-        hipStreamWaitEvent(x->sx, x->ev_begin, 0) != hipSuccess || hipStreamWaitEvent(x->sa, x->ev_begin, 0) != hipSuccess)
+        hipStreamWaitEvent(x->sx, x->ev_begin, 0) != hipSuccess || hipStreamWaitEvent(x->sa, x->ev_begin, 0) != hipSuccess ||
+        hipStreamWaitEvent(x->sh, x->ev_begin, 0) != hipSuccess)
         return LMR_E_HIP;
+    // header rows on their own stream when the transport allows it (LMR_TRANSPORT_SPLIT_HEADERS;
+    // host-buffer transports are host-ordered): chunk j+1's header exchange is posted before
+    // chunk j's all-to-all-v and waits only for chunk j+1's pack, so the host's per-chunk read
+    // of the counts overlaps the previous chunk's records in flight
+    const bool split = tp->host_buffers || (tp->flags & LMR_TRANSPORT_SPLIT_HEADERS);
+    hipStream_t const shd = split ? x->sh : x->sx;
     x->recv_used[0] = x->recv_used[1] = false;
     x->send_used[0] = x->send_used[1] = false;
     lmr_status_t st = lmr_stage_begin(ctx, desc);
@@ -602,16 +633,16 @@ lmr_status_t lmr_batch_exchange(lmr_ctx_t* ctx, const lmr_transport_t* tp, const
         }
         return LMR_OK;
     };
-    // ---- the header all-to-all of chunk j (exchange stream) and its rows to the host
+    // ---- the header all-to-all of chunk j (header stream) and its rows to the host
     auto post_header = [&](uint64_t j) -> lmr_status_t {
         const int b = int(j & 1);
-        if (hipStreamWaitEvent(x->sx, x->ev_packed[b], 0) != hipSuccess) return LMR_E_HIP;
-        lmr_status_t e = tp_alltoall(tp, x, x->hdr_send[b].p, x->hdr_recv[b].p, LMR_XHDR_WORDS * 8, x->sx);
+        if (hipStreamWaitEvent(shd, x->ev_packed[b], 0) != hipSuccess) return LMR_E_HIP;
+        lmr_status_t e = tp_alltoall(tp, x, x->hdr_send[b].p, x->hdr_recv[b].p, LMR_XHDR_WORDS * 8, shd);
         if (e != LMR_OK) { guard.tp_failed = true; return e; }
         int64_t* hs_ = const_cast<int64_t*>(h_send_rows(b));
-        if (hipMemcpyAsync(hs_, x->hdr_send[b].p, rows * 8, hipMemcpyDeviceToHost, x->sx) != hipSuccess ||
-            hipMemcpyAsync(hs_ + rows, x->hdr_recv[b].p, rows * 8, hipMemcpyDeviceToHost, x->sx) != hipSuccess ||
-            hipEventRecord(x->ev_hdr[b], x->sx) != hipSuccess)
+        if (hipMemcpyAsync(hs_, x->hdr_send[b].p, rows * 8, hipMemcpyDeviceToHost, shd) != hipSuccess ||
+            hipMemcpyAsync(hs_ + rows, x->hdr_recv[b].p, rows * 8, hipMemcpyDeviceToHost, shd) != hipSuccess ||
+            hipEventRecord(x->ev_hdr[b], shd) != hipSuccess)
             return LMR_E_HIP;
         return LMR_OK;
     };
@@ -631,6 +662,10 @@ lmr_status_t lmr_batch_exchange(lmr_ctx_t* ctx, const lmr_transport_t* tp, const
         const uint64_t k = lmr_exchange_plan(npes, iw, eb, h_send, h_recv, isb.data(), iso.data(), irb.data(),
                                              iro.data(), vsb.data(), vso.data(), vrb.data(), vro.data());
         if (j == 0) nchunks = std::max<uint64_t>(k, 1);
+        if (split && j + 1 < nchunks) {                 // the next header before this chunk's records
+            if ((st = pack_until(j + 2)) != LMR_OK) return st;
+            if ((st = post_header(j + 1)) != LMR_OK) return st;
+        }
         const uint64_t lo = chunk_lo(j), hi = chunk_hi(j);
         if (!mvsi && j < my_k && hi > lo && free_pack) {
             const uint32_t cap = uint32_t(region_cap(hi - lo));
@@ -743,8 +778,10 @@ lmr_status_t lmr_batch_exchange(lmr_ctx_t* ctx, const lmr_transport_t* tp, const
         // exchange stream: every PE posts the collectives in the same order), and the pack of
         // the chunk after it, which runs while the host waits for that header
         if (j + 1 < nchunks) {
-            if ((st = pack_until(j + 2)) != LMR_OK) return st;
-            if ((st = post_header(j + 1)) != LMR_OK) return st;
+            if (!split) {
+                if ((st = pack_until(j + 2)) != LMR_OK) return st;
+                if ((st = post_header(j + 1)) != LMR_OK) return st;
+            }
             if ((st = pack_until(std::min<uint64_t>(j + 3, nchunks))) != LMR_OK) return st;
         }
     }
@@ -797,11 +834,11 @@ lmr_status_t lmr_batch_exchange(lmr_ctx_t* ctx, const lmr_transport_t* tp, const
             }
         }
     }
-    // ---- the caller's stream continues after the three internal streams
+    // ---- the caller's stream continues after the internal streams
     if (hipEventRecord(x->ev_pack_done, x->sp) != hipSuccess || hipEventRecord(x->ev_x_done, x->sx) != hipSuccess ||
-        hipEventRecord(x->ev_apply_done, x->sa) != hipSuccess ||
+        hipEventRecord(x->ev_apply_done, x->sa) != hipSuccess || hipEventRecord(x->ev_h_done, x->sh) != hipSuccess ||
         hipStreamWaitEvent(s0, x->ev_pack_done, 0) != hipSuccess || hipStreamWaitEvent(s0, x->ev_x_done, 0) != hipSuccess ||
-        hipStreamWaitEvent(s0, x->ev_apply_done, 0) != hipSuccess)
+        hipStreamWaitEvent(s0, x->ev_apply_done, 0) != hipSuccess || hipStreamWaitEvent(s0, x->ev_h_done, 0) != hipSuccess)
         return LMR_E_HIP;
     return LMR_OK;
 }

@@ -57,7 +57,7 @@ class DevPtrGlooTransport:
         self.hip = hip
         self._a2a = _capi.ALLTOALL_FN(self._alltoall)
         self._a2av = _capi.ALLTOALLV_FN(self._alltoallv)
-        self.t = _capi.lmr_transport_t(num_pes, my_pe, 0, 0, None, self._a2a, self._a2av)
+        self.t = _capi.lmr_transport_t(num_pes, my_pe, 0, 1, None, self._a2a, self._a2av)   # flags: split headers
 
     @property
     def ptr(self):
