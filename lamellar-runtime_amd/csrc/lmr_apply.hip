@@ -611,7 +611,7 @@ __host__ __device__ inline uint32_t seg_cap(uint32_t capc, uint32_t x) {
 __device__ __forceinline__ uint32_t xcc_id() { return __builtin_amdgcn_s_getreg((3 << 11) | 20) & (kXcds - 1); }  // HW_REG_XCC_ID
 
 template <int IW, int VB, int RPT, bool PAIRS>
-__global__ __launch_bounds__(1024) void k_coarse_free(PartArgs p) {
+__device__ __forceinline__ void coarse_free_body(const PartArgs& p, const uint32_t g) {
     using V = typename idx_t<VB>::I;
     constexpr uint32_t kRound = RPT * 1024;
     extern __shared__ uint32_t th[];                   // [num_tiles] this block's tile counts
@@ -620,7 +620,7 @@ __global__ __launch_bounds__(1024) void k_coarse_free(PartArgs p) {
     __shared__ uint32_t s_spill;                      // this round has records past their bucket region
     __shared__ uint32_t s_idx[kRound];
     __shared__ V s_val[kRound];
-    const uint32_t g = blockIdx.x, C = p.C;
+    const uint32_t C = p.C;
     const uint32_t xcc = xcc_id();
     const uint32_t capx = sub_cap(p.capc), caps = seg_cap(p.capc, kXcds);
     const int cshift = p.tile_shift + kFineShift;
@@ -758,6 +758,38 @@ __global__ __launch_bounds__(1024) void k_coarse_free(PartArgs p) {
     __syncthreads();
     uint32_t* row = p.counts + uint64_t(g) * p.num_tiles;   // row g (coalesced)
     for (uint32_t t = threadIdx.x; t < p.num_tiles; t += blockDim.x) row[t] = p.accumulate ? row[t] + th[t] : th[t];
+}
+
+template <int IW, int VB, int RPT, bool PAIRS>
+__global__ __launch_bounds__(1024) void k_coarse_free(PartArgs p) {
+    coarse_free_body<IW, VB, RPT, PAIRS>(p, blockIdx.x);
+}
+
+// Count-free staged regions partitioned together (the exchange's sources of one chunk): one
+// launch for up to kFuseFree regions, each with its own block range and rows of the tile-count
+// rows (p.counts + row0 * num_tiles); the bucket regions and their fill counters are the session's.
+constexpr int kFuseFree = 8;
+struct FreeRegion {
+    const uint8_t* idx;
+    uint64_t idx_stride;
+    const uint8_t* val;
+    uint64_t val_stride, val_bits, n, chunk;
+    uint32_t G, row0, block0;
+};
+struct FreeTable {
+    FreeRegion r[kFuseFree];
+    uint32_t nr;
+};
+template <int IW, int VB, int RPT>
+__global__ __launch_bounds__(1024) void k_coarse_free_stage(PartArgs q, FreeTable t) {
+    uint32_t i = 0;
+    while (i + 1 < t.nr && t.r[i + 1].block0 <= blockIdx.x) i++;
+    const FreeRegion& g = t.r[i];
+    PartArgs p = q;
+    p.idx = g.idx; p.idx_stride = g.idx_stride; p.val = g.val; p.val_stride = g.val_stride;
+    p.val_bits = g.val_bits; p.n = g.n; p.chunk = g.chunk; p.G = g.G;
+    p.counts = q.counts + uint64_t(g.row0) * q.num_tiles;
+    coarse_free_body<IW, VB, RPT, false>(p, blockIdx.x - g.block0);
 }
 
 // tile_start[t] = sum over blocks of the coarse pass's row counts (scanned after).
@@ -2185,41 +2217,82 @@ bool stage_free_applies(int dtype, int op, int ret, uint64_t shard_len, uint64_t
 
 static hipError_t stage_region_free(int dtype, int index_size, const ApplyArgs& a, const TiledWs& w,
                                     StageSession& s, hipStream_t st) {
-    PartArgs q = free_args(dtype, a, w, kStageFreeBlocks);
-    q.accumulate = 1;                                      // tile-count rows add up over the session
-    const int vb = dtype_bytes(dtype);
-    const int frpt = free_partition_rpt(dtype, a.op, a.ret, 0, q.num_tiles, w.tmp_cap);
-    if (frpt == 0 || s.nreg >= kMaxRegions) return hipErrorInvalidValue;
-    hipError_t e;
-    if (!s.free_armed) {                                   // fill counters, tile-count rows
-        e = hipMemsetAsync(w.ff, 0, ff_words() * 4, st);
-        if (e == hipSuccess) e = hipMemsetAsync(w.counts, 0, size_t(q.G) * q.num_tiles * 4, st);
-        if (e != hipSuccess) return e;
-        s.free_armed = true;
-    }
-    q.idx = a.idx; q.idx_stride = a.idx_stride; q.val = a.val; q.val_stride = a.val_stride;
-    q.val_bits = a.val_bits; q.n = a.n; q.chunk = (a.n + q.G - 1) / q.G;
-    {
-        ProfScope ps(a.prof, LMR_STAGE_BIN_SCATTER, st, a.n);
-        e = launch_coarse_free(index_size, vb, frpt, q, st);
-    }
-    if (e != hipSuccess) return e;
+    (void)w; (void)st;
+    if (s.nreg >= kMaxRegions) return hipErrorInvalidValue;
+    // recorded; partitioned with the session's other pending regions (stage_partition_free)
     s.reg[s.nreg] = StageRegion{0, a.n, nullptr, nullptr, a.op, LMR_RET_NONE, a.cmp_bits, a.eps_bits};
+    s.pend[s.nreg] = PendingRegion{a, index_size};
     s.nreg += 1;
     s.staged += a.n;
+    return hipSuccess;
+}
+
+// the pending count-free regions, k_coarse_free over groups of up to kFuseFree regions of one
+// index width: a lone region keeps kStageFreeBlocks blocks, a group shares kMaxBinBlocks rows
+static hipError_t stage_partition_free(const TiledWs& w, StageSession& s, hipStream_t st) {
+    const int dtype = s.dtype, vb = dtype_bytes(dtype);
+    while (s.parted < s.nreg) {
+        const ApplyArgs& a0 = s.pend[s.parted].a;
+        const int iw = s.pend[s.parted].iw;
+        PartArgs q = free_args(dtype, a0, w, kStageFreeBlocks);
+        q.accumulate = 1;                                  // tile-count rows add up over the session
+        const int frpt = free_partition_rpt(dtype, a0.op, a0.ret, 0, q.num_tiles, w.tmp_cap);
+        if (frpt == 0) return hipErrorInvalidValue;
+        if (!s.free_armed) {                               // fill counters, tile-count rows
+            hipError_t e = hipMemsetAsync(w.ff, 0, ff_words() * 4, st);
+            if (e == hipSuccess) e = hipMemsetAsync(w.counts, 0, size_t(kMaxBinBlocks) * q.num_tiles * 4, st);
+            if (e != hipSuccess) return e;
+            s.free_armed = true;
+        }
+        int r1 = s.parted;
+        while (r1 < s.nreg && r1 - s.parted < kFuseFree && s.pend[r1].iw == iw) r1++;
+        const uint32_t nr = uint32_t(r1 - s.parted);
+        const uint32_t gcap = nr == 1 ? kStageFreeBlocks : std::max<uint32_t>(32, uint32_t(kMaxBinBlocks) / nr);
+        FreeTable t{};
+        uint32_t rows = 0;
+        uint64_t n_all = 0;
+        for (uint32_t k = 0; k < nr; k++) {
+            const ApplyArgs& a = s.pend[s.parted + int(k)].a;
+            const uint32_t G = uint32_t(std::max<uint64_t>(1, std::min<uint64_t>((a.n + 16383) / 16384, gcap)));
+            t.r[k] = FreeRegion{a.idx, a.idx_stride, a.val, a.val_stride, a.val_bits, a.n, (a.n + G - 1) / G, G,
+                                rows, rows};
+            rows += G;
+            n_all += a.n;
+        }
+        t.nr = nr;
+        s.free_rows = std::max(s.free_rows, rows);
+        hipError_t e;
+        {
+            ProfScope ps(a0.prof, LMR_STAGE_BIN_SCATTER, st, n_all);
+            e = dispatch_iw(iw, [&](auto iwt) {
+                constexpr int IW = decltype(iwt)::value;
+                dispatch_vb_rpt<4>(vb, frpt, [&](auto vbt, auto rpt) {
+                    constexpr int VBc = decltype(vbt)::value, R = decltype(rpt)::value;
+                    hipLaunchKernelGGL((k_coarse_free_stage<IW, VBc, R>), dim3(rows), dim3(1024),
+                                       size_t(q.num_tiles) * 4, st, q, t);
+                });
+                return hipGetLastError();
+            });
+        }
+        if (e != hipSuccess) return e;
+        s.parted = r1;
+    }
     return hipSuccess;
 }
 
 static hipError_t stage_finish_free(const TiledWs& w, StageSession& s, hipStream_t st) {
     const ApplyArgs& a = s.a;
     const int dtype = s.dtype, vb = dtype_bytes(dtype);
-    PartArgs q = free_args(dtype, a, w, kStageFreeBlocks);
-    hipError_t e = launch_free_finish(vb, q, w, s.staged, a.prof, st);
+    hipError_t e = stage_partition_free(w, s, st);
+    PartArgs q = free_args(dtype, a, w, std::max<uint32_t>(s.free_rows, 1));
+    if (e == hipSuccess) e = launch_free_finish(vb, q, w, s.staged, a.prof, st);
     // values are materialised in the bins (regions may mix array and scalar values)
     if (e == hipSuccess) e = launch_tile_sweep(dtype, a, w, q.num_tiles, s.staged, false, nullptr, nullptr, st);
     s.nreg = 0;
+    s.parted = 0;
     s.staged = 0;
     s.free_armed = false;
+    s.free_rows = 0;
     return e;
 }
 
@@ -2245,6 +2318,7 @@ hipError_t launch_stage_region(int dtype, int index_size, const ApplyArgs& a, co
 // the regions [s.parted, s.nreg): count, coarse and fine passes, fused over groups of up to kFuse
 // regions of one index width whose count rows fit the workspace
 hipError_t launch_stage_partition(const TiledWs& w, StageSession& s, hipStream_t st) {
+    if (s.free) return stage_partition_free(w, s, st);
     const int dtype = s.dtype, vb = dtype_bytes(dtype);
     const int shift = tile_shift_for(dtype);
     while (s.parted < s.nreg) {

@@ -758,7 +758,7 @@ lmr_status_t lmr_stage_op(lmr_ctx_t* ctx, uint32_t op, uint64_t cmp_bits, uint64
 lmr_status_t lmr_stage_flush(lmr_ctx_t* ctx, lmr_stream_t stream) {
     if (!ctx || !ctx->stage || !ctx->stage->open) return LMR_E_INVALID;
     StageSession& ss = ctx->stage->s;
-    if (ss.free || ss.parted == ss.nreg) return LMR_OK;
+    if (ss.parted == ss.nreg) return LMR_OK;
     return hip_status(launch_stage_partition(carve_tiled_ws(ctx->ws, ctx->rec_cap), ss,
                                              reinterpret_cast<hipStream_t>(stream)));
 }

@@ -191,6 +191,7 @@ struct StageSession {
     uint64_t crounds = 0;  // crtab rounds in use
     bool free = false;   // count-free regions (stage_free_applies): shared bucket regions, one fine pass
     bool free_armed = false;
+    uint32_t free_rows = 0;  // count-free sessions: tile-count rows the coarse launches used
     bool switched = false;  // the op changed with records staged (lmr_stage_op): later phases counted
     StageRegion reg[kMaxRegions];
     PendingRegion pend[kMaxRegions];
@@ -200,9 +201,9 @@ bool stage_pending_other_op(const StageSession& s, const ApplyArgs& a);
 // true when a staged session of this op takes the count-free regions
 bool stage_free_applies(int dtype, int op, int ret, uint64_t shard_len, uint64_t cap);
 // add the records of `a` as the next region (caller checks capacity: s.staged + a.n <= workspace
-// capacity, a.n <= kStageMaxRegion, s.nreg < kMaxRegions). Counted regions are only recorded:
+// capacity, a.n <= kStageMaxRegion, s.nreg < kMaxRegions). Regions are only recorded:
 // launch_stage_partition partitions every pending region at once (the caller's buffers stay valid
-// until then); count-free regions are partitioned at once.
+// until then).
 hipError_t launch_stage_region(int dtype, int index_size, const ApplyArgs& a, const TiledWs& w,
                                StageSession& s, hipStream_t st);
 hipError_t launch_stage_partition(const TiledWs& w, StageSession& s, hipStream_t st);
