@@ -1243,14 +1243,16 @@ static int bin_blocks_cap(int vb) {
     return v ? v : (coarse_rpt(vb) >= 8 ? 256 : 512);
 }
 // Delta-mode threshold: a tile of a combinable op splits into delta pieces when it holds more
-// than max(LMR_DELTA_MUL x the average tile's records, LMR_DELTA_MIN) records (C3: 4 x / 64K,
-// 2 x / 32K, 2 x / 16K, 1 x / 16K and 1 x / 8K all within 0.50-0.53 ms of tile sweep).
+// than max(LMR_DELTA_MUL x the average tile's records, LMR_DELTA_MIN) records. Round 4 (same box,
+// profiles/r4/ab/r4g_*, r4h_*): 2 x / 32K takes C3's warm tiles off the owner kernel's serialised
+// LDS atomics, tile sweep 0.463-0.484 -> 0.443-0.466 ms (4 x / 64K before; 1 x / 16K and 2 x / 16K
+// no better; no delta at all: 4.69 ms).
 static uint64_t delta_mul() {
-    static int v = env_int("LMR_DELTA_MUL", 4, 1, 1 << 20);
+    static int v = env_int("LMR_DELTA_MUL", 2, 1, 1 << 20);
     return uint64_t(v);
 }
 static uint64_t delta_min() {
-    static int v = env_int("LMR_DELTA_MIN", 65536, 1024, 1 << 30);
+    static int v = env_int("LMR_DELTA_MIN", 32768, 1024, 1 << 30);
     return uint64_t(v);
 }
 static int tile_grid_cap() {

@@ -17,11 +17,13 @@ import sys
 # to the stage). Staged sessions: one bin_scatter / fine_scatter invocation per region, one
 # tile_apply / unpartition invocation per tile sweep.
 STAGES = {
-    "bin_count": (("k_bin_count", "k_ccount"), ("k_bin_count", "k_ccount")),
-    "bin_scatter": (("k_coarse_free", "k_coarse_scatter", "k_bin_scatter"),
-                    ("k_coarse_free", "k_coarse_scatter", "k_coarse_offsets", "k_bin_scatter")),
-    "fine_scatter": (("k_fine_free", "k_fine_scatter", "k_fine_piece"),
-                     ("k_fine_free", "k_fine_scatter", "k_fine_piece", "k_piece_count", "k_free_tile_totals")),
+    "bin_count": (("k_bin_count", "k_ccount", "k_ccount_stage"), ("k_bin_count", "k_ccount", "k_ccount_stage")),
+    "bin_scatter": (("k_coarse_free", "k_coarse_scatter", "k_bin_scatter", "k_coarse_stage", "k_coarse_free_stage"),
+                    ("k_coarse_free", "k_coarse_scatter", "k_coarse_offsets", "k_bin_scatter", "k_coarse_stage",
+                     "k_coarse_free_stage")),
+    "fine_scatter": (("k_fine_free", "k_fine_scatter", "k_fine_piece", "k_fine_stage"),
+                     ("k_fine_free", "k_fine_scatter", "k_fine_piece", "k_piece_count", "k_free_tile_totals",
+                      "k_fine_stage")),
     "tile_apply": (("k_tile_owner",), ("k_tile_owner", "k_tile_delta", "k_tile_plan", "k_stage_plan")),
     "unpartition": (("k_tile_owner",), ("k_unpartition", "k_unpartition_multi", "k_unpart_rounds",
                                         "k_unpart_crounds")),
