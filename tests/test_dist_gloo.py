@@ -461,3 +461,16 @@ def test_host_transport_callbacks_gloo():
             exp = np.concatenate([(np.arange((p + 1) * (r + 2)) + 16 * p + 4 * r) % 251 for p in range(ws)])
             assert np.array_equal(pe[r][f"v{unit}"].astype(np.int64), exp)
         assert pe[r]["bad_status"][0] != 0 and pe[r]["raised"][0] == 1
+
+
+def test_exchange_plan_flag_bits(capi):
+    """The header's flags word: LMR_XHDR_SCALAR (1) means no values travel; LMR_XHDR_ORDERED (2)
+    marks an in-order stream (one reference AM per destination) and changes no split."""
+    from lamellar_runtime_amd import _capi
+    assert (_capi.XHDR_SCALAR, _capi.XHDR_ORDERED) == (1, 2)
+    sh = np.array([[4, -1, 2, 0, 1], [3, -1, 3, 9, 1]])          # ordered; ordered + scalar
+    rh = np.array([[5, -1, 2, 0, 1], [6, -1, 3, 7, 1]])
+    k, (isb, iso, irb, iro, vsb, vso, vrb, vro) = _plan(capi, 2, 4, 8, sh, rh)
+    assert k == 1
+    assert list(isb) == [16, 12] and list(irb) == [20, 24]       # every record's index travels
+    assert list(vsb) == [32, 0] and list(vrb) == [40, 0]         # the scalar stream sends no values

@@ -132,3 +132,19 @@ def test_array_api_small_batches_deterministic(world, lam):
     assert list(olds) == exp and float(f.local_numpy()[0]) == s
     r = a.batch_rem([2, 2], [5, 3]).block()
     assert r is None
+
+
+@pytest.mark.parametrize("dt,op", [("u64", SWAP), ("f64", 1), ("i32", CAS)])
+def test_ordered_apply_in_pieces(world, orc, lam, dt, op):
+    """An ordered stream longer than the reserved sort capacity (2^22 records) runs piece after
+    piece; every record of a piece is applied before any of the next, so each element still
+    sees its records in input order: bit-exact against the sequential oracle, including the
+    records of an element that straddle the piece boundary."""
+    k = world.team().kernels
+    rng = np.random.default_rng(505 + CODE[dt])
+    n = (1 << 22) + 4099
+    shard0, idx, vals, cur, eps = colliding(dt, op, rng, 1 << 16, n)
+    if dt == "f64":
+        vals = rng.random(n) * 8.0 - 4.0                   # inexact sums: the order shows in the bits
+    c = Case(k, orc, lam, dt, op, shard0, idx, vals, "soa", ORDERED, cur=cur, eps=eps)
+    check_exact(c, (dt, op, n))
