@@ -82,7 +82,9 @@ def stage_bytes_per_op(stage, iw, vb, eb, n, shard_len, fetch):
         "fine_scatter": 4 + vb + 2 + vb + pos,          # temp record in, tile-local record (+ rpos) out
         "tile_apply": 2 + vb + res + 2.0 * eb * shard_len / max(n, 1),
         "unpartition": (2 if two_level else 1) * (4 + 2 * eb) if fetch else 0.0,
-        "pack": 8 + 8 + vb + iw + vb + 4,
+        # count-free pack (nothing returned): record in, record out; the counted pack of
+        # returning ops adds the count pass's index read and the u32 position out
+        "pack": 8 + vb + iw + vb + 12 * float(fetch),
         "scatter_results": 4 + 2 * eb,
         "mvsi": vb + res,
         "window": 2 * iw + vb + 4 + vb + pos,           # count (idx) + scatter (idx, val in; u32 idx, val, pos out)
@@ -480,11 +482,13 @@ def main():
     # read/write (+ returned value)) x ops per step / the step time; frac against the
     # 8.0 TB/s HBM3E spec. Per-stage figures (each kernel's own algorithmic bytes over
     # its HIP-event launch time) live in apply_pipeline.stages.
-    iw = 8 if npes == 1 else W.arr.index_size()
     per = {}
     for name, (ms, cnt, recs) in stages.items():
         if cnt:
             per[name] = (ms / cnt, cnt / args.steps, recs / cnt)
+    # index bytes per record the partition passes read: the caller's u64 global indices on
+    # the local path, the exchange's packed local offsets (lmr_index_size) behind a pack
+    iw = 8 if npes == 1 and "pack" not in per else W.arr.index_size()
     step_s = ms_per_step * 1e-3
     achieved = W.survey_bpo * W.ops_per_step / step_s
     traffic = None

@@ -241,7 +241,8 @@ __global__ __launch_bounds__(1024) void k_pack_stage(PackK p) {
     __shared__ uint32_t hist[kStageMaxPes], base[kStageMaxPes + 1], cursor[kStageMaxPes];
     __shared__ I s_off[kRound];
     __shared__ V s_val[kRound];
-    __shared__ uint32_t s_pos[kRound];
+    __shared__ uint32_t s_pos[FREE ? 1 : kRound];   // FREE packs return nothing: no positions, and
+                                                    // the smaller LDS footprint fits 2 blocks per CU
     const uint32_t np = p.npes;
     const int bits = key_bits(np);
     __shared__ uint32_t s_over;
@@ -293,7 +294,7 @@ __global__ __launch_bounds__(1024) void k_pack_stage(PackK p) {
             const uint32_t q = base[m_pe[j]] + m_rank[j];
             s_off[q] = I(m_off[j]);
             s_val[q] = m_v[j];
-            if (p.out_pos) s_pos[q] = uint32_t(r0 + uint64_t(j) * 1024 + threadIdx.x);
+            if (!FREE && p.out_pos) s_pos[q] = uint32_t(r0 + uint64_t(j) * 1024 + threadIdx.x);
         }
         if (r0 + kRound < hi) load_round(r0 + kRound);
         __syncthreads();
@@ -301,7 +302,7 @@ __global__ __launch_bounds__(1024) void k_pack_stage(PackK p) {
             bucket_writeout(hist, base, cursor, np, [&](uint32_t q, uint32_t dst) {
                 reinterpret_cast<I*>(p.out_idx)[dst] = s_off[q];
                 if (vals) reinterpret_cast<V*>(p.out_vals)[dst] = s_val[q];
-                if (p.out_pos) p.out_pos[dst] = s_pos[q];
+                if (!FREE && p.out_pos) p.out_pos[dst] = s_pos[q];
             });
         __syncthreads();
         if constexpr (!FREE)
@@ -400,6 +401,10 @@ hipError_t launch_pack(const PackArgs& a, uint32_t* counts, uint32_t* partials, 
     return hipGetLastError();
 }
 
+#ifndef LMR_PACK_FREE_LDS
+#define LMR_PACK_FREE_LDS 72   // KB of LDS per round buffer: 72 fits 2 blocks per CU (variant builds: -D...)
+#endif
+
 // Count-free unordered pack (nothing returned): destination i's records land in
 // [i * cap, i * cap + dest_counts[i]) of out_idx / out_vals. dest_counts[i] > cap means
 // the region overflowed and the output is incomplete (pack again with launch_pack).
@@ -423,7 +428,7 @@ hipError_t launch_pack_free(const PackArgs& a, uint32_t* fill, uint32_t cap, hip
         const int vbk = a.vals ? int(a.val_bytes) : 1;
         dispatch_pack_stage(int(a.index_size), vbk, [&](auto iw, auto vb) {
             constexpr int IWc = decltype(iw)::value, VBc = decltype(vb)::value;
-            constexpr int RP = (IWc + VBc + 4) * 8 <= 150 ? 8 : 4;
+            constexpr int RP = (IWc + VBc) * 8 <= LMR_PACK_FREE_LDS ? 8 : 4;   // rounds of RP * 1024 records
             if (mode == LMR_MAP_BLOCK)
                 hipLaunchKernelGGL((k_pack_stage<IWc, VBc, RP, LMR_MAP_BLOCK, true>), dim3(unsigned(G)), dim3(1024), 0, s, p);
             else if (mode == LMR_MAP_CYCLIC)
