@@ -1532,7 +1532,7 @@ static hipError_t launch_tile_sweep(int dtype, const ApplyArgs& a, const TiledWs
     t.rts = nullptr; t.nreg = 0; t.rstride = 0; t.mixed = 0;
     const bool delta = op_combines(a.op) && n > thresh;
     const unsigned dgrid = unsigned(std::min<uint64_t>(2 * ((n + kSplit - 1) / kSplit), uint64_t(tile_grid_cap())));
-    return launch_tile_kernels(dtype, a.op, t, delta, dgrid, s);
+    return launch_tile_kernels(dtype, a.op, t, delta, dgrid, s, w.side);
 }
 
 // One tiled piece: a.n <= workspace capacity, a.n < 2^32.
@@ -2503,7 +2503,7 @@ hipError_t launch_stage_finish(const TiledWs& w, StageSession& s, hipStream_t st
         const bool delta = !mixed && op_combines(a.op) && s.staged > thresh;
         const unsigned dgrid = unsigned(std::min<uint64_t>(2 * ((s.staged + kSplit - 1) / kSplit) + 2 * uint64_t(s.nreg),
                                                            uint64_t(tile_grid_cap())));
-        e = launch_tile_kernels(dtype, mixed ? -1 : a.op, t, delta, dgrid, st);
+        e = launch_tile_kernels(dtype, mixed ? -1 : a.op, t, delta, dgrid, st, w.side);
     }
     if (e == hipSuccess && has_res) {
         // binned -> temp slot (in-bounds slots of each region) -> arrival order

@@ -63,6 +63,13 @@ using namespace lmr;
 
 namespace {
 
+// the context's workspace carved for `cap` records, with its side lane
+TiledWs ctx_ws(const lmr_ctx* ctx, uint64_t cap) {
+    TiledWs w = carve_tiled_ws(ctx->ws, cap);
+    w.side = SideLane{ctx->side, ctx->side_fork, ctx->side_join};
+    return w;
+}
+
 constexpr size_t kPackScratchCounts = size_t(kMaxPackPes) * kMaxBinBlocks;
 
 struct CtxExtra {
@@ -184,7 +191,7 @@ uint64_t load_scalar_bits(const void* val, int dtype) {
 // applying what is staged first whenever the workspace or the region table is full.
 hipError_t stage_records(lmr_ctx* ctx, StageSession& ss, const ApplyArgs& a, int dtype, int iw, uint64_t split,
                          hipStream_t s) {
-    TiledWs w = carve_tiled_ws(ctx->ws, ctx->rec_cap);
+    TiledWs w = ctx_ws(ctx, ctx->rec_cap);
     const int eb = dtype_bytes(dtype);
     uint64_t piece = ctx->rec_cap < kStageMaxRegion ? ctx->rec_cap : kStageMaxRegion;
     if (split > 1) {
@@ -256,10 +263,10 @@ lmr_status_t run_apply(lmr_ctx* ctx, const lmr_apply_desc_t* d, ApplyArgs a, int
         ss.dtype = int(d->dtype);
         ss.free = stage_free_applies(int(d->dtype), a.op, a.ret, d->shard_len, ctx->rec_cap);
         hipError_t e = stage_records(ctx, ss, a, int(d->dtype), iw, split, s);
-        if (e == hipSuccess) e = launch_stage_finish(carve_tiled_ws(ctx->ws, ctx->rec_cap), ss, s);
+        if (e == hipSuccess) e = launch_stage_finish(ctx_ws(ctx, ctx->rec_cap), ss, s);
         return hip_status(e);
     }
-    TiledWs w = carve_tiled_ws(ctx->ws, ctx->rec_cap);
+    TiledWs w = ctx_ws(ctx, ctx->rec_cap);
     const uint64_t n = a.n;
     for (uint64_t p0 = 0; p0 < n; p0 += ctx->rec_cap) {
         uint64_t m = n - p0 < ctx->rec_cap ? n - p0 : ctx->rec_cap;
@@ -309,7 +316,13 @@ lmr_status_t lmr_ctx_create(int device, lmr_ctx_t** out) {
     c->d_err = reinterpret_cast<uint32_t*>(p);
     // the error word and the pack scan's look-back scratch start zeroed
     if (hipMemset(p, 0, pack_scratch_bytes()) != hipSuccess) { (void)hipFree(p); delete c; return LMR_E_HIP; }
-    if (ord_reserve(c, kOrderedMinPiece) != hipSuccess) { lmr_ctx_destroy(c); return LMR_E_HIP; }
+    if (ord_reserve(c, kOrderedMinPiece) != hipSuccess ||
+        hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreateWithFlags(&c->side_fork, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&c->side_join, hipEventDisableTiming) != hipSuccess) {
+        lmr_ctx_destroy(c);
+        return LMR_E_HIP;
+    }
     *out = c;
     return LMR_OK;
 }
@@ -323,6 +336,10 @@ lmr_status_t lmr_ctx_destroy(lmr_ctx_t* ctx) {
     win_state_free(ctx->win);
     wire_bufs_free(ctx->wire);
     ord_bufs_free(ctx->ord);
+    if (ctx->side) (void)hipStreamSynchronize(ctx->side);
+    if (ctx->side_fork) (void)hipEventDestroy(ctx->side_fork);
+    if (ctx->side_join) (void)hipEventDestroy(ctx->side_join);
+    if (ctx->side) (void)hipStreamDestroy(ctx->side);
     if (ctx->ws) (void)hipFree(ctx->ws);
     if (ctx->d_err) (void)hipFree(ctx->d_err);
     if (ctx->prof) {
@@ -347,7 +364,7 @@ lmr_status_t lmr_ctx_reserve(lmr_ctx_t* ctx, uint64_t max_records) {
     ctx->ws = reinterpret_cast<uint8_t*>(p);
     ctx->ws_bytes = b;
     {   // the scan's look-back scratch starts zeroed (every scan leaves it so)
-        const TiledWs w = carve_tiled_ws(ctx->ws, max_records);
+        const TiledWs w = ctx_ws(ctx, max_records);
         if (hipMemset(w.partials, 0, scan_scratch_words(size_t(kMaxTiles) * kMaxBinBlocks) * 4) != hipSuccess)
             return LMR_E_HIP;
     }
@@ -716,7 +733,7 @@ lmr_status_t lmr_stage_soa(lmr_ctx_t* ctx, const void* d_indices, uint32_t index
                        !(d->strategy == LMR_STRATEGY_AUTO && n < 65536);
     if (!tiled) {                                                     // small stream: applied now,
         if (S->s.nreg > 0 && stage_pending_other_op(S->s, a)) {      // after earlier op phases
-            const hipError_t e = launch_stage_finish(carve_tiled_ws(ctx->ws, ctx->rec_cap), S->s, s);
+            const hipError_t e = launch_stage_finish(ctx_ws(ctx, ctx->rec_cap), S->s, s);
             if (e != hipSuccess) return hip_status(e);
         }
         return run_apply(ctx, d, a, int(index_size), s);
@@ -739,7 +756,7 @@ lmr_status_t lmr_stage_op(lmr_ctx_t* ctx, uint32_t op, uint64_t cmp_bits, uint64
     if (S->s.nreg > 0) {
         // count-free regions share their bucket regions: apply them before the next op phase
         if (S->s.free) {
-            const hipError_t e = launch_stage_finish(carve_tiled_ws(ctx->ws, ctx->rec_cap), S->s,
+            const hipError_t e = launch_stage_finish(ctx_ws(ctx, ctx->rec_cap), S->s,
                                                      reinterpret_cast<hipStream_t>(stream));
             if (e != hipSuccess) return hip_status(e);
         }
@@ -759,7 +776,7 @@ lmr_status_t lmr_stage_flush(lmr_ctx_t* ctx, lmr_stream_t stream) {
     if (!ctx || !ctx->stage || !ctx->stage->open) return LMR_E_INVALID;
     StageSession& ss = ctx->stage->s;
     if (ss.parted == ss.nreg) return LMR_OK;
-    return hip_status(launch_stage_partition(carve_tiled_ws(ctx->ws, ctx->rec_cap), ss,
+    return hip_status(launch_stage_partition(ctx_ws(ctx, ctx->rec_cap), ss,
                                              reinterpret_cast<hipStream_t>(stream)));
 }
 
@@ -768,7 +785,7 @@ lmr_status_t lmr_stage_finish(lmr_ctx_t* ctx, lmr_stream_t stream) {
     StageState* S = ctx->stage;
     S->open = false;
     if (S->s.nreg == 0) return LMR_OK;
-    return hip_status(launch_stage_finish(carve_tiled_ws(ctx->ws, ctx->rec_cap), S->s,
+    return hip_status(launch_stage_finish(ctx_ws(ctx, ctx->rec_cap), S->s,
                                           reinterpret_cast<hipStream_t>(stream)));
 }
 

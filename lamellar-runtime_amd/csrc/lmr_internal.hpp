@@ -31,6 +31,9 @@ struct lmr_ctx {
     lmr::WinState* win = nullptr;      // window partition of shards above one tiled window, lazily made
     lmr::WireBufs* wire = nullptr;     // staging of lmr_apply_msg (AM wire format), lazily made
     lmr::OrdBufs* ord = nullptr;       // sort buffers of the ordered apply (n > 1024), see ord_reserve
+    // side lane of the tile sweep: the delta pieces of hot tiles run beside the owner tiles
+    hipStream_t side = nullptr;
+    hipEvent_t side_fork = nullptr, side_join = nullptr;
 };
 
 namespace lmr {
@@ -58,6 +61,12 @@ struct ProfScope {
     }
     ~ProfScope() { end(); }
     void end() { if (p) prof_end(p, st, s, n); p = nullptr; }
+};
+
+// A second stream (and its fork / join events) a launch may run independent work on.
+struct SideLane {
+    hipStream_t s = nullptr;
+    hipEvent_t fork = nullptr, join = nullptr;
 };
 
 // Workspace carve-up of one tiled piece.
@@ -90,6 +99,7 @@ struct TiledWs {
     uint32_t* rfill;       // staged apply: [kMaxRegions][kMaxTiles] each region's fine-pass tile fills
     uint64_t cap;          // records of one tiled piece (bin arrays, position maps)
     uint64_t tmp_cap;      // records the temp arrays (tmp_idx / tmp_val) hold, > cap
+    SideLane side;         // the context's side lane (null: everything on the launch stream)
 };
 size_t tiled_ws_bytes(uint64_t cap);
 // largest workspace capacity (records) whose temp slots fit the kernels' uint32 slot math

@@ -3,6 +3,7 @@
 // lmr_apply.hip so the two translation units compile in parallel.
 #include "lmr_tile.hpp"
 #include "lmr_device.hpp"
+#include <cstdlib>
 
 // k_tile_owner reads 4 binned records per thread with wide loads (0: one record at a time)
 #ifndef LMR_OWN_VEC
@@ -422,19 +423,41 @@ static unsigned grid_for(uint64_t n, unsigned block, unsigned cap) {
 }
 
 
-hipError_t launch_tile_kernels(int dtype, int opt, const TileArgs& t, bool delta, unsigned dgrid, hipStream_t s) {
-    return dispatch_dtype_t(dtype, [&](auto tag) {
+// The delta pieces (hot tiles, device atomics and LDS combining: latency-bound) run on the side
+// lane beside the owner tiles (HBM-bound); the owner kernel skips the split tiles, so the two
+// touch disjoint tiles, records and results. LMR_DELTA_SIDE=0 keeps both on the launch stream.
+static bool delta_side_enabled() {
+    static const bool on = [] {
+        const char* v = getenv("LMR_DELTA_SIDE");
+        return !(v && v[0] == '0');
+    }();
+    return on;
+}
+
+hipError_t launch_tile_kernels(int dtype, int opt, const TileArgs& t, bool delta, unsigned dgrid, hipStream_t s,
+                               const SideLane& side) {
+    const bool lane = delta && side.s && delta_side_enabled();
+    if (lane && (hipEventRecord(side.fork, s) != hipSuccess || hipStreamWaitEvent(side.s, side.fork, 0) != hipSuccess))
+        return hipErrorUnknown;
+    const hipError_t e = dispatch_dtype_t(dtype, [&](auto tag) {
         using Ty = decltype(tag);
         auto go = [&](auto optc) {
             constexpr int OPT = decltype(optc)::value;
+            if (lane)          // first, so its blocks start while the owner grid fills the chip
+                hipLaunchKernelGGL((k_tile_delta<Ty, OPT>), dim3(dgrid), dim3(1024), size_t(kTileBytes), side.s, t);
             hipLaunchKernelGGL((k_tile_owner<Ty, OPT>), dim3(t.num_tiles), dim3(1024), size_t(kTileBytes), s, t);
-            if (delta) hipLaunchKernelGGL((k_tile_delta<Ty, OPT>), dim3(dgrid), dim3(1024), size_t(kTileBytes), s, t);
+            if (delta && !lane)
+                hipLaunchKernelGGL((k_tile_delta<Ty, OPT>), dim3(dgrid), dim3(1024), size_t(kTileBytes), s, t);
         };
         if (opt == LMR_OP_ADD) go(std::integral_constant<int, LMR_OP_ADD>{});
         else if (opt == LMR_OP_FETCH_ADD) go(std::integral_constant<int, LMR_OP_FETCH_ADD>{});
         else go(std::integral_constant<int, -1>{});
         return hipGetLastError();
     });
+    // the launch stream continues after both (joined even when a launch failed)
+    if (lane && (hipEventRecord(side.join, side.s) != hipSuccess || hipStreamWaitEvent(s, side.join, 0) != hipSuccess))
+        return e != hipSuccess ? e : hipErrorUnknown;
+    return e;
 }
 
 }  // namespace lmr

@@ -66,9 +66,11 @@ __host__ __device__ constexpr bool op_combines(int op) {
            op == LMR_OP_XOR || op == LMR_OP_FETCH_XOR;
 }
 
-// k_tile_owner over every tile (+ k_tile_delta over the delta pieces when `delta`);
+// k_tile_owner over every tile (+ k_tile_delta over the delta pieces when `delta`, on the
+// side lane when there is one: the two kernels touch disjoint tiles and records);
 // opt: LMR_OP_ADD / LMR_OP_FETCH_ADD select the specialised kernels, anything else the
 // generic op switch
-hipError_t launch_tile_kernels(int dtype, int opt, const TileArgs& t, bool delta, unsigned dgrid, hipStream_t s);
+hipError_t launch_tile_kernels(int dtype, int opt, const TileArgs& t, bool delta, unsigned dgrid, hipStream_t s,
+                               const SideLane& side);
 
 }  // namespace lmr
