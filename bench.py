@@ -60,6 +60,8 @@ def parse():
     p.add_argument("--cpu-sample-log2", type=int, default=25)
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-verify", action="store_true")
+    p.add_argument("--no-other-configs", action="store_true",
+                   help="default run only: skip the short C3 / C5 lines (other_configs)")
     p.add_argument("--e2e", action="store_true",
                    help="also time the host-buffer path: pinned host records -> H2D copy -> op")
     return p.parse_args()
@@ -552,6 +554,9 @@ def main():
     }
     if args.e2e and cfg in ("c2", "c4"):
         out["e2e"] = e2e(lam, team, W, args)
+    if args.config is None and npes == 1 and not args.no_other_configs:
+        del W
+        out["other_configs"] = other_configs(lam, world, team, args)
     if me == 0 and npes == 1 and not args.no_cpu_baseline:
         cb = cpu_baseline(args, cfg)
         out["cpu_baseline"] = cb.get("primary")
@@ -563,6 +568,41 @@ def main():
     if dist.is_available() and dist.is_initialized():
         dist.barrier()
         dist.destroy_process_group()
+
+
+def other_configs(lam, world, team, args):
+    """The default run (N = 1, C2) also times BASELINE.json's other single-GPU configurations
+    (C3, C5) with the same clock, fewer steps and no profiling: short reported lines beside the
+    headline, each verified against its checker after its timed steps."""
+    k = team.kernels
+    dev = k.device
+    res = {}
+    for cfg, cls in (("c3", FetchAddZipf), ("c5", MixedU32)):
+        try:
+            W = cls(lam, team, args)
+            W.setup()
+            k.reserve(W.n)
+            steps, warm = 10, 3
+            for _ in range(warm):
+                W.step()
+            world.wait_all()
+            torch.cuda.synchronize(dev)
+            t0 = time.perf_counter()
+            for _ in range(steps):
+                W.step()
+            world.wait_all()
+            torch.cuda.synchronize(dev)
+            el = time.perf_counter() - t0
+            ms = el / steps * 1e3
+            res[cfg] = {"workload": W.describe(), "ms_per_step": ms, "value": W.ops_per_step * steps / el,
+                        "unit": "ops/s", "steps": steps, "warmup": warm, "dtype": W.dtype,
+                        "roofline_frac": W.survey_bpo * W.ops_per_step / (ms * 1e-3) / HBM_PEAK,
+                        "bytes_per_op": W.survey_bpo, "verified": W.verify(warm + steps)}
+            del W
+            torch.cuda.empty_cache()
+        except Exception as e:  # a failing side line never costs the headline line
+            res[cfg] = {"error": f"{type(e).__name__}: {e}"}
+    return res
 
 
 def e2e(lam, team, W, args):

@@ -118,6 +118,19 @@ __device__ __forceinline__ T lds_acc_wave(typename word_of<T>::W* tile, uint32_t
     return res;
 }
 
+// the identity of addition: -0.0 for floats (-0.0 + x == x for every x, signed zeros included)
+template <typename T>
+__device__ __forceinline__ T add_ident() {
+    using U = typename bits_of<T>::U;
+    if constexpr (is_flt<T>::v) return from_bits<T>(U(U(1) << (8 * sizeof(U) - 1)));
+    else return T(0);
+}
+
+#ifndef LMR_OWN_COMBINE
+#define LMR_OWN_COMBINE 1
+#endif
+constexpr bool kOwnCombine = LMR_OWN_COMBINE != 0;   // wave-combined add in the owner kernel (A/B: -D...=0)
+
 // OPT >= 0 fixes the op at compile time (hot paths); -1 reads it from the args.
 // Owner mode: one block per tile — load the tile into LDS, apply the tile's
 // records with LDS atomics, write it back. Kept free of the delta path's
@@ -228,7 +241,13 @@ __global__ __launch_bounds__(1024, 8) void k_tile_owner(TileArgs a) {
             continue;
         }
     }
-    for (uint32_t r0 = lo + threadIdx.x; r0 < hi; r0 += kOwnUnroll * 1024u) {
+    // add / fetch_add (compile-time op): a wave's records on one element (Zipf-warm elements of
+    // an owner tile) are combined with a wave scan and applied with one LDS atomic (lds_acc_wave:
+    // each record returns base (+) the values before it in the group, applied as one step); the
+    // loop is block-uniform so every lane of a wave takes part in the scan
+    constexpr bool kComb = kOwnCombine && (OPT == LMR_OP_ADD || OPT == LMR_OP_FETCH_ADD);
+    for (uint32_t b0 = lo; b0 < hi; b0 += kOwnUnroll * 1024u) {
+        const uint32_t r0 = b0 + threadIdx.x;
         uint32_t l[kOwnUnroll];
         T v[kOwnUnroll];
 #pragma unroll
@@ -240,7 +259,11 @@ __global__ __launch_bounds__(1024, 8) void k_tile_owner(TileArgs a) {
 #pragma unroll
         for (int k = 0; k < kOwnUnroll; k++) {
             const uint32_t r = r0 + uint32_t(k) * 1024u;
-            if (r < hi) {
+            if constexpr (kComb) {
+                const bool in = r < hi;
+                const T old = lds_acc_wave<T>(tile, l[k], v[k], in, LMR_OP_FETCH_ADD, add_ident<T>(), a.kind, a.err);
+                if (in && ret != LMR_RET_NONE) reinterpret_cast<T*>(a.results)[r] = old;
+            } else if (r < hi) {
                 uint8_t ok = 0;
                 T old = rmw_lds<T>(tile + l[k], op, a.kind, v[k], cmp, eps, ok, a.err);
                 if (ret != LMR_RET_NONE) {
