@@ -126,10 +126,12 @@ __device__ __forceinline__ T add_ident() {
     else return T(0);
 }
 
+// Off: measured no better (same box, alternating, profiles/r4/ab/r4l_*: C3 tile sweep 0.428-0.429 ->
+// 0.433-0.435 ms, C2 unchanged): the owner tiles' warm elements are not where their time goes
 #ifndef LMR_OWN_COMBINE
-#define LMR_OWN_COMBINE 1
+#define LMR_OWN_COMBINE 0
 #endif
-constexpr bool kOwnCombine = LMR_OWN_COMBINE != 0;   // wave-combined add in the owner kernel (A/B: -D...=0)
+constexpr bool kOwnCombine = LMR_OWN_COMBINE != 0;   // wave-combined add in the owner kernel (A/B: -D...=1)
 
 // OPT >= 0 fixes the op at compile time (hot paths); -1 reads it from the args.
 // Owner mode: one block per tile — load the tile into LDS, apply the tile's
