@@ -60,6 +60,8 @@ def parse():
     p.add_argument("--cpu-sample-log2", type=int, default=25)
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-verify", action="store_true")
+    p.add_argument("--reserve-log2", type=int, default=None,
+                   help="workspace reservation (records, log2) when above the step's records")
     p.add_argument("--no-other-configs", action="store_true",
                    help="default run only: skip the short C3 / C5 lines (other_configs)")
     p.add_argument("--e2e", action="store_true",
@@ -448,7 +450,7 @@ def main():
     cfg = args.config or ("c2" if npes == 1 else "c4")
     W = {"c2": AddUniform, "c4": AddUniform, "c3": FetchAddZipf, "c5": MixedU32}[cfg](lam, team, args)
     W.setup()
-    k.reserve(W.n)
+    k.reserve(max(W.n, 1 << args.reserve_log2) if args.reserve_log2 else W.n)
     world.barrier()
 
     for _ in range(args.warmup):

@@ -23,7 +23,11 @@ struct Prof {
     hipEvent_t get() {
         if (next == pool.size()) {
             hipEvent_t e = nullptr;
-            if (hipEventCreate(&e) != hipSuccess) return nullptr;
+            // device-scope release: the stage events only time kernels, and a system-scope fence
+            // (the default) writes back and invalidates the caches at every stage boundary
+            if (hipEventCreateWithFlags(&e, device_scope_events() ? hipEventReleaseToDevice : hipEventDefault) !=
+                hipSuccess)
+                return nullptr;
             pool.push_back(e);
         }
         return pool[next++];
@@ -318,8 +322,8 @@ lmr_status_t lmr_ctx_create(int device, lmr_ctx_t** out) {
     if (hipMemset(p, 0, pack_scratch_bytes()) != hipSuccess) { (void)hipFree(p); delete c; return LMR_E_HIP; }
     if (ord_reserve(c, kOrderedMinPiece) != hipSuccess ||
         hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking) != hipSuccess ||
-        hipEventCreateWithFlags(&c->side_fork, hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&c->side_join, hipEventDisableTiming) != hipSuccess) {
+        hipEventCreateWithFlags(&c->side_fork, side_event_flags()) != hipSuccess ||
+        hipEventCreateWithFlags(&c->side_join, side_event_flags()) != hipSuccess) {
         lmr_ctx_destroy(c);
         return LMR_E_HIP;
     }

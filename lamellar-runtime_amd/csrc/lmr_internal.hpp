@@ -1,6 +1,7 @@
 // lmr_internal.hpp — host-side internals shared by the .hip translation units
 // of liblamellar_gpu_ops.so (not part of the C ABI).
 #pragma once
+#include <cstdlib>
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stddef.h>
@@ -37,6 +38,20 @@ struct lmr_ctx {
 };
 
 namespace lmr {
+
+// Events that only order kernels on two streams of one device (the side lane) or only time
+// kernels (stage profiling) need no system-scope fence; LMR_EVENT_SCOPE=system keeps HIP's
+// default one (A/B).
+inline bool device_scope_events() {
+    static const bool on = [] {
+        const char* v = getenv("LMR_EVENT_SCOPE");
+        return !(v && v[0] == 's');
+    }();
+    return on;
+}
+inline unsigned side_event_flags() {
+    return hipEventDisableTiming | (device_scope_events() ? hipEventDisableSystemFence : 0u);
+}
 
 // ---- tiling constants (gfx950: 160 KiB LDS per CU; two 64 KiB tiles per CU) ----
 constexpr int kTileBytes = 64 * 1024;
