@@ -1153,63 +1153,88 @@ static uint64_t rt_rounds_for(uint64_t cap) { return cap / 4096 + uint64_t(kMaxR
 // coarse rounds of staged regions (>= 4K records each, one partial round per producer block of <= 64K)
 static uint64_t crt_rounds_for(uint64_t cap) { return cap / 4096 + cap / 65536 + uint64_t(kMaxRegions) * 2; }
 
-size_t tiled_ws_bytes(uint64_t cap) {
-    size_t b = 0;
+// The workspace layout, in one place: ws_layout(cap, base, &w) carves it, ws_layout(cap) sizes it.
+// Measurement knobs: LMR_WS_PAD_KB = P puts P KiB x (i + 1) of padding after the i-th record
+// array (staggered starts), LMR_WS_LAYOUT_LOG2 = L spaces the record arrays as for 2^L records.
+static size_t ws_env(const char* name) {
+    const char* v = getenv(name);
+    return v && *v ? size_t(atol(v)) : 0;
+}
+static size_t ws_layout(uint64_t cap, uint8_t* base = nullptr, TiledWs* w = nullptr) {
+    static const size_t pad_kb = ws_env("LMR_WS_PAD_KB");
+    static const size_t lay_log2 = ws_env("LMR_WS_LAYOUT_LOG2");
+    const uint64_t lcap = lay_log2 && (uint64_t(1) << lay_log2) > cap ? uint64_t(1) << lay_log2 : cap;
     auto al = [](size_t x) { return (x + 255) & ~size_t(255); };
-    b += al(size_t(kMaxTiles) * kMaxBinBlocks * 4);                         // counts
-    b += al(scan_scratch_words(size_t(kMaxTiles) * kMaxBinBlocks) * 4);     // scan scratch (zeroed)
-    b += al((size_t(kMaxTiles) + 1) * 4);                                   // tile_start
-    b += al(cap * 2) + al(cap * 8) + al(cap * 4) + al(4);
-    b += al((size_t(kMaxCoarse) * kMaxBinBlocks + 1) * 4);
-    b += al(tmp_cap_for(cap) * 4) + al(tmp_cap_for(cap) * 8) + al(cap * 4);
-    b += 2 * al((size_t(kMaxTiles) + 1) * 4) + al(size_t(kMaxTiles) / kScanItems * 4 + 256) + al(4);
-    b += al((size_t(kMaxTiles) + 2 * (cap / kSplit) + 2) * 16);   // owner items + delta pieces
-    b += al(size_t(kMaxRegions) * (kMaxTiles + 1) * 4);             // staged regions' tile starts
-    b += al(size_t(kStageInfoWords) * 4);                            // staged piece table / totals
-    b += al(ff_words() * 4);                                         // count-free fill counters
-    b += al(rt_rounds_for(cap) * 256 * 4);                           // staged run tables
-    b += al(size_t(kMaxRegions) * 2 * (kMaxCoarse + 1) * 4);         // staged piece tables
-    b += al(crt_rounds_for(cap) * 256 * 4);                          // staged coarse run tables
-    b += 2 * al(size_t(kMaxRegions) * kMaxTiles * 4);                // staged regions' tile totals, fills
-    return b;
+    size_t off = 0;
+    int arr = 0;
+    auto take = [&](size_t bytes, bool rec_array = false) {
+        const size_t o = off;
+        off += al(bytes);
+        if (rec_array) off += pad_kb * 1024 * size_t(++arr);
+        return base ? base + o : nullptr;
+    };
+    uint8_t* counts = take(size_t(kMaxTiles) * kMaxBinBlocks * 4);
+    uint8_t* partials = take(scan_scratch_words(size_t(kMaxTiles) * kMaxBinBlocks) * 4);
+    uint8_t* tile_start = take((size_t(kMaxTiles) + 1) * 4);
+    uint8_t* bin_lidx = take(lcap * 2, true);
+    uint8_t* bin_val = take(lcap * 8, true);
+    uint8_t* rpos = take(lcap * 4, true);
+    uint8_t* total = take(4);
+    uint8_t* coarse_off = take((size_t(kMaxCoarse) * kMaxBinBlocks + 1) * 4);
+    uint8_t* tmp_idx = take(tmp_cap_for(lcap) * 4, true);
+    uint8_t* tmp_val = take(tmp_cap_for(lcap) * 8, true);
+    uint8_t* qpos = take(lcap * 4, true);
+    uint8_t* tile_items = take((size_t(kMaxTiles) + 1) * 4);
+    uint8_t* tile_items2 = take((size_t(kMaxTiles) + 1) * 4);
+    uint8_t* plan_partials = take(size_t(kMaxTiles) / kScanItems * 4 + 256);
+    uint8_t* item_count = take(4);
+    uint8_t* items = take((size_t(kMaxTiles) + 2 * (cap / kSplit) + 2) * 16);   // owner items + delta pieces
+    uint8_t* rts = take(size_t(kMaxRegions) * (kMaxTiles + 1) * 4);             // staged regions' tile starts
+    uint8_t* sinfo = take(size_t(kStageInfoWords) * 4);                          // staged piece table / totals
+    uint8_t* ff = take(ff_words() * 4);                                          // count-free fill counters
+    uint8_t* runtab = take(rt_rounds_for(cap) * 256 * 4);                       // staged run tables
+    uint8_t* ptab = take(size_t(kMaxRegions) * 2 * (kMaxCoarse + 1) * 4);       // staged piece tables
+    uint8_t* crtab = take(crt_rounds_for(cap) * 256 * 4);                       // staged coarse run tables
+    uint8_t* rtot = take(size_t(kMaxRegions) * kMaxTiles * 4);                  // staged regions' tile totals
+    uint8_t* rfill = take(size_t(kMaxRegions) * kMaxTiles * 4);                 //   and fills
+    if (w) {
+        w->counts = reinterpret_cast<uint32_t*>(counts);
+        w->partials = reinterpret_cast<uint32_t*>(partials);
+        w->tile_start = reinterpret_cast<uint32_t*>(tile_start);
+        w->bin_lidx = reinterpret_cast<uint16_t*>(bin_lidx);
+        w->bin_val = bin_val;
+        w->rpos = reinterpret_cast<uint32_t*>(rpos);
+        w->total = reinterpret_cast<uint32_t*>(total);
+        w->coarse_off = reinterpret_cast<uint32_t*>(coarse_off);
+        w->tmp_idx = reinterpret_cast<uint32_t*>(tmp_idx);
+        w->tmp_val = tmp_val;
+        w->qpos = reinterpret_cast<uint32_t*>(qpos);
+        w->tile_items = reinterpret_cast<uint32_t*>(tile_items);
+        w->tile_items2 = reinterpret_cast<uint32_t*>(tile_items2);
+        w->plan_partials = reinterpret_cast<uint32_t*>(plan_partials);
+        w->item_count = reinterpret_cast<uint32_t*>(item_count);
+        w->items = items;
+        w->rts = reinterpret_cast<uint32_t*>(rts);
+        w->sinfo = reinterpret_cast<uint32_t*>(sinfo);
+        w->ff = reinterpret_cast<uint32_t*>(ff);
+        w->runtab = reinterpret_cast<uint32_t*>(runtab);
+        w->rt_rounds = rt_rounds_for(cap);
+        w->ptab = reinterpret_cast<uint32_t*>(ptab);
+        w->crtab = reinterpret_cast<uint32_t*>(crtab);
+        w->crt_rounds = crt_rounds_for(cap);
+        w->rtot = reinterpret_cast<uint32_t*>(rtot);
+        w->rfill = reinterpret_cast<uint32_t*>(rfill);
+        w->cap = cap;
+        w->tmp_cap = tmp_cap_for(cap);
+    }
+    return off;
 }
 
+size_t tiled_ws_bytes(uint64_t cap) { return ws_layout(cap); }
+
 TiledWs carve_tiled_ws(uint8_t* base, uint64_t cap) {
-    auto al = [](size_t x) { return (x + 255) & ~size_t(255); };
     TiledWs w;
-    uint8_t* p = base;
-    w.counts = reinterpret_cast<uint32_t*>(p); p += al(size_t(kMaxTiles) * kMaxBinBlocks * 4);
-    w.partials = reinterpret_cast<uint32_t*>(p);
-    p += al(scan_scratch_words(size_t(kMaxTiles) * kMaxBinBlocks) * 4);
-    w.tile_start = reinterpret_cast<uint32_t*>(p); p += al((size_t(kMaxTiles) + 1) * 4);
-    w.bin_lidx = reinterpret_cast<uint16_t*>(p); p += al(cap * 2);
-    w.bin_val = p; p += al(cap * 8);
-    w.rpos = reinterpret_cast<uint32_t*>(p); p += al(cap * 4);
-    w.total = reinterpret_cast<uint32_t*>(p); p += al(4);
-    w.coarse_off = reinterpret_cast<uint32_t*>(p); p += al((size_t(kMaxCoarse) * kMaxBinBlocks + 1) * 4);
-    w.tmp_idx = reinterpret_cast<uint32_t*>(p); p += al(tmp_cap_for(cap) * 4);
-    w.tmp_val = p; p += al(tmp_cap_for(cap) * 8);
-    w.qpos = reinterpret_cast<uint32_t*>(p); p += al(cap * 4);
-    w.tile_items = reinterpret_cast<uint32_t*>(p); p += al((size_t(kMaxTiles) + 1) * 4);
-    w.tile_items2 = reinterpret_cast<uint32_t*>(p); p += al((size_t(kMaxTiles) + 1) * 4);
-    w.plan_partials = reinterpret_cast<uint32_t*>(p); p += al(size_t(kMaxTiles) / kScanItems * 4 + 256);
-    w.item_count = reinterpret_cast<uint32_t*>(p); p += al(4);
-    w.items = p;                                   // [kMaxTiles] owner items, then delta pieces
-    p += al((size_t(kMaxTiles) + 2 * (cap / kSplit) + 2) * 16);
-    w.rts = reinterpret_cast<uint32_t*>(p); p += al(size_t(kMaxRegions) * (kMaxTiles + 1) * 4);
-    w.sinfo = reinterpret_cast<uint32_t*>(p); p += al(size_t(kStageInfoWords) * 4);
-    w.ff = reinterpret_cast<uint32_t*>(p); p += al(ff_words() * 4);
-    w.runtab = reinterpret_cast<uint32_t*>(p); p += al(rt_rounds_for(cap) * 256 * 4);
-    w.ptab = reinterpret_cast<uint32_t*>(p);
-    w.rt_rounds = rt_rounds_for(cap);
-    p += al(size_t(kMaxRegions) * 2 * (kMaxCoarse + 1) * 4);
-    w.crtab = reinterpret_cast<uint32_t*>(p);
-    w.crt_rounds = crt_rounds_for(cap);
-    p += al(crt_rounds_for(cap) * 256 * 4);
-    w.rtot = reinterpret_cast<uint32_t*>(p); p += al(size_t(kMaxRegions) * kMaxTiles * 4);
-    w.rfill = reinterpret_cast<uint32_t*>(p);
-    w.cap = cap;
-    w.tmp_cap = tmp_cap_for(cap);
+    ws_layout(cap, base, &w);
     return w;
 }
 

@@ -344,7 +344,7 @@ lmr_status_t lmr_ctx_destroy(lmr_ctx_t* ctx) {
     if (ctx->side_fork) (void)hipEventDestroy(ctx->side_fork);
     if (ctx->side_join) (void)hipEventDestroy(ctx->side_join);
     if (ctx->side) (void)hipStreamDestroy(ctx->side);
-    if (ctx->ws) (void)hipFree(ctx->ws);
+    if (ctx->ws_alloc) (void)hipFree(ctx->ws_alloc);
     if (ctx->d_err) (void)hipFree(ctx->d_err);
     if (ctx->prof) {
         for (hipEvent_t e : ctx->prof->pool) (void)hipEventDestroy(e);
@@ -359,13 +359,20 @@ lmr_status_t lmr_ctx_reserve(lmr_ctx_t* ctx, uint64_t max_records) {
     if (max_records > max_rec_cap()) max_records = max_rec_cap();
     if (ctx->stage && ctx->stage->s.nreg > 0) return LMR_E_INVALID;   // staged records live in the workspace
     (void)hipSetDevice(ctx->device);
-    if (ctx->ws) { (void)hipFree(ctx->ws); ctx->ws = nullptr; ctx->ws_bytes = 0; ctx->rec_cap = 0; }
+    if (ctx->ws_alloc) (void)hipFree(ctx->ws_alloc);
+    ctx->ws = ctx->ws_alloc = nullptr; ctx->ws_bytes = 0; ctx->rec_cap = 0;
     if (max_records == 0) return LMR_OK;
     if (ord_reserve(ctx, max_records) != hipSuccess) return LMR_E_HIP;
     size_t b = tiled_ws_bytes(max_records);
+    // (measurement knobs: LMR_WS_EXTRA_MB allocates more than the layout needs, LMR_WS_SHIFT_KB
+    // starts the layout that far into the allocation)
+    const char* ex = getenv("LMR_WS_EXTRA_MB");
+    const char* sh = getenv("LMR_WS_SHIFT_KB");
+    const size_t extra = ex ? size_t(atol(ex)) << 20 : 0, shift = sh ? size_t(atol(sh)) << 10 : 0;
     void* p = nullptr;
-    if (hipMalloc(&p, b) != hipSuccess) return LMR_E_HIP;
-    ctx->ws = reinterpret_cast<uint8_t*>(p);
+    if (hipMalloc(&p, b + extra + shift) != hipSuccess) return LMR_E_HIP;
+    ctx->ws_alloc = reinterpret_cast<uint8_t*>(p);
+    ctx->ws = ctx->ws_alloc + shift;
     ctx->ws_bytes = b;
     {   // the scan's look-back scratch starts zeroed (every scan leaves it so)
         const TiledWs w = ctx_ws(ctx, max_records);

@@ -22,6 +22,7 @@ struct lmr_ctx {
     uint32_t* d_err = nullptr;     // device error word (LMR_ERRBIT_*)
     // tiled-apply / pack workspace (allocated by lmr_ctx_reserve, never on the hot path)
     uint8_t* ws = nullptr;
+    uint8_t* ws_alloc = nullptr;   // the allocation ws lies in (hipFree)
     size_t ws_bytes = 0;
     uint64_t rec_cap = 0;          // records one tiled piece may hold
     int num_cus = 256;
