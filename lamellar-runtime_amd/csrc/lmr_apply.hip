@@ -1154,36 +1154,27 @@ static uint64_t rt_rounds_for(uint64_t cap) { return cap / 4096 + uint64_t(kMaxR
 static uint64_t crt_rounds_for(uint64_t cap) { return cap / 4096 + cap / 65536 + uint64_t(kMaxRegions) * 2; }
 
 // The workspace layout, in one place: ws_layout(cap, base, &w) carves it, ws_layout(cap) sizes it.
-// Measurement knobs: LMR_WS_PAD_KB = P puts P KiB x (i + 1) of padding after the i-th record
-// array (staggered starts), LMR_WS_LAYOUT_LOG2 = L spaces the record arrays as for 2^L records.
-static size_t ws_env(const char* name) {
-    const char* v = getenv(name);
-    return v && *v ? size_t(atol(v)) : 0;
-}
+// (Measured and not kept, profiles/r4/ab/r4p_*, r4q_*: staggered padding between the record arrays,
+// their spacing as for a larger capacity, a larger allocation or a shifted base: all within 0.5 %.)
 static size_t ws_layout(uint64_t cap, uint8_t* base = nullptr, TiledWs* w = nullptr) {
-    static const size_t pad_kb = ws_env("LMR_WS_PAD_KB");
-    static const size_t lay_log2 = ws_env("LMR_WS_LAYOUT_LOG2");
-    const uint64_t lcap = lay_log2 && (uint64_t(1) << lay_log2) > cap ? uint64_t(1) << lay_log2 : cap;
     auto al = [](size_t x) { return (x + 255) & ~size_t(255); };
     size_t off = 0;
-    int arr = 0;
-    auto take = [&](size_t bytes, bool rec_array = false) {
+    auto take = [&](size_t bytes) {
         const size_t o = off;
         off += al(bytes);
-        if (rec_array) off += pad_kb * 1024 * size_t(++arr);
         return base ? base + o : nullptr;
     };
     uint8_t* counts = take(size_t(kMaxTiles) * kMaxBinBlocks * 4);
     uint8_t* partials = take(scan_scratch_words(size_t(kMaxTiles) * kMaxBinBlocks) * 4);
     uint8_t* tile_start = take((size_t(kMaxTiles) + 1) * 4);
-    uint8_t* bin_lidx = take(lcap * 2, true);
-    uint8_t* bin_val = take(lcap * 8, true);
-    uint8_t* rpos = take(lcap * 4, true);
+    uint8_t* bin_lidx = take(cap * 2);
+    uint8_t* bin_val = take(cap * 8);
+    uint8_t* rpos = take(cap * 4);
     uint8_t* total = take(4);
     uint8_t* coarse_off = take((size_t(kMaxCoarse) * kMaxBinBlocks + 1) * 4);
-    uint8_t* tmp_idx = take(tmp_cap_for(lcap) * 4, true);
-    uint8_t* tmp_val = take(tmp_cap_for(lcap) * 8, true);
-    uint8_t* qpos = take(lcap * 4, true);
+    uint8_t* tmp_idx = take(tmp_cap_for(cap) * 4);
+    uint8_t* tmp_val = take(tmp_cap_for(cap) * 8);
+    uint8_t* qpos = take(cap * 4);
     uint8_t* tile_items = take((size_t(kMaxTiles) + 1) * 4);
     uint8_t* tile_items2 = take((size_t(kMaxTiles) + 1) * 4);
     uint8_t* plan_partials = take(size_t(kMaxTiles) / kScanItems * 4 + 256);

@@ -364,15 +364,10 @@ lmr_status_t lmr_ctx_reserve(lmr_ctx_t* ctx, uint64_t max_records) {
     if (max_records == 0) return LMR_OK;
     if (ord_reserve(ctx, max_records) != hipSuccess) return LMR_E_HIP;
     size_t b = tiled_ws_bytes(max_records);
-    // (measurement knobs: LMR_WS_EXTRA_MB allocates more than the layout needs, LMR_WS_SHIFT_KB
-    // starts the layout that far into the allocation)
-    const char* ex = getenv("LMR_WS_EXTRA_MB");
-    const char* sh = getenv("LMR_WS_SHIFT_KB");
-    const size_t extra = ex ? size_t(atol(ex)) << 20 : 0, shift = sh ? size_t(atol(sh)) << 10 : 0;
     void* p = nullptr;
-    if (hipMalloc(&p, b + extra + shift) != hipSuccess) return LMR_E_HIP;
+    if (hipMalloc(&p, b) != hipSuccess) return LMR_E_HIP;
     ctx->ws_alloc = reinterpret_cast<uint8_t*>(p);
-    ctx->ws = ctx->ws_alloc + shift;
+    ctx->ws = ctx->ws_alloc;
     ctx->ws_bytes = b;
     {   // the scan's look-back scratch starts zeroed (every scan leaves it so)
         const TiledWs w = ctx_ws(ctx, max_records);
