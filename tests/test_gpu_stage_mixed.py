@@ -249,3 +249,46 @@ def test_fused_partition_groups(world, lam):
         ref = _fold(op, ref, i, v)
     assert np.array_equal(shard.cpu().numpy().view(np.uint32), ref)
     assert stages["bin_count"][1] == 3 and stages["fine_scatter"][1] == 4, stages   # (+1: the free phase)
+
+
+def test_deferred_fetch_add_batches_one_sweep(world, lam, orc):
+    """Four deferred fetch_add batches (the bench's C3 pattern with a 4-batch workspace) with a
+    hot element (12 % of the records) and 64 warm ones: one session, one shard sweep (the hot
+    tile in delta pieces over the four regions, beside the owner tiles); the final state is the
+    sum and the four batches' olds are jointly a valid linearisation (concurrent batches, as the
+    reference's op AMs are)."""
+    team = world.team()
+    k = team.kernels
+    arr = lam.AtomicArray(team, L, lam.Distribution.Block, "u32")
+    rng = np.random.default_rng(4242)
+    nb = 1 << 19
+    s0 = rng.integers(0, 2**32, L, dtype=np.uint64).astype(np.uint32)
+    arr.local_data().copy_(torch.from_numpy(s0.view(np.int32)).to(k.device))
+    hot_el = int(rng.integers(0, L))
+    warm = rng.choice(L, 64, replace=False)
+    idxs, vals = [], []
+    for _ in range(4):
+        r = rng.random(nb)
+        w = warm[rng.integers(0, warm.size, nb)]
+        idxs.append(np.where(r < 0.12, hot_el, np.where(r < 0.3, w, rng.integers(0, L, nb))).astype(np.uint64))
+        vals.append(rng.integers(1, 9, nb, dtype=np.uint64).astype(np.uint32))
+    ti = lambda a: torch.from_numpy(a.astype(np.int64)).to(k.device)
+    tv = lambda a: torch.from_numpy(a.view(np.int32)).to(k.device)
+    k.reserve(4 * nb)
+    k.profile(True)
+    k.profile_read(reset=True)
+    try:
+        hs = [arr.batch_fetch_add(ti(i), tv(v)).spawn() for i, v in zip(idxs, vals)]
+        assert k._deferred is not None                    # nothing applied yet
+        rs = [h.block() for h in hs]
+        stages = k.profile_read(reset=True)
+    finally:
+        k.profile(False)
+    assert k.errors() == 0
+    assert stages["tile_apply"][1] == 1, stages         # one sweep for the four batches
+    final = arr.to_numpy()
+    iall, vall = np.concatenate(idxs), np.concatenate(vals)
+    rall = np.concatenate([r.cpu().numpy().view(np.uint32) for r in rs])
+    assert np.array_equal(final, _fold(ADD, s0, iall, vall))
+    st, bad = orc.check_linearizable(1, U32, np.uint32, FETCH_ADD, s0, final, iall, vall, rall)
+    assert st == 0, (st, bad)
