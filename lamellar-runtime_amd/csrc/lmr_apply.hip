@@ -780,7 +780,7 @@ struct FreeTable {
     FreeRegion r[kFuseFree];
     uint32_t nr;
 };
-template <int IW, int VB, int RPT>
+template <int IW, int VB, int RPT, bool PAIRS>
 __global__ __launch_bounds__(1024) void k_coarse_free_stage(PartArgs q, FreeTable t) {
     uint32_t i = 0;
     while (i + 1 < t.nr && t.r[i + 1].block0 <= blockIdx.x) i++;
@@ -789,7 +789,7 @@ __global__ __launch_bounds__(1024) void k_coarse_free_stage(PartArgs q, FreeTabl
     p.idx = g.idx; p.idx_stride = g.idx_stride; p.val = g.val; p.val_stride = g.val_stride;
     p.val_bits = g.val_bits; p.n = g.n; p.chunk = g.chunk; p.G = g.G;
     p.counts = q.counts + uint64_t(g.row0) * q.num_tiles;
-    coarse_free_body<IW, VB, RPT, false>(p, blockIdx.x - g.block0);
+    coarse_free_body<IW, VB, RPT, PAIRS>(p, blockIdx.x - g.block0);
 }
 
 // tile_start[t] = sum over blocks of the coarse pass's row counts (scanned after).
@@ -2228,6 +2228,21 @@ __global__ __launch_bounds__(1024) void k_stage_plan(const uint32_t* rts, uint32
 // once with device atomics (spill). The finish runs the tile totals, one k_fine_free
 // over all buckets and one tile sweep: no per-region counting and no piece tables.
 constexpr uint32_t kStageFreeBlocks = 256;
+// blocks of one grouped k_coarse_free_stage launch, shared by its regions (LMR_FREE_GROUP_BLOCKS)
+static uint32_t free_group_blocks() {
+    static int v = env_int("LMR_FREE_GROUP_BLOCKS", kMaxBinBlocks, 32, kMaxBinBlocks);
+    return uint32_t(v);
+}
+// blocks of a lone region's k_coarse_free_stage launch (LMR_FREE_BLOCKS)
+static uint32_t free_single_blocks() {
+    static int v = env_int("LMR_FREE_BLOCKS", kStageFreeBlocks, 16, kMaxBinBlocks);
+    return uint32_t(v);
+}
+// paired loads in the staged count-free pass (LMR_FREE_STAGE_PAIRS=0: one record per load)
+static bool free_stage_pairs() {
+    static int v = env_int("LMR_FREE_STAGE_PAIRS", 1, 0, 1);
+    return v != 0;
+}
 
 bool stage_free_applies(int dtype, int op, int ret, uint64_t shard_len, uint64_t cap) {
     return free_partition_applies(dtype, op, ret, shard_len, 0, cap);
@@ -2265,15 +2280,20 @@ static hipError_t stage_partition_free(const TiledWs& w, StageSession& s, hipStr
         int r1 = s.parted;
         while (r1 < s.nreg && r1 - s.parted < kFuseFree && s.pend[r1].iw == iw) r1++;
         const uint32_t nr = uint32_t(r1 - s.parted);
-        const uint32_t gcap = nr == 1 ? kStageFreeBlocks : std::max<uint32_t>(32, uint32_t(kMaxBinBlocks) / nr);
+        const uint32_t gcap = nr == 1 ? free_single_blocks() : std::max<uint32_t>(32, free_group_blocks() / nr);
         FreeTable t{};
         uint32_t rows = 0;
         uint64_t n_all = 0;
+        bool pairs = kCoarsePairs && iw == 8 && vb == 8 && (frpt % 2) == 0;
         for (uint32_t k = 0; k < nr; k++) {
             const ApplyArgs& a = s.pend[s.parted + int(k)].a;
             const uint32_t G = uint32_t(std::max<uint64_t>(1, std::min<uint64_t>((a.n + 16383) / 16384, gcap)));
-            t.r[k] = FreeRegion{a.idx, a.idx_stride, a.val, a.val_stride, a.val_bits, a.n, (a.n + G - 1) / G, G,
-                                rows, rows};
+            const uint64_t chunk = (a.n + G - 1) / G;
+            t.r[k] = FreeRegion{a.idx, a.idx_stride, a.val, a.val_stride, a.val_bits, a.n, chunk, G, rows, rows};
+            // paired 16-B loads (as the one-shot pass): contiguous, 16-B aligned u64 indices and
+            // values, and every block's range whole pairs (even chunks, even n)
+            pairs = pairs && a.idx_stride == 8 && a.val && a.val_stride == 8 && chunk % 2 == 0 && a.n % 2 == 0 &&
+                    ((reinterpret_cast<uintptr_t>(a.idx) | reinterpret_cast<uintptr_t>(a.val)) & 15) == 0;
             rows += G;
             n_all += a.n;
         }
@@ -2286,8 +2306,13 @@ static hipError_t stage_partition_free(const TiledWs& w, StageSession& s, hipStr
                 constexpr int IW = decltype(iwt)::value;
                 dispatch_vb_rpt<4>(vb, frpt, [&](auto vbt, auto rpt) {
                     constexpr int VBc = decltype(vbt)::value, R = decltype(rpt)::value;
-                    hipLaunchKernelGGL((k_coarse_free_stage<IW, VBc, R>), dim3(rows), dim3(1024),
-                                       size_t(q.num_tiles) * 4, st, q, t);
+                    constexpr bool kP = IW == 8 && VBc == 8 && R % 2 == 0;
+                    if (kP && pairs && free_stage_pairs())
+                        hipLaunchKernelGGL((k_coarse_free_stage<IW, VBc, R, kP>), dim3(rows), dim3(1024),
+                                           size_t(q.num_tiles) * 4, st, q, t);
+                    else
+                        hipLaunchKernelGGL((k_coarse_free_stage<IW, VBc, R, false>), dim3(rows), dim3(1024),
+                                           size_t(q.num_tiles) * 4, st, q, t);
                 });
                 return hipGetLastError();
             });
