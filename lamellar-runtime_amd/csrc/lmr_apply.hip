@@ -2228,9 +2228,19 @@ __global__ __launch_bounds__(1024) void k_stage_plan(const uint32_t* rts, uint32
 // once with device atomics (spill). The finish runs the tile totals, one k_fine_free
 // over all buckets and one tile sweep: no per-region counting and no piece tables.
 constexpr uint32_t kStageFreeBlocks = 256;
-// blocks of one grouped k_coarse_free_stage launch, shared by its regions (LMR_FREE_GROUP_BLOCKS)
+// blocks of one grouped k_coarse_free_stage launch, shared by its regions (LMR_FREE_GROUP_BLOCKS).
+// One block per CU in all (the pass holds 144 KB of LDS per block): every block zeroes and writes
+// a tile-count row and the tile totals read them all, so more blocks cost rows, not bandwidth.
+// Two C2 batches in one session, same box (profiles/r4/ab/r4v_*, r4w_*): 1024 blocks 3.40-3.42 ms,
+// 512 3.40, 256 3.06-3.21, 128 4.18-4.20; a lone region: 256 3.62, 128 4.42, 64 6.42 ms.
 static uint32_t free_group_blocks() {
-    static int v = env_int("LMR_FREE_GROUP_BLOCKS", kMaxBinBlocks, 32, kMaxBinBlocks);
+    static int v = env_int("LMR_FREE_GROUP_BLOCKS", kStageFreeBlocks, 32, kMaxBinBlocks);
+    return uint32_t(v);
+}
+// blocks per region when counted regions are partitioned together (LMR_COUNT_GROUP_BLOCKS: the
+// group's budget, split over its regions; 0 = each region its own count)
+static uint32_t count_group_blocks() {
+    static int v = env_int("LMR_COUNT_GROUP_BLOCKS", 0, 0, 8 * kMaxBinBlocks);
     return uint32_t(v);
 }
 // blocks of a lone region's k_coarse_free_stage launch (LMR_FREE_BLOCKS)
@@ -2380,12 +2390,17 @@ hipError_t launch_stage_partition(const TiledWs& w, StageSession& s, hipStream_t
         uint32_t cb = 0, gb = 0, fb = 0;
         uint64_t n_all = 0;
         int r = s.parted;
+        // a group's regions share a block budget (LMR_COUNT_GROUP_BLOCKS; 0: each region its own)
+        const uint32_t in_group = uint32_t(std::min<int>(kFuse, s.nreg - s.parted));
+        const uint64_t gbudget = count_group_blocks() && in_group > 1
+                                     ? std::max<uint64_t>(32, count_group_blocks() / in_group) : 0;
         for (; r < s.nreg && r - s.parted < kFuse && s.pend[r].iw == iw; r++) {
             const ApplyArgs& a = s.pend[r].a;
             StageRegion& g = s.reg[r];
             const bool has_res = a.ret != LMR_RET_NONE;
             uint64_t G = (a.n + 65535) / 65536;
             if (G > uint64_t(bin_blocks_cap(vb))) G = bin_blocks_cap(vb);
+            if (gbudget && G > gbudget) G = gbudget;
             if (G < 1) G = 1;
             // count blocks per producer block: one 1024-thread block per CU leaves a lone
             // region's read-only count pass at half occupancy (LMR_CCOUNT_SPLIT)
