@@ -60,10 +60,11 @@ def parse():
     p.add_argument("--cpu-sample-log2", type=int, default=25)
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-verify", action="store_true")
-    p.add_argument("--reserve-log2", type=int, default=28,
+    p.add_argument("--reserve-log2", type=int, default=29,
                    help="tiled-apply workspace (records, log2; 0: the step's records). The engine defers "
                         "large 1-PE batches into one staged session until the workspace is full, so a "
-                        "2^28-record workspace sweeps the shard once per four C3 batches (12 GB of HBM)")
+                        "2^29-record workspace (24 GB of HBM) sweeps the shard once per two C2 / eight C3 "
+                        "batches")
     p.add_argument("--no-other-configs", action="store_true",
                    help="default run only: skip the short C3 / C5 lines (other_configs)")
     p.add_argument("--e2e", action="store_true",

@@ -2237,11 +2237,15 @@ static uint32_t free_group_blocks() {
     static int v = env_int("LMR_FREE_GROUP_BLOCKS", kStageFreeBlocks, 32, kMaxBinBlocks);
     return uint32_t(v);
 }
-// blocks per region when counted regions are partitioned together (LMR_COUNT_GROUP_BLOCKS: the
-// group's budget, split over its regions; 0 = each region its own count)
-static uint32_t count_group_blocks() {
-    static int v = env_int("LMR_COUNT_GROUP_BLOCKS", 0, 0, 8 * kMaxBinBlocks);
-    return uint32_t(v);
+// Counted regions partitioned together share a block budget per pass (split over the group's
+// regions; LMR_COUNT_GROUP_BLOCKS overrides, 0 = each region its own count): as with the count-free
+// pass, every block adds count rows and a partial round per bucket, so a group of four to eight
+// regions runs best with few blocks each. Same box (profiles/r4/ab/r4x_count_groups.log), two
+// steps per session: C3 (8-byte values) 1.83 -> 1.68 ms at 512, 1.71 at 256; C5 (4-byte) 2.04 ->
+// 1.93 at 512, 1.81 at 256.
+static uint32_t count_group_blocks(int vb) {
+    static int v = env_int("LMR_COUNT_GROUP_BLOCKS", -1, -1, 8 * kMaxBinBlocks);
+    return v >= 0 ? uint32_t(v) : (vb == 8 ? 512u : 256u);
 }
 // blocks of a lone region's k_coarse_free_stage launch (LMR_FREE_BLOCKS)
 static uint32_t free_single_blocks() {
@@ -2392,8 +2396,8 @@ hipError_t launch_stage_partition(const TiledWs& w, StageSession& s, hipStream_t
         int r = s.parted;
         // a group's regions share a block budget (LMR_COUNT_GROUP_BLOCKS; 0: each region its own)
         const uint32_t in_group = uint32_t(std::min<int>(kFuse, s.nreg - s.parted));
-        const uint64_t gbudget = count_group_blocks() && in_group > 1
-                                     ? std::max<uint64_t>(32, count_group_blocks() / in_group) : 0;
+        const uint64_t gbudget = count_group_blocks(vb) && in_group > 1
+                                     ? std::max<uint64_t>(32, count_group_blocks(vb) / in_group) : 0;
         for (; r < s.nreg && r - s.parted < kFuse && s.pend[r].iw == iw; r++) {
             const ApplyArgs& a = s.pend[r].a;
             StageRegion& g = s.reg[r];
