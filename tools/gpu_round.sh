@@ -5,7 +5,7 @@
 #   check   <tag> [pytest selection]   the -m gpu suite (default: all of tests/) and smoke()
 #   bench   <tag> <cfg>...             bench lines (c4 = one-rank rehearsal, forced exchange)
 #   prof    <tag> <cfg>...             rocprofv3 kernel trace + separate FETCH_SIZE / WRITE_SIZE passes
-#   ab      <tag> <cfg> <reps> <spec>...  same-box A/B (tools/ab_mix.sh specs "<lib>|<env>")
+#   ab      <tag> <cfg> <reps> <spec>...  same-box A/B (tools/ab_mix.sh specs "<lib>|<env>[|<bench args>]")
 #   default <tag>                      the default bench line (N = 1, with its CPU baselines)
 cd "${GRAFT_REPO_ROOT:-.}"
 export PYTHONUNBUFFERED=1 TMPDIR=/tmp
