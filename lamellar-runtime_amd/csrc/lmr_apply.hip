@@ -2247,12 +2247,6 @@ static uint32_t count_group_blocks(int vb) {
     static int v = env_int("LMR_COUNT_GROUP_BLOCKS", -1, -1, 8 * kMaxBinBlocks);
     return v >= 0 ? uint32_t(v) : (vb == 8 ? 512u : 256u);
 }
-// fine-pass blocks of a group of counted regions, split over them (LMR_FINE_GROUP_BLOCKS; 0: each
-// region its own LMR_FINE_BLOCKS)
-static uint32_t fine_group_blocks() {
-    static int v = env_int("LMR_FINE_GROUP_BLOCKS", 0, 0, 8 * kMaxBinBlocks);
-    return uint32_t(v);
-}
 // blocks of a lone region's k_coarse_free_stage launch (LMR_FREE_BLOCKS)
 static uint32_t free_single_blocks() {
     static int v = env_int("LMR_FREE_BLOCKS", kStageFreeBlocks, 16, kMaxBinBlocks);
@@ -2453,9 +2447,9 @@ hipError_t launch_stage_partition(const TiledWs& w, StageSession& s, hipStream_t
             pa.rt = rounds ? w.runtab + s.rounds * (2 * kFine) : nullptr;
             pa.ptab = ptab;
             pa.rpp = rpp;
-            uint64_t fcap = uint64_t(fine_blocks_cap());
-            if (fine_group_blocks() && in_group > 1) fcap = std::min<uint64_t>(fcap, std::max<uint64_t>(32, fine_group_blocks() / in_group));
-            const uint32_t fgrid = uint32_t(std::min<uint64_t>(max_pieces, fcap));
+            // (a group budget for the fine pass as for count / coarse measured no better: the fine
+            // blocks are persistent over pieces, profiles/r4/ab/r4fa_*)
+            const uint32_t fgrid = uint32_t(std::min<uint64_t>(max_pieces, uint64_t(fine_blocks_cap())));
             ft.r[k] = FineRegion{pa, fb, fgrid};
             fb += fgrid;
             g.round_base = uint32_t(s.rounds);
