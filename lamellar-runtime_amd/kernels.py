@@ -7,6 +7,7 @@ is no CPU fallback; without a GPU the constructor raises.
 from __future__ import annotations
 
 import ctypes
+import os
 from ctypes import byref, c_uint32, c_uint64, c_void_p
 
 import torch
@@ -60,7 +61,8 @@ class DeviceKernels:
         self.ctx = c_void_p()
         check(self.lib.lmr_ctx_create(device.index or 0, byref(self.ctx)), "lmr_ctx_create")
         self.strategy = int(strategy)
-        self.max_ws_records = int(max_ws_records)
+        # (LAMELLAR_MAX_WS_RECORDS raises or lowers the cap, e.g. for deeper deferred sessions)
+        self.max_ws_records = int(os.environ.get("LAMELLAR_MAX_WS_RECORDS", max_ws_records))
         self.reserved = 0
         # the open deferred session of asynchronous batches (defer_soa): [shard key, (op, cmp, eps),
         # tensors its kernels still write or read]; applied by flush()
