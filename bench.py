@@ -60,6 +60,9 @@ def parse():
     p.add_argument("--cpu-sample-log2", type=int, default=25)
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-verify", action="store_true")
+    p.add_argument("--input-sets", type=int, default=0,
+                   help="distinct input buffers rotated over the steps (0: one per step of a deferred "
+                        "session, up to 8)")
     p.add_argument("--reserve-log2", type=int, default=29,
                    help="tiled-apply workspace (records, log2; 0: the step's records). The engine defers "
                         "large 1-PE batches into one staged session until the workspace is full, so a "
@@ -112,6 +115,31 @@ class Workload:
         g.manual_seed(0x1A3E11A2 + self.me)
         return g
 
+    t = 0          # steps issued (selects the input set)
+    sets = None    # distinct input buffers, one per step of a deferred session
+
+    def make_sets(self, nsets):
+        """Distinct copies of the step's records (each a random permutation of them, so every step
+        applies the same multiset and the verify invariants hold), rotated over consecutive steps:
+        the batches one deferred session sweeps together read different buffers, as distinct
+        batches of a real caller would, so none of them is served from a cache the previous
+        batch's pass left warm."""
+        g = torch.Generator(device=self.dev)
+        g.manual_seed(0x5E75 + self.me)
+        base = self.inputs()
+        self.sets = [base]
+        for _ in range(1, max(1, nsets)):
+            cp = []
+            for i, v in base:
+                perm = torch.randperm(i.numel(), device=self.dev, generator=g)
+                cp.append((i[perm].contiguous(), v[perm].contiguous()))
+            self.sets.append(cp)
+
+    def next_inputs(self):
+        s = self.sets[self.t % len(self.sets)] if self.sets else self.inputs()
+        self.t += 1
+        return s
+
 
 class AddUniform(Workload):
     """C2 (N = 1) / C4 (N > 1): u64 batch_add, uniform indices."""
@@ -128,8 +156,12 @@ class AddUniform(Workload):
         self.vals = torch.randint(-2**63, 2**63 - 1, (self.n,), dtype=torch.int64, device=self.dev, generator=g)
         self.ops_per_step = self.n
 
+    def inputs(self):
+        return [(self.idx, self.vals)]
+
     def step(self):
-        self.arr.batch_add(self.idx, self.vals).spawn()
+        (i, v), = self.next_inputs()
+        self.arr.batch_add(i, v).spawn()
 
     def verify(self, nsteps):
         # wrapping-sum invariant: sum(array) == steps * sum(vals), over all PEs (mod 2^64)
@@ -178,8 +210,12 @@ class FetchAddZipf(Workload):
         self.ops_per_step = self.n
         self.top_share = float((r == 0).float().mean())
 
+    def inputs(self):
+        return [(self.idx, self.vals)]
+
     def step(self):
-        self.last = self.arr.batch_fetch_add(self.idx, self.vals).spawn()
+        (i, v), = self.next_inputs()
+        self.last = self.arr.batch_fetch_add(i, v).spawn()
 
     def verify(self, nsteps):
         # exact with vals = 1.0: element = steps * (records hitting it, all PEs)
@@ -221,9 +257,12 @@ class MixedU32(Workload):
             self.parts.append((i, v))
         self.ops_per_step = 5 * m
 
+    def inputs(self):
+        return list(self.parts)
+
     def step(self):
         a = self.arr
-        (i0, v0), (i1, v1), (i2, v2), (i3, v3), (i4, v4) = self.parts
+        (i0, v0), (i1, v1), (i2, v2), (i3, v3), (i4, v4) = self.next_inputs()
         a.batch_bit_and(i0, v0).spawn()
         a.batch_bit_or(i1, v1).spawn()
         a.batch_bit_xor(i2, v2).spawn()
@@ -455,6 +494,7 @@ def main():
     W.setup()
     ws_records = max(W.n, 1 << args.reserve_log2) if args.reserve_log2 else W.n
     k.reserve(ws_records)
+    W.make_sets(input_sets(args, k.reserved, W.ops_per_step))
     world.barrier()
 
     for _ in range(args.warmup):
@@ -558,6 +598,7 @@ def main():
             "op": W.op_name,
             "strategy": args.strategy,
             "workspace_records": k.reserved,
+            "input_sets": len(W.sets) if W.sets else 1,
             "parallelism": f"{npes} PE(s), one per GPU",
         },
         "roofline": roof,
@@ -586,6 +627,13 @@ def main():
         dist.destroy_process_group()
 
 
+def input_sets(args, ws_records, ops_per_step):
+    """Distinct input sets: one per step a deferred session can hold (up to 8), or --input-sets."""
+    if args.input_sets:
+        return args.input_sets
+    return int(max(1, min(8, ws_records // max(1, ops_per_step))))
+
+
 def other_configs(lam, world, team, args):
     """The default run (N = 1, C2) also times BASELINE.json's other single-GPU configurations
     (C3, C5) with the same clock, fewer steps and no profiling: short reported lines beside the
@@ -598,6 +646,7 @@ def other_configs(lam, world, team, args):
             W = cls(lam, team, args)
             W.setup()
             k.reserve(W.n)
+            W.make_sets(input_sets(args, k.reserved, W.ops_per_step))
             steps, warm = 10, 3
             for _ in range(warm):
                 W.step()
