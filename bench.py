@@ -560,8 +560,7 @@ def main():
             "frac": achieved / HBM_PEAK, "traffic": traffic,
             "traffic_source": ("HBM bytes per step: committed rocprofv3 FETCH_SIZE/WRITE_SIZE passes "
                                f"(profiles/pmc_traffic_{cfg}.json, FETCH_SIZE x2 per the gfx950 note) x launches "
-                               "per step of this run; not measured in this run; the round-4 passes re-read "
-                               "one input buffer per step and read low, DESIGN.md §6") if traffic else None,
+                               "per step of this run; not measured in this run") if traffic else None,
             "scope": "whole step (every kernel of the op path), SURVEY 8(d) bytes per op",
             "bytes_per_op": W.survey_bpo, "ops_per_step": W.ops_per_step, "dominant_kernel": dom}
     stage_rows = {}
