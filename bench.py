@@ -68,6 +68,11 @@ def parse():
                         "large 1-PE batches into one staged session until the workspace is full, so a "
                         "2^29-record workspace (24 GB of HBM) sweeps the shard once per two C2 / eight C3 "
                         "batches")
+    p.add_argument("--inputs", default="owned", choices=["owned", "borrowed"],
+                   help="owned: each batch's input tensors are handed over with Owned(...) (the "
+                        "reference's by-value Vec input; the bench never changes them), so consecutive "
+                        "deferred batches are partitioned together; borrowed: plain tensors, each "
+                        "batch partitioned at its spawn")
     p.add_argument("--no-other-configs", action="store_true",
                    help="default run only: skip the short C3 / C5 lines (other_configs)")
     p.add_argument("--e2e", action="store_true",
@@ -138,6 +143,9 @@ class Workload:
     def next_inputs(self):
         s = self.sets[self.t % len(self.sets)] if self.sets else self.inputs()
         self.t += 1
+        if self.args.inputs == "owned":
+            own = self.lam.Owned
+            s = [(own(i), own(v)) for i, v in s]
         return s
 
 
@@ -598,6 +606,7 @@ def main():
             "strategy": args.strategy,
             "workspace_records": k.reserved,
             "input_sets": len(W.sets) if W.sets else 1,
+            "inputs": args.inputs,
             "parallelism": f"{npes} PE(s), one per GPU",
         },
         "roofline": roof,
@@ -636,16 +645,26 @@ def input_sets(args, ws_records, ops_per_step):
 def other_configs(lam, world, team, args):
     """The default run (N = 1, C2) also times BASELINE.json's other single-GPU configurations
     (C3, C5) with the same clock, fewer steps and no profiling: short reported lines beside the
-    headline, each verified against its checker after its timed steps."""
+    headline, each verified against its checker after its timed steps. Two more C2 lines: plain
+    (borrowed) input tensors, and one batch per sweep with no deferral at all (the latency of an
+    isolated 2^28-record batch)."""
+    from lamellar_runtime_amd import engine
     k = team.kernels
     dev = k.device
     res = {}
-    for cfg, cls in (("c3", FetchAddZipf), ("c5", MixedU32)):
+    lines = (("c3", FetchAddZipf, None), ("c5", MixedU32, None),
+             ("c2_borrowed", AddUniform, "borrowed"), ("c2_one_batch", AddUniform, "nodefer"))
+    for cfg, cls, mode in lines:
+        saved = (args.inputs, engine._DEFER)
         try:
+            if mode == "borrowed":
+                args.inputs = "borrowed"
+            elif mode == "nodefer":
+                engine._DEFER = False                     # every batch applied at its spawn
             W = cls(lam, team, args)
             W.setup()
             k.reserve(W.n)
-            W.make_sets(input_sets(args, k.reserved, W.ops_per_step))
+            W.make_sets(input_sets(args, k.reserved, W.ops_per_step) if mode != "nodefer" else 1)
             steps, warm = 10, 3
             for _ in range(warm):
                 W.step()
@@ -658,7 +677,12 @@ def other_configs(lam, world, team, args):
             torch.cuda.synchronize(dev)
             el = time.perf_counter() - t0
             ms = el / steps * 1e3
-            res[cfg] = {"workload": W.describe(), "ms_per_step": ms, "value": W.ops_per_step * steps / el,
+            desc = W.describe()
+            if mode == "borrowed":
+                desc += "; plain (borrowed) input tensors: each batch partitioned at its spawn, the shard sweep shared"
+            elif mode == "nodefer":
+                desc += "; no deferral (LAMELLAR_DEFER=0): each batch partitioned and applied at its spawn, one sweep per batch"
+            res[cfg] = {"workload": desc, "ms_per_step": ms, "value": W.ops_per_step * steps / el,
                         "unit": "ops/s", "steps": steps, "warmup": warm, "dtype": W.dtype,
                         "roofline_frac": W.survey_bpo * W.ops_per_step / (ms * 1e-3) / HBM_PEAK,
                         "bytes_per_op": W.survey_bpo, "verified": W.verify(warm + steps)}
@@ -666,6 +690,8 @@ def other_configs(lam, world, team, args):
             torch.cuda.empty_cache()
         except Exception as e:  # a failing side line never costs the headline line
             res[cfg] = {"error": f"{type(e).__name__}: {e}"}
+        finally:
+            args.inputs, engine._DEFER = saved
     return res
 
 

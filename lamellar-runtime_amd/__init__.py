@@ -17,11 +17,11 @@ from .kernels import LamellarError, DeviceKernels
 from .world import LamellarWorld, LamellarWorldBuilder, LamellarTeam
 from .array import (AtomicArray, Err, GlobalLockArray, LocalLockArray, Ok, ReadOnlyArray,
                     UnsafeArray)
-from .engine import BatchResult, run_batch
+from .engine import BatchResult, Owned, run_batch
 
 __all__ = [
     "ArrayKind", "ArrayOpCmd", "BatchReturnType", "Distribution", "LmrStatus", "Strategy",
     "DTYPES", "dtype_of", "LamellarError", "DeviceKernels", "LamellarWorld",
     "LamellarWorldBuilder", "LamellarTeam", "AtomicArray", "Err", "GlobalLockArray",
-    "LocalLockArray", "Ok", "ReadOnlyArray", "UnsafeArray", "BatchResult", "run_batch",
+    "LocalLockArray", "Ok", "ReadOnlyArray", "UnsafeArray", "BatchResult", "Owned", "run_batch",
 ]

@@ -137,6 +137,9 @@ SIGNATURES = {
                          c_uint32, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     "lmr_host_register": (c_int, [c_void_p, c_uint64]),
     "lmr_host_unregister": (c_int, [c_void_p]),
+    "lmr_host_registered": (c_int, [c_void_p, c_uint64, POINTER(c_uint64), POINTER(c_uint64), POINTER(c_uint32)]),
+    "lmr_host_alloc": (c_int, [c_uint64, POINTER(c_void_p)]),
+    "lmr_host_free": (c_int, [c_void_p]),
     "lmr_apply_mvmi_host": (c_int, [c_void_p, POINTER(lmr_apply_desc_t), c_void_p, c_uint64, c_uint32,
                                     c_void_p, c_void_p, c_void_p]),
     "lmr_reduce": (c_int, [c_void_p, c_uint32, c_uint32, c_void_p, c_uint64, c_void_p, c_void_p, c_void_p]),

@@ -334,6 +334,7 @@ lmr_status_t lmr_ctx_create(int device, lmr_ctx_t** out) {
 lmr_status_t lmr_ctx_destroy(lmr_ctx_t* ctx) {
     if (!ctx) return LMR_E_INVALID;
     (void)hipSetDevice(ctx->device);
+    (void)hipDeviceSynchronize();                      // every buffer below may still be in use
     host_stage_free(ctx->host);
     stage_state_free(ctx->stage);
     xstate_free(ctx->xch);
@@ -395,7 +396,7 @@ lmr_status_t lmr_ctx_profile(lmr_ctx_t* ctx, int enable) {
     if (!ctx) return LMR_E_INVALID;
     if (enable && !ctx->prof) ctx->prof = new Prof();
     if (!enable && ctx->prof) {
-        (void)hipDeviceSynchronize();
+        for (auto& r : ctx->prof->pending) (void)hipEventSynchronize(r.b);   // the recorded stages only
         for (hipEvent_t e : ctx->prof->pool) (void)hipEventDestroy(e);
         delete ctx->prof;
         ctx->prof = nullptr;

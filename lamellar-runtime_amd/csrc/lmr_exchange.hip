@@ -422,9 +422,14 @@ lmr_status_t lmr_transport_rccl_create(const uint8_t id[128], uint32_t num_pes, 
         return LMR_E_HIP;
     }
     t->device = device;
-    // the header communicator (collective like the init; without ncclCommSplit, or if the split
-    // fails, headers share the data communicator and its stream)
-    if (rccl().comm_split && rccl().comm_split(t->comm, 0, int(my_pe), &t->hcomm, nullptr) != ncclSuccess)
+    // the header communicator (collective like the init; without ncclCommSplit, if the split
+    // fails, or with LMR_SPLIT_HEADERS=0 -- which every rank must set alike -- headers share the
+    // data communicator and its stream). The two communicators' collectives run on two streams
+    // and may start in a different order on different ranks; that cannot deadlock as long as
+    // both RCCL kernels are co-resident on every GPU (each takes a few CUs of 256: a header
+    // all-to-all is one channel), which is what the split assumes.
+    static const bool split = [] { const char* v = getenv("LMR_SPLIT_HEADERS"); return !(v && v[0] == '0'); }();
+    if (split && rccl().comm_split && rccl().comm_split(t->comm, 0, int(my_pe), &t->hcomm, nullptr) != ncclSuccess)
         t->hcomm = nullptr;
     t->tp.num_pes = num_pes;
     t->tp.my_pe = my_pe;

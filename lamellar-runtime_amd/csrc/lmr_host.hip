@@ -17,45 +17,97 @@
 // engines read it in place.
 //
 // The library DMAs only between the device and host memory it knows is page-locked: ranges
-// registered through lmr_host_register (kept in a registry) and its own pinned bounce buffers.
-// Records in pageable memory are copied by the host into a pinned slot before their upload;
-// results / Ok flags bound for pageable memory land in a pinned slot and the host copies them
-// out (the call then returns once they are written). In round 3 the Ok flags of
-// compare_exchange went by an asynchronous copy into a pageable array next to a registered one,
-// leaving the runtime to pin pageable memory on the fly beside our registrations; the next
-// pageable host-to-device copy of the process faulted twice. tools/hostreg_probe.cpp (run on
-// the GPU box, profiles/r4/hostreg_probe.txt) showed that the runtime keeps no mapping of an
-// unregistered range (scenarios A-C, F, G), so the "stale registration" reading of those
-// faults was wrong; it also showed that hipHostUnregister with a pointer inside a registered
-// range aborts the process (E), which the registry now refuses with LMR_E_INVALID.
+// registered through lmr_host_register, memory the HIP runtime itself allocated pinned
+// (lmr_host_alloc / hipHostMalloc), and its own pinned bounce buffers. Records in pageable memory
+// are copied by the host into a pinned slot before their upload; results / Ok flags bound for
+// pageable memory land in a pinned slot and the host copies them out (the call then returns
+// once they are written).
+//
+// Registration contract (round 5). Three device faults (rounds 3 and 4) surfaced at the first
+// pageable host-to-device copy after host tests had registered two ranges that shared a page
+// (slices of one numpy arena, or two heap neighbours), unregistered both and freed the memory;
+// the runs that kept registered ranges allocated for the life of the process never faulted, and
+// single page-aligned registrations that are unregistered, unmapped and mapped again at the same
+// address copy cleanly (tools/hostreg_probe2.cpp, profiles/r5/hostreg_probe2.txt, scenarios 4-5).
+// What differs is one page pinned by two registrations and released by two unpins. The registry
+// therefore pins page-aligned segments only, one per set of overlapping page ranges,
+// reference-counted by the caller ranges they cover: registering a range whose pages touch an
+// existing segment re-pins the union once (after draining the library's host streams), and a
+// segment is unpinned, with its own page-aligned base, when its last caller range is unregistered.
+// No page is ever pinned twice, and no unpin leaves a page that another registration still covers.
+// Caller ranges keep their byte bounds: a copy is DMA'd in place only when it lies inside one
+// registered caller range (hipHostRegister with a pointer inside a registered range aborts the
+// process, probe scenario E: the registry refuses it with LMR_E_INVALID). Short-lived pinned
+// buffers come from lmr_host_alloc / lmr_host_free (hipHostMalloc: no user page pinning at all).
 #include "lmr_internal.hpp"
 #include "../../include/lamellar_gpu_ops.h"
 #include <stdlib.h>
 #include <string.h>
+#include <algorithm>
 #include <iterator>
+#include <vector>
 #include <map>
 #include <mutex>
+#include <set>
+#include <shared_mutex>
 
 namespace lmr {
 
-// ranges registered through lmr_host_register: start -> end (bytes)
-std::mutex& reg_mu() {
-    static std::mutex m;
-    return m;
-}
-std::map<uintptr_t, uintptr_t>& regs() {
-    static std::map<uintptr_t, uintptr_t> r;
+static const uintptr_t kHostPage = 4096;
+
+// page-aligned pinned segment [lo, hi): refs = caller ranges inside it
+struct HostSeg {
+    uintptr_t hi;
+    uint32_t refs;
+};
+// a caller range [lo, hi) and the segment holding it
+struct HostRange {
+    uintptr_t hi;
+    uintptr_t seg;
+};
+struct HostRegistry {
+    std::mutex mu;                                   // registry maps and the stage list
+    std::shared_mutex pin;                           // shared: a call DMAs through a segment; unique: re-pin / unpin
+    std::map<uintptr_t, HostSeg> segs;
+    std::map<uintptr_t, HostRange> ranges;
+    std::set<HostStage*> stages;                     // every context's host stage (drained before an unpin)
+    std::set<void*> allocs;                          // lmr_host_alloc blocks
+};
+HostRegistry& reg() {
+    static HostRegistry r;
     return r;
 }
-// true when [p, p + bytes) lies inside one registered range
+// true when [p, p + bytes) lies inside one registered caller range (caller holds reg().mu)
+static bool in_range_locked(uintptr_t lo, uintptr_t hi) {
+    auto& R = reg().ranges;
+    auto it = R.upper_bound(lo);
+    if (it == R.begin()) return false;
+    --it;
+    return it->first <= lo && hi <= it->second.hi;
+}
 bool host_range_registered(const void* p, uint64_t bytes) {
     if (!p || bytes == 0) return false;
-    const uintptr_t lo = reinterpret_cast<uintptr_t>(p), hi = lo + bytes;
-    std::lock_guard<std::mutex> g(reg_mu());
-    auto it = regs().upper_bound(lo);
-    if (it == regs().begin()) return false;
-    --it;
-    return it->first <= lo && hi <= it->second;
+    const uintptr_t lo = reinterpret_cast<uintptr_t>(p);
+    std::lock_guard<std::mutex> g(reg().mu);
+    return in_range_locked(lo, lo + bytes);
+}
+// memory the runtime allocated pinned (hipHostMalloc, torch's pinned allocator) covering the
+// whole range: DMA'd in place as well
+static bool runtime_pinned(const void* p, uint64_t bytes) {
+    if (!p || bytes == 0) return false;
+    {
+        std::lock_guard<std::mutex> g(reg().mu);
+        if (reg().allocs.count(const_cast<void*>(p))) return true;
+    }
+    hipPointerAttribute_t a{}, b{};
+    if (hipPointerGetAttributes(&a, p) != hipSuccess) { (void)hipGetLastError(); return false; }
+    if (a.type != hipMemoryTypeHost || !a.hostPointer) return false;
+    const void* last = static_cast<const uint8_t*>(p) + bytes - 1;
+    if (hipPointerGetAttributes(&b, last) != hipSuccess) { (void)hipGetLastError(); return false; }
+    return b.type == hipMemoryTypeHost && b.hostPointer == a.hostPointer;
+}
+static bool host_dma_ok(const void* p, uint64_t bytes) {
+    return host_range_registered(p, bytes) || runtime_pinned(p, bytes);
 }
 
 struct HostStage {
@@ -74,6 +126,10 @@ struct HostStage {
 
 void host_stage_free(HostStage* h) {
     if (!h) return;
+    {
+        std::lock_guard<std::mutex> g(reg().mu);
+        reg().stages.erase(h);
+    }
     if (h->h2d) (void)hipStreamSynchronize(h->h2d);
     if (h->d2h) (void)hipStreamSynchronize(h->d2h);
     for (int b = 0; b < 2; b++) {
@@ -116,6 +172,10 @@ static hipError_t host_stage_get(lmr_ctx* ctx, HostStage** out) {
         if (e == hipSuccess) e = hipEventCreateWithFlags(&h->drained[b], hipEventDisableTiming);
     }
     if (e != hipSuccess) { host_stage_free(h); return e; }
+    {
+        std::lock_guard<std::mutex> g(reg().mu);
+        reg().stages.insert(h);
+    }
     ctx->host = h;
     *out = h;
     return hipSuccess;
@@ -131,6 +191,21 @@ static hipError_t host_bounce_get(HostStage* h) {
     return e;
 }
 
+// every context's host-stage copies done (caller holds reg().mu and the unique pin lock: no
+// lmr_apply_mvmi_host is between its checks and its last enqueued copy)
+static hipError_t drain_host_stages_locked() {
+    hipError_t r = hipSuccess;
+    for (HostStage* h : reg().stages) {
+        hipError_t e = hipStreamSynchronize(h->h2d);
+        if (e == hipSuccess) e = hipStreamSynchronize(h->d2h);
+        if (e != hipSuccess) r = e;
+    }
+    return r;
+}
+
+static uintptr_t page_down(uintptr_t x) { return x & ~(kHostPage - 1); }
+static uintptr_t page_up(uintptr_t x) { return (x + kHostPage - 1) & ~(kHostPage - 1); }
+
 }  // namespace lmr
 
 using namespace lmr;
@@ -140,22 +215,125 @@ extern "C" {
 lmr_status_t lmr_host_register(void* ptr, uint64_t bytes) {
     if (!ptr || bytes == 0) return LMR_E_INVALID;
     const uintptr_t lo = reinterpret_cast<uintptr_t>(ptr), hi = lo + bytes;
-    std::lock_guard<std::mutex> g(reg_mu());
-    auto it = regs().lower_bound(lo);                    // overlapping an earlier registration: refused
-    if (it != regs().end() && it->first < hi) return LMR_E_INVALID;
-    if (it != regs().begin() && std::prev(it)->second > lo) return LMR_E_INVALID;
-    if (hipHostRegister(ptr, bytes, hipHostRegisterDefault) != hipSuccess) return LMR_E_HIP;
-    regs()[lo] = hi;
+    if (hi < lo) return LMR_E_INVALID;
+    HostRegistry& R = reg();
+    std::unique_lock<std::shared_mutex> pin(R.pin);
+    std::lock_guard<std::mutex> g(R.mu);
+    auto it = R.ranges.lower_bound(lo);                  // overlapping an earlier caller range: refused
+    if (it != R.ranges.end() && it->first < hi) return LMR_E_INVALID;
+    if (it != R.ranges.begin() && std::prev(it)->second.hi > lo) return LMR_E_INVALID;
+    // the page range, grown to every segment it shares a page with
+    uintptr_t plo = page_down(lo), phi = page_up(hi);
+    std::vector<uintptr_t> merged;
+    uint32_t refs = 1;
+    for (bool grew = true; grew;) {
+        grew = false;
+        auto s = R.segs.upper_bound(plo);
+        if (s != R.segs.begin()) --s;
+        for (; s != R.segs.end() && s->first < phi; ++s) {
+            if (s->second.hi <= plo) continue;
+            if (std::find(merged.begin(), merged.end(), s->first) != merged.end()) continue;
+            merged.push_back(s->first);
+            refs += s->second.refs;
+            if (s->first < plo) { plo = s->first; grew = true; }
+            if (s->second.hi > phi) { phi = s->second.hi; grew = true; }
+        }
+    }
+    if (merged.size() == 1 && merged[0] == plo && R.segs[plo].hi == phi) {   // inside one segment's pages
+        R.segs[plo].refs = refs;
+        R.ranges[lo] = HostRange{hi, plo};
+        return LMR_OK;
+    }
+    std::vector<uintptr_t> unpinned;
+    auto restore = [&]() {                               // the old segments as they were
+        for (uintptr_t m : unpinned)
+            (void)hipHostRegister(reinterpret_cast<void*>(m), R.segs[m].hi - m, hipHostRegisterDefault);
+    };
+    if (!merged.empty()) {
+        // re-pin the union once: the library's copies through the old segments are done first
+        if (drain_host_stages_locked() != hipSuccess) return LMR_E_HIP;
+        for (uintptr_t m : merged) {
+            if (hipHostUnregister(reinterpret_cast<void*>(m)) != hipSuccess) {
+                (void)hipGetLastError();
+                restore();
+                return LMR_E_HIP;
+            }
+            unpinned.push_back(m);
+        }
+    }
+    if (hipHostRegister(reinterpret_cast<void*>(plo), phi - plo, hipHostRegisterDefault) != hipSuccess) {
+        (void)hipGetLastError();
+        restore();
+        return LMR_E_HIP;
+    }
+    for (uintptr_t m : merged) R.segs.erase(m);
+    R.segs[plo] = HostSeg{phi, refs};
+    for (auto& r : R.ranges)
+        if (std::find(merged.begin(), merged.end(), r.second.seg) != merged.end()) r.second.seg = plo;
+    R.ranges[lo] = HostRange{hi, plo};
     return LMR_OK;
 }
 
 lmr_status_t lmr_host_unregister(void* ptr) {
     if (!ptr) return LMR_E_INVALID;
-    std::lock_guard<std::mutex> g(reg_mu());
-    auto it = regs().find(reinterpret_cast<uintptr_t>(ptr));
-    if (it == regs().end()) return LMR_E_INVALID;        // not the start of a registration
-    regs().erase(it);
-    return hipHostUnregister(ptr) == hipSuccess ? LMR_OK : LMR_E_HIP;
+    HostRegistry& R = reg();
+    std::unique_lock<std::shared_mutex> pin(R.pin);
+    std::lock_guard<std::mutex> g(R.mu);
+    auto it = R.ranges.find(reinterpret_cast<uintptr_t>(ptr));
+    if (it == R.ranges.end()) return LMR_E_INVALID;      // not the start of a registration
+    auto s = R.segs.find(it->second.seg);
+    if (s == R.segs.end()) return LMR_E_INVALID;
+    if (s->second.refs > 1) {                            // the segment still covers other ranges
+        s->second.refs--;
+        R.ranges.erase(it);
+        return LMR_OK;
+    }
+    if (drain_host_stages_locked() != hipSuccess) return LMR_E_HIP;
+    if (hipHostUnregister(reinterpret_cast<void*>(s->first)) != hipSuccess) {
+        (void)hipGetLastError();
+        return LMR_E_HIP;                                // registry unchanged: still registered
+    }
+    R.segs.erase(s);
+    R.ranges.erase(it);
+    return LMR_OK;
+}
+
+lmr_status_t lmr_host_registered(const void* ptr, uint64_t bytes, uint64_t* seg_base, uint64_t* seg_bytes,
+                                 uint32_t* seg_ranges) {
+    if (!ptr || bytes == 0) return LMR_E_INVALID;
+    const uintptr_t lo = reinterpret_cast<uintptr_t>(ptr);
+    HostRegistry& R = reg();
+    std::lock_guard<std::mutex> g(R.mu);
+    if (!in_range_locked(lo, lo + bytes)) return LMR_E_INVALID;
+    auto r = std::prev(R.ranges.upper_bound(lo));
+    const auto& sg = R.segs.at(r->second.seg);
+    if (seg_base) *seg_base = r->second.seg;
+    if (seg_bytes) *seg_bytes = sg.hi - r->second.seg;
+    if (seg_ranges) *seg_ranges = sg.refs;
+    return LMR_OK;
+}
+
+lmr_status_t lmr_host_alloc(uint64_t bytes, void** out) {
+    if (!out || bytes == 0) return LMR_E_INVALID;
+    *out = nullptr;
+    void* p = nullptr;
+    if (hipHostMalloc(&p, bytes, hipHostMallocDefault) != hipSuccess) { (void)hipGetLastError(); return LMR_E_HIP; }
+    std::lock_guard<std::mutex> g(reg().mu);
+    reg().allocs.insert(p);
+    *out = p;
+    return LMR_OK;
+}
+
+lmr_status_t lmr_host_free(void* ptr) {
+    if (!ptr) return LMR_E_INVALID;
+    HostRegistry& R = reg();
+    std::unique_lock<std::shared_mutex> pin(R.pin);
+    std::lock_guard<std::mutex> g(R.mu);
+    if (!R.allocs.count(ptr)) return LMR_E_INVALID;
+    if (drain_host_stages_locked() != hipSuccess) return LMR_E_HIP;
+    if (hipHostFree(ptr) != hipSuccess) { (void)hipGetLastError(); return LMR_E_HIP; }
+    R.allocs.erase(ptr);
+    return LMR_OK;
 }
 
 lmr_status_t lmr_apply_mvmi_host(lmr_ctx_t* ctx, const lmr_apply_desc_t* desc, const void* h_idx_vals,
@@ -176,17 +354,24 @@ lmr_status_t lmr_apply_mvmi_host(lmr_ctx_t* ctx, const lmr_apply_desc_t* desc, c
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
     const uint64_t P = h->piece_recs;
     if (desc->strategy != LMR_STRATEGY_DIRECT && P >= 65536 && ctx->rec_cap < P) {
-        (void)hipDeviceSynchronize();
+        // the workspace grows (once): the context's earlier work is ordered on `stream` (one
+        // stream at a time per context) plus the library's own side and host-stage streams
+        if (hipStreamSynchronize(s) != hipSuccess || (ctx->side && hipStreamSynchronize(ctx->side) != hipSuccess) ||
+            hipStreamSynchronize(h->h2d) != hipSuccess || hipStreamSynchronize(h->d2h) != hipSuccess)
+            return LMR_E_HIP;
         lmr_status_t st = lmr_ctx_reserve(ctx, P);
         if (st != LMR_OK) return st;
     }
+    // registrations stay pinned while this call enqueues copies through them (lmr_host_unregister
+    // takes the lock exclusively and drains the host-stage streams before it unpins)
+    std::shared_lock<std::shared_mutex> pin(reg().pin);
     const uint32_t ret = lmr_op_ret_kind(desc->op);
     const bool want_res = h_results && ret != LMR_RET_NONE;
     const bool want_ok = h_ok && ret == LMR_RET_RESULT;
     // pageable buffers go through the pinned bounce slots
-    const bool rec_pinned = host_range_registered(h_idx_vals, n * rb);
-    const bool res_pinned = !want_res || host_range_registered(h_results, n * eb);
-    const bool ok_pinned = !want_ok || host_range_registered(h_ok, n);
+    const bool rec_pinned = host_dma_ok(h_idx_vals, n * rb);
+    const bool res_pinned = !want_res || host_dma_ok(h_results, n * eb);
+    const bool ok_pinned = !want_ok || host_dma_ok(h_ok, n);
     if ((!rec_pinned || !res_pinned || !ok_pinned) && host_bounce_get(h) != hipSuccess) return LMR_E_HIP;
     const uint8_t* src = reinterpret_cast<const uint8_t*>(h_idx_vals);
     // results of a bounced piece are copied out by the host once its download is done

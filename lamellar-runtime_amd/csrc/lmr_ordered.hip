@@ -223,10 +223,8 @@ hipError_t ord_reserve(lmr_ctx* ctx, uint64_t recs) {
     if (e != hipSuccess) return e;
     void* p = nullptr;
     if ((e = hipMalloc(&p, piece_bytes(recs, tmp))) != hipSuccess) return e;
-    if (B->p) {                                          // (outside the hot path: lmr_ctx_reserve)
-        (void)hipDeviceSynchronize();
-        (void)hipFree(B->p);
-    }
+    if (B->p)                                            // (outside the hot path: lmr_ctx_reserve, whose
+        (void)hipFree(B->p);                             //  caller has completed the context's work)
     B->p = p;
     B->bytes = piece_bytes(recs, tmp);
     B->recs = recs;

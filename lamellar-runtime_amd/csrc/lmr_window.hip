@@ -129,10 +129,12 @@ hipError_t win_dispatch(int iw, int vb, F&& f) {
 struct WinBuf {
     void* p = nullptr;
     size_t cap = 0;
-    hipError_t need(size_t bytes) {
+    // grow-only; the old buffer may still be read by this context's earlier work, which is
+    // ordered on the call's stream (the context contract, lamellar_gpu_ops.h)
+    hipError_t need(size_t bytes, hipStream_t s) {
         if (bytes <= cap) return hipSuccess;
         if (p) {
-            hipError_t e = hipDeviceSynchronize();      // the old buffer may still be read
+            hipError_t e = hipStreamSynchronize(s);
             if (e != hipSuccess) return e;
             (void)hipFree(p);
             p = nullptr;
@@ -155,8 +157,7 @@ struct WinState {
 };
 
 void win_state_free(WinState* w) {
-    if (!w) return;
-    (void)hipDeviceSynchronize();
+    if (!w) return;                                  // (lmr_ctx_destroy has drained the device)
     for (WinBuf* b : {&w->ctl, &w->idx, &w->val, &w->pos, &w->res, &w->ok}) b->release();
     if (w->h_counts) (void)hipHostFree(w->h_counts);
     if (w->ev) (void)hipEventDestroy(w->ev);
@@ -189,12 +190,12 @@ hipError_t apply_windowed(lmr_ctx* ctx, const lmr_apply_desc_t* d, const ApplyAr
     // pieces: positions are u32 and the temp arrays grow to one piece
     const uint64_t piece = std::min<uint64_t>(a.n, std::max<uint64_t>(ctx->rec_cap, uint64_t(1) << 22));
     const uint64_t pc = std::min<uint64_t>(piece, uint64_t(1) << 31);
-    if ((e = ws->ctl.need((3 * kMaxWindows + 1) * 4)) != hipSuccess ||
-        (e = ws->idx.need(pc * 4 + 16)) != hipSuccess ||
-        (a.val && (e = ws->val.need(pc * eb + 16)) != hipSuccess) ||
-        (ret && (e = ws->pos.need(pc * 4 + 16)) != hipSuccess) ||
-        (ret && (e = ws->res.need(pc * eb + 16)) != hipSuccess) ||
-        (want_ok && (e = ws->ok.need(pc + 16)) != hipSuccess))
+    if ((e = ws->ctl.need((3 * kMaxWindows + 1) * 4, s)) != hipSuccess ||
+        (e = ws->idx.need(pc * 4 + 16, s)) != hipSuccess ||
+        (a.val && (e = ws->val.need(pc * eb + 16, s)) != hipSuccess) ||
+        (ret && (e = ws->pos.need(pc * 4 + 16, s)) != hipSuccess) ||
+        (ret && (e = ws->res.need(pc * eb + 16, s)) != hipSuccess) ||
+        (want_ok && (e = ws->ok.need(pc + 16, s)) != hipSuccess))
         return e;
     uint32_t* counts = reinterpret_cast<uint32_t*>(ws->ctl.p);
     uint32_t* offsets = counts + kMaxWindows;

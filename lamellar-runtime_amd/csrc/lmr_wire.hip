@@ -105,8 +105,7 @@ struct WireBufs {
 };
 
 void wire_bufs_free(WireBufs* b) {
-    if (!b) return;
-    (void)hipDeviceSynchronize();
+    if (!b) return;                                  // (lmr_ctx_destroy has drained the device)
     if (b->h) (void)hipHostFree(b->h);
     if (b->d) (void)hipFree(b->d);
     delete b;

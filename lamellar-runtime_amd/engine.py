@@ -36,8 +36,35 @@ _FORCE_EXCHANGE = os.environ.get("LAMELLAR_FORCE_EXCHANGE", "0") == "1"
 # Large 1-PE batches are deferred: staged into the context's open session and applied with the
 # batches issued after them in one shard sweep, at the next flush point (a handle's block(),
 # wait_all, reading the array, any other device call). LAMELLAR_DEFER=0 applies each at once.
+# The reference consumes a batch's input when the batch is built (the pack copies it into op
+# buffers before batch_* returns, unsafe/operations.rs:663-811; a Vec input is moved in), so a
+# caller may change its own buffers right after spawn(). A deferred batch whose input is the
+# caller's device tensor (borrowed) is therefore partitioned at spawn, in stream order
+# (lmr_stage_flush): its records are in the library's workspace before any later work on the
+# stream, and only the shard sweep is shared. Inputs the library made itself (host sequences,
+# converted dtypes) or that the caller hands over with Owned(...) -- Rust's by-value Vec input --
+# stay with the session until it is applied, so consecutive batches also share the partition.
 _DEFER = os.environ.get("LAMELLAR_DEFER", "1") != "0"
 _DEFER_MIN = 65536
+
+
+class Owned:
+    """An op input handed over to the library (the reference's by-value `Vec<T>` OpInput,
+    src/array/operations.rs:435-585): the caller does not modify the tensor until the batch has
+    been applied (its handle's block(), wait_all(), or any read of the array)."""
+
+    __slots__ = ("value",)
+
+    def __init__(self, value):
+        self.value = value
+
+
+def _unwrap(x):
+    return (x.value, True) if isinstance(x, Owned) else (x, False)
+
+
+def _same_storage(a, b):
+    return isinstance(b, torch.Tensor) and a.untyped_storage().data_ptr() == b.untyped_storage().data_ptr()
 
 
 class BatchResult:
@@ -64,30 +91,35 @@ def _is_scalar(x):
 
 
 def index_input(k, x):
-    """OpInput<usize>: scalar -> (True, int, 1); sequence -> (False, int64 tensor, len)."""
+    """OpInput<usize>: scalar -> (True, int, 1, False); sequence -> (False, int64 tensor, len,
+    borrowed). `borrowed`: the tensor is the caller's own device storage (not Owned)."""
+    x, owned = _unwrap(x)
     if _is_scalar(x):
-        return True, int(x), 1
+        return True, int(x), 1, False
     if isinstance(x, torch.Tensor):
         t = x.reshape(-1)
         if t.dtype != torch.int64:
             t = t.to(torch.int64)
         t = t.to(k.device) if t.device != k.device else t
-        return False, t.contiguous(), int(t.numel())
+        t = t.contiguous()
+        return False, t, int(t.numel()), (not owned) and _same_storage(t, x)
     a = np.asarray(x)
     if a.size == 0:
-        return False, k.empty(0, torch.int64), 0
+        return False, k.empty(0, torch.int64), 0, False
     a = a.reshape(-1)
     if a.dtype == np.uint64:
         a = a.view(np.int64)
     else:
         a = a.astype(np.int64)
-    return False, torch.from_numpy(np.ascontiguousarray(a)).to(k.device), int(a.size)
+    return False, torch.from_numpy(np.ascontiguousarray(a)).to(k.device), int(a.size), False
 
 
 def value_input(k, dt: DType, x):
-    """OpInput<T>: scalar -> (True, bits, 1); sequence -> (False, storage tensor, len)."""
+    """OpInput<T>: scalar -> (True, bits, 1, False); sequence -> (False, storage tensor, len,
+    borrowed)."""
+    x, owned = _unwrap(x)
     if _is_scalar(x):
-        return True, dt.to_bits(x), 1
+        return True, dt.to_bits(x), 1, False
     if isinstance(x, torch.Tensor):
         t = x.reshape(-1)
         if t.dtype != dt.torch:
@@ -96,11 +128,12 @@ def value_input(k, dt: DType, x):
             else:
                 t = _np_to_storage(t.cpu().numpy(), dt)
         t = t.to(k.device) if t.device != k.device else t
-        return False, t.contiguous(), int(t.numel())
+        t = t.contiguous()
+        return False, t, int(t.numel()), (not owned) and _same_storage(t, x)
     a = np.asarray(x).reshape(-1)
     if a.size == 0:
-        return False, k.empty(0, dt.torch), 0
-    return False, _np_to_storage(a, dt).to(k.device), int(a.size)
+        return False, k.empty(0, dt.torch), 0, False
+    return False, _np_to_storage(a, dt).to(k.device), int(a.size), False
 
 
 _STORAGE_NP = {1: np.int8, 2: np.int16, 4: np.int32, 8: np.int64}
@@ -125,8 +158,8 @@ def run_batch(arr, op, index, val, current=None, eps=None) -> BatchResult:
     ret = RET_KIND[op]
     cmp_bits = dt.to_bits(current) if current is not None else 0
     eps_bits = dt.to_bits(eps) if eps is not None else 0
-    i_scalar, idx, i_len = index_input(k, index)
-    v_scalar, vals, v_len = value_input(k, dt, val)
+    i_scalar, idx, i_len, i_borrowed = index_input(k, index)
+    v_scalar, vals, v_len, v_borrowed = value_input(k, dt, val)
     if i_len > 1 and v_len > 1 and i_len != v_len:
         raise LamellarError(LmrStatus.LENGTH, f"{i_len} indices vs {v_len} values")
     n = 0 if (i_len == 0 or v_len == 0) else max(i_len, v_len)   # "no vals no indices" :345-347
@@ -136,7 +169,7 @@ def run_batch(arr, op, index, val, current=None, eps=None) -> BatchResult:
         _distributed(arr, k, dt, op, i_scalar, idx, i_len, v_scalar, vals, v_len, results, ok, cmp_bits, eps_bits)
     elif n:
         _local(arr, k, dt, op, i_scalar, idx, v_scalar, vals, n, i_len == 1 and v_len > 1, results, ok,
-               cmp_bits, eps_bits)
+               cmp_bits, eps_bits, i_borrowed or v_borrowed)
     return BatchResult(results, ok, dt, ret)
 
 
@@ -151,7 +184,8 @@ def _host_map(arr, g):
     return pe.value, off.value
 
 
-def _local(arr, k, dt, op, i_scalar, idx, v_scalar, vals, n, mvsi, results, ok, cmp_bits, eps_bits):
+def _local(arr, k, dt, op, i_scalar, idx, v_scalar, vals, n, mvsi, results, ok, cmp_bits, eps_bits,
+           borrowed=False):
     shard, slen = arr._shard_view(), arr.num_elems_local()
     if mvsi:
         _, off = _host_map(arr, idx)
@@ -159,11 +193,12 @@ def _local(arr, k, dt, op, i_scalar, idx, v_scalar, vals, n, mvsi, results, ok, 
         return
     if i_scalar:
         idx = torch.tensor([idx], dtype=torch.int64, device=k.device)
-    apply = k.apply_soa
     if _DEFER and n >= _DEFER_MIN and getattr(k, "defer_soa", None) is not None:
-        apply = k.defer_soa
-    apply(shard, slen, arr.kind, dt, op, idx, 8, None if v_scalar else vals,
-          vals if v_scalar else 0, n, results, ok, cmp_bits, eps_bits)
+        k.defer_soa(shard, slen, arr.kind, dt, op, idx, 8, None if v_scalar else vals,
+                    vals if v_scalar else 0, n, results, ok, cmp_bits, eps_bits, borrowed=borrowed)
+        return
+    k.apply_soa(shard, slen, arr.kind, dt, op, idx, 8, None if v_scalar else vals,
+                vals if v_scalar else 0, n, results, ok, cmp_bits, eps_bits)
 
 
 def _distributed(arr, k, dt, op, i_scalar, idx, i_len, v_scalar, vals, v_len, results, ok, cmp_bits, eps_bits):

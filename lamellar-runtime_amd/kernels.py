@@ -10,6 +10,7 @@ import ctypes
 import os
 from ctypes import byref, c_uint32, c_uint64, c_void_p
 
+import numpy as np
 import torch
 
 from . import _capi
@@ -126,8 +127,11 @@ class DeviceKernels:
     # flush() runs before anything else touches the device state this context manages
     # (every other call here, synchronize, error reads, the arrays' local data).
     def defer_soa(self, shard, shard_len, kind, dt, op, idx, iw, vals, scalar_bits, n,
-                  results=None, ok=None, cmp_bits=0, eps_bits=0):
-        """Stage n records for a later flush(); their results / Ok flags are valid after it."""
+                  results=None, ok=None, cmp_bits=0, eps_bits=0, borrowed=False):
+        """Stage n records for a later flush(); their results / Ok flags are valid after it.
+        borrowed: idx / vals are the caller's own buffers, which it may change after this call
+        returns -- the records are partitioned now (lmr_stage_flush, stream-ordered), so only
+        the shard sweep waits for the flush."""
         key = (shard.data_ptr(), int(shard_len), int(kind), int(dt.code))
         if self._deferred is not None and self._deferred[0] != key:
             self.flush()
@@ -152,6 +156,8 @@ class DeviceKernels:
             self._deferred = None
             self.lib.lmr_stage_finish(self.ctx, self.stream())
             check(st, "lmr_stage_soa")
+        if borrowed:
+            check(self.lib.lmr_stage_flush(self.ctx, self.stream()), "lmr_stage_flush")
 
     def flush(self):
         """Apply the deferred batches (one sweep) on this stream."""
@@ -262,6 +268,23 @@ class DeviceKernels:
 
     def host_unregister(self, arr):
         check(self.lib.lmr_host_unregister(arr.ctypes.data), "lmr_host_unregister")
+
+    def host_registered(self, arr):
+        """(segment base, segment bytes, caller ranges in the segment) of a registered buffer,
+        or None (lmr_host_registered)."""
+        base, nb, refs = c_uint64(0), c_uint64(0), c_uint32(0)
+        st = self.lib.lmr_host_registered(arr.ctypes.data, int(arr.nbytes), byref(base), byref(nb), byref(refs))
+        return (base.value, nb.value, refs.value) if st == 0 else None
+
+    def host_alloc(self, nbytes, dtype=np.uint8):
+        """A pinned host buffer (lmr_host_alloc) as a numpy array; release with host_free."""
+        p = ctypes.c_void_p()
+        check(self.lib.lmr_host_alloc(int(nbytes), byref(p)), "lmr_host_alloc")
+        raw = (ctypes.c_uint8 * int(nbytes)).from_address(p.value)
+        return np.frombuffer(raw, dtype=np.uint8).view(dtype)
+
+    def host_free(self, arr):
+        check(self.lib.lmr_host_free(arr.ctypes.data), "lmr_host_free")
 
     def apply_svmi(self, shard, shard_len, kind, dt, op, scalar_bits, indices, n, iw,
                    results=None, ok=None, cmp_bits=0, eps_bits=0):

@@ -85,12 +85,14 @@ def test_apply_mvmi_host_collisions_sum(world, orc, lam):
     assert np.array_equal(d_shard.cpu().numpy().view(np.uint64), ref)
 
 
-def test_registered_ranges_freed_and_reused(world, orc, lam):
-    """Registered op buffers and result arrays that share pages (slices of one host arena),
-    unregistered and freed right after each apply; the freed memory is reused by the next
-    arena and by pageable host-to-device copies in between. compare_exchange's Ok flags go to
-    a pageable array (the library's bounce slot) beside the registered results. Every round
-    is bit-exact against the oracle."""
+def test_registered_ranges_share_one_segment(world, orc, lam):
+    """Registered op buffers and result arrays that share a page (slices of one host arena): the
+    registry pins the page-aligned union once (one segment, both ranges inside it), keeps it
+    pinned while either range is registered and unpins it, at its page-aligned base, with the
+    last one. The arena is freed afterwards and its memory reused by the next arena and by
+    pageable host-to-device copies in between. compare_exchange's Ok flags go to a pageable
+    array (the library's bounce slot) beside the registered results. Every round is bit-exact
+    against the oracle."""
     k = world.team().kernels
     dt = "u32"
     shard_len, n = 300000, 2 * 65536 + 777
@@ -115,11 +117,19 @@ def test_registered_ranges_freed_and_reused(world, orc, lam):
         k.host_register(buf)
         k.host_register(h_res)
         try:
+            seg_b, seg_r = k.host_registered(buf), k.host_registered(h_res)
+            lo, hi = buf.ctypes.data, h_res.ctypes.data + h_res.nbytes
+            assert seg_b == seg_r and seg_b[2] == 2                 # one segment, two ranges
+            assert seg_b[0] % 4096 == 0 and seg_b[1] % 4096 == 0
+            assert seg_b[0] <= lo and hi <= seg_b[0] + seg_b[1] and seg_b[0] > lo - 4096
             k.apply_mvmi_host(d_shard, shard_len, 1, lam.dtype_of(dt), CAS, buf, 4, h_res, h_ok,
                               lam.dtype_of(dt).to_bits(cur), 0)
         finally:
             k.host_unregister(buf)
+            left = k.host_registered(h_res)                       # the segment stays for h_res
             k.host_unregister(h_res)
+        assert left == (seg_b[0], seg_b[1], 1)
+        assert k.host_registered(h_res) is None and k.host_registered(buf) is None
         assert k.errors() == 0
         assert bits_equal(d_shard.cpu().numpy().view(NP[dt])[:shard_len], ref)
         assert bits_equal(h_res.copy(), res_o)
@@ -129,3 +139,31 @@ def test_registered_ranges_freed_and_reused(world, orc, lam):
         for _ in range(3):
             x = rng.integers(0, 2**31, n, dtype=np.int64)
             assert np.array_equal(torch.from_numpy(x).cuda().cpu().numpy(), x)
+
+
+def test_host_alloc_buffers_dma_in_place(world, orc, lam):
+    """Short-lived pinned buffers from lmr_host_alloc: records and fetch results DMA'd in place
+    without registration (u64 fetch_add, conflict-free, bit-exact), freed after each round."""
+    k = world.team().kernels
+    rng = np.random.default_rng(41)
+    shard_len, n = 300000, 2 * 65536 + 99
+    rb, vo = orc.record_bytes(4, CODE["u64"]), orc.record_val_offset(4, CODE["u64"])
+    for _ in range(3):
+        shard0 = rand_elems("u64", shard_len, rng, FETCH_ADD)
+        idx = rng.permutation(shard_len)[:n].astype(np.uint64)
+        vals = rand_vals("u64", n, rng, FETCH_ADD)
+        recs = to_aos(idx, vals, 4, "u64", rb, vo)
+        ref = shard0.copy()
+        st_o, res_o, _ = orc.apply_mvmi(ref, 1, CODE["u64"], np.uint64, FETCH_ADD, recs, 4)
+        assert st_o == 0
+        buf = k.host_alloc(recs.nbytes)
+        h_res = k.host_alloc(n * 8, np.uint64)
+        try:
+            buf[:] = recs
+            d_shard = to_dev(shard0)
+            k.apply_mvmi_host(d_shard, shard_len, 1, lam.dtype_of("u64"), FETCH_ADD, buf, 4, h_res)
+            assert bits_equal(d_shard.cpu().numpy().view(np.uint64)[:shard_len], ref)
+            assert bits_equal(h_res.copy(), res_o)
+        finally:
+            k.host_free(buf)
+            k.host_free(h_res)
