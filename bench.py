@@ -561,6 +561,8 @@ def main():
         tr = json.load(open(pmc))
         if all(st in tr for st in per if st not in ("scan",)):
             traffic = sum(tr.get(st, 0.0) * per[st][1] for st in per)
+            if "pack" in per and "_transport_per_pack" in tr:     # the exchange's RCCL copies
+                traffic += tr["_transport_per_pack"] * per["pack"][1]
     dom = max(per, key=lambda st: per[st][0] * per[st][1]) if per else None
     # per stage: records per launch from the library's own count (a stage may run on a
     # subset of a step's batches, e.g. C5's counted stages)

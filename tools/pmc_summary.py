@@ -67,6 +67,14 @@ def main():
         if inv:
             out[st] = sum(tot.get(x, 0.0) for x in ks) / inv
             print(f"stage {st:16s} {out[st] / 1e6:10.1f} MB per invocation")
+    # the exchange's transport kernels (RCCL's copies) per pack invocation (one per chunk)
+    rccl = sum(v for k, v in tot.items() if k.startswith("rccl") or k.startswith("ncclDevKernel"))
+    if rccl and out.get("pack"):
+        inv = sum(cnt.get(a, 0) for a in STAGES["pack"][0])
+        if cnt.get("k_pack_count") and cnt.get("k_pack_stage"):
+            inv = cnt["k_pack_count"]
+        out["_transport_per_pack"] = rccl / inv
+        print(f"transport (RCCL kernels)  {out['_transport_per_pack'] / 1e6:10.1f} MB per pack invocation")
     if len(sys.argv) > 2:
         json.dump(out, open(sys.argv[2], "w"), indent=1)
 
