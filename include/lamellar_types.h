@@ -43,6 +43,7 @@ typedef enum {
 #define LMR_ERRBIT_DIVZERO     0x2u
 #define LMR_ERRBIT_OVERFLOW    0x4u
 #define LMR_ERRBIT_UNSUPPORTED 0x8u
+#define LMR_ERRBIT_TRANSPORT   0x10u   /* a peer-transport wait timed out (a PE never arrived) */
 
 /* Element types with a device path. usize/isize are 64-bit on every target the
  * reference supports, so they map to U64/I64. u128/i128/bool are out of scope

@@ -74,7 +74,7 @@ class lmr_transport_t(Structure):
     ]
 
 
-XHDR_WORDS = 5     # LMR_XHDR_WORDS
+XHDR_WORDS = 7     # LMR_XHDR_WORDS
 XHDR_SCALAR, XHDR_ORDERED = 1, 2   # LMR_XHDR_SCALAR, LMR_XHDR_ORDERED (flags word of a header row)
 
 
@@ -166,6 +166,9 @@ SIGNATURES = {
     "lmr_rccl_unique_id": (c_int, [c_void_p]),
     "lmr_transport_rccl_create": (c_int, [c_void_p, c_uint32, c_uint32, c_int, POINTER(c_void_p)]),
     "lmr_transport_rccl_destroy": (c_int, [c_void_p]),
+    "lmr_transport_peer_create": (c_int, [c_void_p, ctypes.c_char_p, c_uint64, c_int, POINTER(c_void_p)]),
+    "lmr_transport_peer_destroy": (c_int, [c_void_p]),
+    "lmr_transport_peer_stats": (c_int, [c_void_p, POINTER(c_uint64), POINTER(c_uint64)]),
     "lmr_batch_exchange": (c_int, [c_void_p, c_void_p, POINTER(lmr_layout_t), POINTER(lmr_apply_desc_t),
                                    c_void_p, c_uint64, c_uint64, c_void_p, c_void_p, c_uint64, c_void_p,
                                    c_void_p, c_void_p]),

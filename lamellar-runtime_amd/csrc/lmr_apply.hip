@@ -775,6 +775,10 @@ struct FreeRegion {
     const uint8_t* val;
     uint64_t val_stride, val_bits, n, chunk;
     uint32_t G, row0, block0;
+    // device-count region (a fixed receive region of the exchange): n is the region's capacity and
+    // *n_dev (written by an earlier kernel or collective on the stream) its record count, clamped
+    // to n; the G blocks split the actual count
+    const int64_t* n_dev;
 };
 struct FreeTable {
     FreeRegion r[kFuseFree];
@@ -788,6 +792,11 @@ __global__ __launch_bounds__(1024) void k_coarse_free_stage(PartArgs q, FreeTabl
     PartArgs p = q;
     p.idx = g.idx; p.idx_stride = g.idx_stride; p.val = g.val; p.val_stride = g.val_stride;
     p.val_bits = g.val_bits; p.n = g.n; p.chunk = g.chunk; p.G = g.G;
+    if (g.n_dev) {
+        const int64_t c = *g.n_dev;
+        p.n = c <= 0 ? 0 : min(g.n, uint64_t(c));
+        p.chunk = ((p.n + g.G - 1) / g.G + 1) & ~uint64_t(1);   // even: whole pairs per block
+    }
     p.counts = q.counts + uint64_t(g.row0) * q.num_tiles;
     coarse_free_body<IW, VB, RPT, PAIRS>(p, blockIdx.x - g.block0);
 }
@@ -2263,15 +2272,25 @@ bool stage_free_applies(int dtype, int op, int ret, uint64_t shard_len, uint64_t
 }
 
 static hipError_t stage_region_free(int dtype, int index_size, const ApplyArgs& a, const TiledWs& w,
-                                    StageSession& s, hipStream_t st) {
+                                    StageSession& s, hipStream_t st, const int64_t* n_dev = nullptr,
+                                    uint64_t expect = 0) {
     (void)w; (void)st;
     if (s.nreg >= kMaxRegions) return hipErrorInvalidValue;
     // recorded; partitioned with the session's other pending regions (stage_partition_free)
     s.reg[s.nreg] = StageRegion{0, a.n, nullptr, nullptr, a.op, LMR_RET_NONE, a.cmp_bits, a.eps_bits};
-    s.pend[s.nreg] = PendingRegion{a, index_size};
+    s.pend[s.nreg] = PendingRegion{a, index_size, n_dev};
     s.nreg += 1;
-    s.staged += a.n;
+    // a device-count region counts its expected records (its capacity is an upper bound; the
+    // session's bucket regions spill to device atomics if a stream brings more than expected)
+    s.staged += n_dev ? std::min(expect, a.n) : a.n;
     return hipSuccess;
+}
+
+hipError_t launch_stage_region_dev(int dtype, int index_size, const ApplyArgs& a, const int64_t* n_dev,
+                                   uint64_t expect, const TiledWs& w, StageSession& s, hipStream_t st) {
+    if (a.n == 0) return hipSuccess;
+    if (!s.free || !n_dev) return hipErrorInvalidValue;
+    return stage_region_free(dtype, index_size, a, w, s, st, n_dev, expect);
 }
 
 // the pending count-free regions, k_coarse_free over groups of up to kFuseFree regions of one
@@ -2303,9 +2322,11 @@ static hipError_t stage_partition_free(const TiledWs& w, StageSession& s, hipStr
             const ApplyArgs& a = s.pend[s.parted + int(k)].a;
             const uint32_t G = uint32_t(std::max<uint64_t>(1, std::min<uint64_t>((a.n + 16383) / 16384, gcap)));
             const uint64_t chunk = (a.n + G - 1) / G;
-            t.r[k] = FreeRegion{a.idx, a.idx_stride, a.val, a.val_stride, a.val_bits, a.n, chunk, G, rows, rows};
+            const int64_t* nd = s.pend[s.parted + int(k)].n_dev;
+            t.r[k] = FreeRegion{a.idx, a.idx_stride, a.val, a.val_stride, a.val_bits, a.n, chunk, G, rows, rows, nd};
             // paired 16-B loads (as the one-shot pass): contiguous, 16-B aligned u64 indices and
-            // values, and every block's range whole pairs (even chunks, even n)
+            // values, and every block's range whole pairs (even chunks, even n; a device-count
+            // region's last pair may read one record past its count, inside its capacity + 1)
             pairs = pairs && a.idx_stride == 8 && a.val && a.val_stride == 8 && chunk % 2 == 0 && a.n % 2 == 0 &&
                     ((reinterpret_cast<uintptr_t>(a.idx) | reinterpret_cast<uintptr_t>(a.val)) & 15) == 0;
             rows += G;
@@ -2333,6 +2354,12 @@ static hipError_t stage_partition_free(const TiledWs& w, StageSession& s, hipStr
         }
         if (e != hipSuccess) return e;
         s.parted = r1;
+    }
+    // partitioned count-free regions need nothing more (the sweep reads the shared bucket
+    // regions): one entry stands for them all, so a session can take any number of streams
+    if (s.nreg > 1) {
+        s.reg[0] = s.reg[s.nreg - 1];
+        s.nreg = s.parted = 1;
     }
     return hipSuccess;
 }

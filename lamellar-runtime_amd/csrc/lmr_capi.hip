@@ -110,6 +110,7 @@ lmr_status_t status_of_bits(uint32_t b) {
     if (b & LMR_ERRBIT_DIVZERO) return LMR_E_DIVZERO;
     if (b & LMR_ERRBIT_OVERFLOW) return LMR_E_OVERFLOW;
     if (b & LMR_ERRBIT_UNSUPPORTED) return LMR_E_UNSUPPORTED;
+    if (b & LMR_ERRBIT_TRANSPORT) return LMR_E_HIP;
     return LMR_OK;
 }
 
@@ -287,6 +288,36 @@ lmr_status_t run_apply(lmr_ctx* ctx, const lmr_apply_desc_t* d, ApplyArgs a, int
 }
 
 }  // namespace
+
+namespace lmr {
+
+bool stage_session_free(const lmr_ctx* ctx) { return ctx->stage && ctx->stage->open && ctx->stage->s.free; }
+
+lmr_status_t stage_soa_dev(lmr_ctx* ctx, const void* d_indices, uint32_t index_size, const void* d_vals,
+                           const void* val, uint64_t cap, uint64_t expect, const int64_t* d_n, hipStream_t s) {
+    if (!stage_session_free(ctx) || !valid_iw(index_size) || !d_n) return LMR_E_INVALID;
+    if (cap == 0) return LMR_OK;
+    if (!d_indices || (!d_vals && !val)) return LMR_E_INVALID;
+    StageState* S = ctx->stage;
+    const lmr_apply_desc_t* d = &S->desc;
+    ApplyArgs a = base_args(ctx, d, nullptr, nullptr);
+    a.idx = reinterpret_cast<const uint8_t*>(d_indices);
+    a.idx_stride = index_size;
+    a.val = reinterpret_cast<const uint8_t*>(d_vals);
+    a.val_stride = d_vals ? uint64_t(dtype_bytes(int(d->dtype))) : 0;
+    a.val_bits = d_vals ? 0 : load_scalar_bits(val, int(d->dtype));
+    a.n = cap;
+    a.ret = S->s.a.ret;
+    const TiledWs w = ctx_ws(ctx, ctx->rec_cap);
+    const uint64_t e = std::min(expect, cap);
+    if (S->s.staged + e > ctx->rec_cap || S->s.nreg == kMaxRegions) {
+        const hipError_t he = launch_stage_finish(w, S->s, s);
+        if (he != hipSuccess) return hip_status(he);
+    }
+    return hip_status(launch_stage_region_dev(int(d->dtype), int(index_size), a, d_n, e, w, S->s, s));
+}
+
+}  // namespace lmr
 
 extern "C" {
 

@@ -101,6 +101,7 @@ struct XState {
     DevBuf hdr_send[2], hdr_recv[2], send_idx[2], send_vals[2];
     DevBuf recv_idx[2], recv_vals[2];
     std::vector<DevBuf> pos, res, rok;   // per chunk (returning ops)
+    DevBuf ovf_idx, ovf_vals, ovf_count;  // count-free pack: records past their region (global index, value)
     DevBuf back, back_ok;
     HostBuf h_hdr;                       // per chunk parity: [send rows | recv rows] int64
     HostBuf h_send, h_recv;              // host-buffer transports
@@ -120,7 +121,8 @@ void xstate_free(XState* x) {
     (void)x->drain();
     for (DevBuf* b : {&x->hdr_send[0], &x->hdr_send[1], &x->hdr_recv[0], &x->hdr_recv[1], &x->counts, &x->offsets,
                       &x->one_idx, &x->fill, &x->send_idx[0], &x->send_idx[1], &x->send_vals[0], &x->send_vals[1],
-                      &x->recv_idx[0], &x->recv_idx[1], &x->recv_vals[0], &x->recv_vals[1], &x->back, &x->back_ok})
+                      &x->recv_idx[0], &x->recv_idx[1], &x->recv_vals[0], &x->recv_vals[1], &x->back, &x->back_ok,
+                      &x->ovf_idx, &x->ovf_vals, &x->ovf_count})
         b->release();
     for (auto* v : {&x->pos, &x->res, &x->rok})
         for (DevBuf& b : *v) b.release();
@@ -153,10 +155,10 @@ static hipError_t xstate_init(XState* x) {
     return e;
 }
 
-// per-PE header rows of one chunk: [count, MVSI local index or -1, flags (LMR_XHDR_SCALAR |
-// LMR_XHDR_ORDERED), scalar bits, chunk count]
+// per-PE header rows of one chunk: [count, MVSI local index or -1, flags (LMR_XHDR_*), scalar
+// bits, chunk count, packed records of the batch, chunk size]
 __global__ void k_xhdr(const uint64_t* counts, uint32_t npes, int64_t mvsi_pe, int64_t mvsi_off, int64_t mvsi_n,
-                       int64_t flags, uint64_t sbits, int64_t my_k, int64_t* hdr) {
+                       int64_t flags, uint64_t sbits, int64_t my_k, int64_t m, int64_t chunk, int64_t* hdr) {
     const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
     if (p >= npes) return;
     int64_t* r = hdr + uint64_t(p) * LMR_XHDR_WORDS;
@@ -166,6 +168,8 @@ __global__ void k_xhdr(const uint64_t* counts, uint32_t npes, int64_t mvsi_pe, i
     r[2] = flags;
     r[3] = int64_t(sbits);
     r[4] = my_k;
+    r[5] = m;
+    r[6] = chunk;
 }
 
 }  // namespace lmr
@@ -361,6 +365,13 @@ bool self_bypass_enabled() {
     return !(e && e[0] == 't');
 }
 
+// fixed-region mode (LAMELLAR_EXCHANGE_FIXED=0 turns it off; every PE must set it alike): whole
+// fixed regions on the wire, device-side counts at the owner, no host read of later chunks' rows
+bool fixed_mode_enabled() {
+    const char* e = getenv("LAMELLAR_EXCHANGE_FIXED");
+    return !(e && e[0] == '0');
+}
+
 uint64_t exchange_chunk() {
     const char* e = getenv("LAMELLAR_EXCHANGE_CHUNK");
     uint64_t c = (e && *e) ? strtoull(e, nullptr, 10) : (uint64_t(1) << 26);
@@ -374,6 +385,8 @@ uint64_t exchange_chunk() {
 uint32_t unit_for(uint32_t w) { return (w % 8 == 0) ? 8 : (w % 4 == 0 ? 4 : 1); }
 
 }  // namespace
+
+uint64_t lmr::exchange_chunk_records() { return exchange_chunk(); }
 
 extern "C" {
 
@@ -519,17 +532,26 @@ lmr_status_t lmr_batch_exchange(lmr_ctx_t* ctx, const lmr_transport_t* tp, const
         x->h_hdr.need(4 * rows * 8) != hipSuccess)
         return LMR_E_HIP;
     const uint64_t cmax = std::min<uint64_t>(m, chunk);
-    // nothing returned: the count-free pack (fixed per-PE regions, no count pass); a chunk
-    // whose records overflow a region is packed again with the counted pack
-    const bool free_pack = !returning && !ordered && npes <= 512 && free_pack_enabled();
+    // nothing returned: the count-free pack (fixed per-destination regions, no count pass);
+    // records past a destination's region go to an overflow list, exchanged after the last chunk
+    const bool free_pack = !returning && !ordered && !mvsi && npes <= 512 && free_pack_enabled();
     const uint32_t me = layout->my_pe;
     const bool bypass = npes > 1 && self_bypass_enabled();
     auto region_cap = [&](uint64_t c) -> uint64_t {
         const uint64_t q = (c + npes - 1) / npes;
         return q + q / 8 + 4096;
     };
+    // a sender's region capacity for its chunk j (records m, chunk size ch): 0 past its last chunk
+    auto cap_of = [&](uint64_t mm, uint64_t ch, uint64_t j) -> uint64_t {
+        if (ch == 0 || j * ch >= mm) return 0;
+        return region_cap(std::min(ch, mm - j * ch));
+    };
     const uint64_t send_recs = free_pack ? std::max<uint64_t>(cmax, uint64_t(npes) * region_cap(cmax)) : cmax;
     if (free_pack && (send_recs > 0xFFFFFFFFull || x->fill.need(size_t(npes) * 4 + 8, x) != hipSuccess))
+        return LMR_E_HIP;
+    if (free_pack && (x->ovf_idx.need(m * 8 + 16, x) != hipSuccess ||
+                      x->ovf_vals.need((scalar ? 0 : m * eb) + 16, x) != hipSuccess ||
+                      x->ovf_count.need(16, x) != hipSuccess))
         return LMR_E_HIP;
     for (int b = 0; b < 2; b++)
         if (x->send_idx[b].need(send_recs * iw + 8, x) != hipSuccess ||
@@ -540,6 +562,7 @@ lmr_status_t lmr_batch_exchange(lmr_ctx_t* ctx, const lmr_transport_t* tp, const
         hipStreamWaitEvent(x->sx, x->ev_begin, 0) != hipSuccess || hipStreamWaitEvent(x->sa, x->ev_begin, 0) != hipSuccess ||
         hipStreamWaitEvent(x->sh, x->ev_begin, 0) != hipSuccess)
         return LMR_E_HIP;
+    if (free_pack && hipMemsetAsync(x->ovf_count.p, 0, 8, x->sp) != hipSuccess) return LMR_E_HIP;
     // header rows on their own stream when the transport allows it (LMR_TRANSPORT_SPLIT_HEADERS;
     // host-buffer transports are host-ordered): chunk j+1's header exchange is posted before
     // chunk j's all-to-all-v and waits only for chunk j+1's pack, so the host's per-chunk read
@@ -550,6 +573,12 @@ lmr_status_t lmr_batch_exchange(lmr_ctx_t* ctx, const lmr_transport_t* tp, const
     x->send_used[0] = x->send_used[1] = false;
     lmr_status_t st = lmr_stage_begin(ctx, desc);
     if (st != LMR_OK) return st;
+    // fixed-region mode: a FIXED sender's regions go whole to DEVCOUNT receivers (their count-free
+    // session stages each region with its record count read on the device from the header rows),
+    // so when every PE is both the host reads no header after chunk 0
+    const bool devcount = fixed_mode_enabled() && !returning && !ordered && stage_session_free(ctx);
+    const int64_t my_flags = (scalar ? LMR_XHDR_SCALAR : 0) | (ordered ? LMR_XHDR_ORDERED : 0) |
+                             (free_pack ? LMR_XHDR_FIXED : 0) | (devcount ? LMR_XHDR_DEVCOUNT : 0);
     // a failed exchange closes the session (its staged records are dropped) so the context
     // stays usable; the work already enqueued on the internal streams drains first (after a
     // transport failure the transport is aborted first: peers may never post their halves)
@@ -587,15 +616,19 @@ lmr_status_t lmr_batch_exchange(lmr_ctx_t* ctx, const lmr_transport_t* tp, const
             ctx, layout, gidx + lo, cnt, v, desc->dtype, iw, x->send_idx[b].p, scalar ? nullptr : x->send_vals[b].p, pos,
             x->counts.as<uint64_t>(), x->offsets.as<uint64_t>(), reinterpret_cast<lmr_stream_t>(x->sp));
     };
+    // send buffer b and its header rows: chunk j-2's all-to-all-v (and, for own records staged
+    // from the send buffer or counted from the header rows, chunk j-2's staging) are done with them
+    auto wait_send_slot = [&](int b) -> lmr_status_t {
+        if (x->send_used[b] && hipStreamWaitEvent(x->sp, x->ev_send_free[b], 0) != hipSuccess) return LMR_E_HIP;
+        if (x->recv_used[b] && hipStreamWaitEvent(x->sp, x->ev_recv_free[b], 0) != hipSuccess) return LMR_E_HIP;
+        return LMR_OK;
+    };
     auto pack_chunk = [&](uint64_t j) -> lmr_status_t {
         const uint64_t lo = chunk_lo(j), cnt = chunk_hi(j) - lo;
         const int b = int(j & 1);
         const bool packed = !mvsi && j < my_k && cnt > 0;
-        // send buffer b and its header rows: chunk j-2's all-to-all-v (and, for own records
-        // staged from the send buffer, chunk j-2's staging) must be done with them
-        if (x->send_used[b] && hipStreamWaitEvent(x->sp, x->ev_send_free[b], 0) != hipSuccess) return LMR_E_HIP;
-        if (bypass && x->recv_used[b] && hipStreamWaitEvent(x->sp, x->ev_recv_free[b], 0) != hipSuccess)
-            return LMR_E_HIP;
+        lmr_status_t e = wait_send_slot(b);
+        if (e != LMR_OK) return e;
         if (returning && x->pos.size() <= j) x->pos.resize(j + 1);
         if (packed) {
             if (returning && x->pos[j].need(cnt * 4 + 8, x) != hipSuccess) return LMR_E_HIP;
@@ -615,17 +648,20 @@ lmr_status_t lmr_batch_exchange(lmr_ctx_t* ctx, const lmr_transport_t* tp, const
                 pa.err = ctx->d_err;
                 pa.prof = ctx->prof;
                 pa.stable = false;
+                pa.ovf_gidx = x->ovf_idx.as<uint64_t>();
+                pa.ovf_vals = scalar ? nullptr : x->ovf_vals.as<uint8_t>();
+                pa.ovf_count = x->ovf_count.as<uint32_t>();
+                pa.ovf_cap = m;
                 if (launch_pack_free(pa, x->fill.as<uint32_t>(), uint32_t(region_cap(cnt)), x->sp) != hipSuccess)
                     return LMR_E_HIP;
             } else {
-                const lmr_status_t e = counted_pack(j);
+                e = counted_pack(j);
                 if (e != LMR_OK) return e;
             }
         }
-        const int64_t flags = (scalar ? LMR_XHDR_SCALAR : 0) | (ordered ? LMR_XHDR_ORDERED : 0);
         hipLaunchKernelGGL(k_xhdr, dim3((npes + 255) / 256), dim3(256), 0, x->sp, packed ? x->counts.as<uint64_t>() : nullptr,
-                           npes, mvsi && j == 0 ? mvsi_pe : -1, mvsi_off, int64_t(n), flags, sbits, int64_t(my_k),
-                           x->hdr_send[b].as<int64_t>());
+                           npes, mvsi && j == 0 ? mvsi_pe : -1, mvsi_off, int64_t(n), my_flags, sbits, int64_t(my_k),
+                           int64_t(m), int64_t(chunk), x->hdr_send[b].as<int64_t>());
         if (hipGetLastError() != hipSuccess) return LMR_E_HIP;
         return hipEventRecord(x->ev_packed[b], x->sp) == hipSuccess ? LMR_OK : LMR_E_HIP;
     };
@@ -638,10 +674,12 @@ lmr_status_t lmr_batch_exchange(lmr_ctx_t* ctx, const lmr_transport_t* tp, const
         }
         return LMR_OK;
     };
-    // ---- the header all-to-all of chunk j (header stream) and its rows to the host
+    // ---- the header all-to-all of chunk j (header stream) and its rows to the host. Receive
+    // rows b are read on the device by chunk j-2's staging of fixed regions: that is done first.
     auto post_header = [&](uint64_t j) -> lmr_status_t {
         const int b = int(j & 1);
         if (hipStreamWaitEvent(shd, x->ev_packed[b], 0) != hipSuccess) return LMR_E_HIP;
+        if (x->recv_used[b] && hipStreamWaitEvent(shd, x->ev_recv_free[b], 0) != hipSuccess) return LMR_E_HIP;
         lmr_status_t e = tp_alltoall(tp, x, x->hdr_send[b].p, x->hdr_recv[b].p, LMR_XHDR_WORDS * 8, shd);
         if (e != LMR_OK) { guard.tp_failed = true; return e; }
         int64_t* hs_ = const_cast<int64_t*>(h_send_rows(b));
@@ -651,42 +689,218 @@ lmr_status_t lmr_batch_exchange(lmr_ctx_t* ctx, const lmr_transport_t* tp, const
             return LMR_E_HIP;
         return LMR_OK;
     };
+    // ---- owner side with host counts (apply stream): stage every source's records of receive
+    // buffer b (counts cnt[p]; own records from send buffer b at the given offsets when bypassed)
+    auto stage_host = [&](int b, const int64_t* h_recv, const std::vector<uint64_t>& cnt, uint64_t self_io,
+                          uint64_t self_vo, const uint8_t* send_vals, uint64_t j) -> lmr_status_t {
+        uint64_t io = 0, vo = 0, ro = 0;
+        lmr_stream_t sa = reinterpret_cast<lmr_stream_t>(x->sa);
+        lmr_status_t e;
+        for (uint32_t p = 0; p < npes;) {
+            const int64_t* r = h_recv + uint64_t(p) * LMR_XHDR_WORDS;
+            const uint64_t c = cnt[p];
+            if (c == 0) { p++; continue; }
+            void* res = returning ? x->res[j].as<uint8_t>() + ro * eb : nullptr;
+            uint8_t* okp = want_ok ? x->rok[j].as<uint8_t>() + ro : nullptr;
+            const bool own = bypass && p == me;         // this PE's own records: from the send buffer
+            const uint8_t* src_i = own ? x->send_idx[b].as<uint8_t>() + self_io : x->recv_idx[b].as<uint8_t>() + iro[p];
+            const uint8_t* src_v = own ? send_vals + self_vo : x->recv_vals[b].as<uint8_t>() + vro[p];
+            if (r[1] >= 0) {                            // MVSI: one atomic block at its index
+                lmr_apply_desc_t d = *desc;
+                e = lmr_apply_mvsi(ctx, &d, src_v, c, uint64_t(r[1]), res, okp, sa);
+                if (e != LMR_OK) return e;
+                ro += c;
+                p++;
+                continue;
+            }
+            // consecutive sources with the same value form and order flag, adjacent in the
+            // receive buffer, go in one stream (an ordered stream of several sources keeps each
+            // source's records in its order)
+            const int64_t fl = r[2] & (LMR_XHDR_SCALAR | LMR_XHDR_ORDERED), bits = r[3];
+            const bool sc = (fl & LMR_XHDR_SCALAR) != 0, ord = (fl & LMR_XHDR_ORDERED) != 0;
+            uint32_t q = p;
+            uint64_t tot = 0;
+            while (q < npes) {
+                const int64_t* w = h_recv + uint64_t(q) * LMR_XHDR_WORDS;
+                if (cnt[q] == 0) { q++; continue; }
+                if (w[1] >= 0 || (w[2] & (LMR_XHDR_SCALAR | LMR_XHDR_ORDERED)) != fl || (sc && w[3] != bits)) break;
+                if (bypass && (q == me) != own) break;  // own records are a stream of their own
+                if (!own && q != p && iro[q] != iro[p] + tot * iw) break;   // not adjacent (clamped regions)
+                tot += cnt[q];
+                q++;
+                if (own) break;
+            }
+            const uint64_t ubits = uint64_t(bits);
+            if (ord) {                                  // applied now, each element's records in stream order
+                lmr_apply_desc_t d = *desc;
+                d.strategy = LMR_STRATEGY_ORDERED;
+                e = lmr_apply_soa(ctx, &d, src_i, iw, sc ? nullptr : src_v, sc ? &ubits : nullptr, tot, res, okp, sa);
+            } else {
+                e = lmr_stage_soa(ctx, src_i, iw, sc ? nullptr : src_v, sc ? &ubits : nullptr, tot, res, okp, sa);
+            }
+            if (e != LMR_OK) return e;
+            ro += tot;
+            p = q;
+        }
+        (void)io; (void)vo;
+        return LMR_OK;
+    };
+    uint64_t nchunks = 1;
+    bool nowait = false, any_fixed = false;
+    std::vector<int64_t> src_m(npes), src_ch(npes), src_fl(npes), src_bits(npes);
+    // ---- the peer transport's push: one host handshake per batch; if every PE packs and stages
+    // fixed regions that fit the receive regions, every sender's pack writes straight into the
+    // owners' regions (lmr_peer.hip) and nothing else crosses between the PEs but the mailbox
+    PeerTransport* peer = peer_of(tp);
+    bool push = false;
+    if (peer) {
+        std::vector<int64_t> pi;
+        const int64_t fits = (!free_pack || region_cap(cmax) <= peer_region_records(peer)) ? 1 : 0;
+        const int64_t info[8] = {my_flags, int64_t(m), int64_t(chunk), int64_t(my_k), int64_t(sbits), fits, 0, 0};
+        if ((st = peer_handshake(peer, info, pi)) != LMR_OK) return st;
+        push = iw <= 8 && eb <= 8;
+        for (uint32_t p = 0; p < npes; p++) {
+            const int64_t* r = pi.data() + size_t(p) * 8;
+            push = push && (r[0] & LMR_XHDR_FIXED) && (r[0] & LMR_XHDR_DEVCOUNT) && r[5];
+            src_fl[p] = r[0];
+            src_m[p] = r[1];
+            src_ch[p] = r[2];
+            src_bits[p] = r[4];
+            nchunks = std::max<uint64_t>(nchunks, uint64_t(std::max<int64_t>(r[3], 1)));
+        }
+    }
+    if (push) {
+        any_fixed = true;
+        uint32_t* fill = x->fill.as<uint32_t>();
+        for (uint64_t j = 0; j < nchunks; j++) {
+            const int b = int(j & 1);
+            const uint64_t seq = peer_chunk_seq(peer, j);
+            // sender (pack stream): every owner has consumed this parity's region, then the pack
+            // writes each owner's runs into it and the counts are published
+            if (peer_wait_freed(peer, b, ctx->d_err, x->sp) != hipSuccess) return LMR_E_HIP;
+            const uint64_t lo = chunk_lo(j), cnt = chunk_hi(j) - lo;
+            if (j < my_k && cnt > 0) {
+                PackArgs pa;
+                pa.layout = *layout;
+                pa.gidx = gidx + lo;
+                pa.vals = scalar ? nullptr : static_cast<const uint8_t*>(d_vals) + lo * eb;
+                pa.val_bytes = eb;
+                pa.n = cnt;
+                pa.index_size = iw;
+                pa.out_idx = nullptr;
+                pa.out_vals = nullptr;
+                pa.out_pos = nullptr;
+                pa.dest_counts = x->counts.as<uint64_t>();
+                pa.dest_offsets = nullptr;
+                pa.err = ctx->d_err;
+                pa.prof = ctx->prof;
+                pa.stable = false;
+                pa.ovf_gidx = x->ovf_idx.as<uint64_t>();
+                pa.ovf_vals = scalar ? nullptr : x->ovf_vals.as<uint8_t>();
+                pa.ovf_count = x->ovf_count.as<uint32_t>();
+                pa.ovf_cap = m;
+                pa.out_idx_tab = peer_idx_table(peer, b);
+                pa.out_vals_tab = scalar ? nullptr : peer_vals_table(peer, b);
+                if (launch_pack_free(pa, fill, uint32_t(region_cap(cnt)), x->sp) != hipSuccess) return LMR_E_HIP;
+            } else if (hipMemsetAsync(fill, 0, size_t(npes) * 4, x->sp) != hipSuccess) {
+                return LMR_E_HIP;
+            }
+            if (peer_publish(peer, b, fill, seq, x->sp) != hipSuccess) return LMR_E_HIP;
+            // owner (apply stream): every source has published, each region staged with its count
+            if (peer_wait_published(peer, b, seq, ctx->d_err, x->sa) != hipSuccess) return LMR_E_HIP;
+            for (uint32_t p = 0; p < npes; p++) {
+                const uint64_t cap = cap_of(uint64_t(std::max<int64_t>(src_m[p], 0)),
+                                            uint64_t(std::max<int64_t>(src_ch[p], 0)), j);
+                if (cap == 0) continue;
+                const bool sc = (src_fl[p] & LMR_XHDR_SCALAR) != 0;
+                const uint64_t ch = uint64_t(std::max<int64_t>(src_ch[p], 1));
+                const uint64_t expect = (std::min(ch, uint64_t(std::max<int64_t>(src_m[p], 0))) + npes - 1) / npes;
+                const uint64_t ubits = uint64_t(src_bits[p]);
+                st = stage_soa_dev(ctx, peer_recv_idx(peer, p, b), iw, sc ? nullptr : peer_recv_vals(peer, p, b),
+                                   sc ? &ubits : nullptr, cap, expect, peer_recv_count(peer, p, b), x->sa);
+                if (st != LMR_OK) return st;
+            }
+            if ((st = lmr_stage_flush(ctx, reinterpret_cast<lmr_stream_t>(x->sa))) != LMR_OK) return st;
+            if (peer_mark_free(peer, b, seq, x->sa) != hipSuccess) return LMR_E_HIP;
+        }
+    } else {
     // chunk 0: pack, header exchange; chunk 1's pack (local work) runs during the wait
     if ((st = pack_until(1)) != LMR_OK) return st;
     if ((st = post_header(0)) != LMR_OK) return st;
     if ((st = pack_until(std::min<uint64_t>(my_k, 2))) != LMR_OK) return st;
-    uint64_t nchunks = 1;
+    nchunks = 1;
     for (uint64_t j = 0; j < nchunks; j++) {
         const int b = int(j & 1);
-        // ---- the host reads chunk j's header rows (one wait per chunk: RCCL's send / recv
-        // counts are host arguments); meanwhile the pack stream runs chunk j+1's pack and the
-        // apply stream chunk j-1's staging
-        if (hipEventSynchronize(x->ev_hdr[b]) != hipSuccess) return LMR_E_HIP;
         const int64_t* h_send = h_send_rows(b);
         const int64_t* h_recv = h_recv_rows(b);
-        const uint64_t k = lmr_exchange_plan(npes, iw, eb, h_send, h_recv, isb.data(), iso.data(), irb.data(),
-                                             iro.data(), vsb.data(), vso.data(), vrb.data(), vro.data());
-        if (j == 0) nchunks = std::max<uint64_t>(k, 1);
+        if (j == 0 || !nowait) {
+            // ---- the host reads chunk j's header rows (RCCL's send / recv counts are host
+            // arguments); meanwhile the pack stream runs chunk j+1's pack and the apply stream
+            // chunk j-1's staging
+            if (hipEventSynchronize(x->ev_hdr[b]) != hipSuccess) return LMR_E_HIP;
+            const uint64_t k = lmr_exchange_plan(npes, iw, eb, h_send, h_recv, isb.data(), iso.data(), irb.data(),
+                                                 iro.data(), vsb.data(), vso.data(), vrb.data(), vro.data());
+            if (j == 0) {
+                nchunks = std::max<uint64_t>(k, 1);
+                nowait = true;
+                for (uint32_t p = 0; p < npes; p++) {
+                    const int64_t* r = h_recv + uint64_t(p) * LMR_XHDR_WORDS;
+                    src_fl[p] = r[2];
+                    src_bits[p] = r[3];
+                    src_m[p] = r[5];
+                    src_ch[p] = r[6];
+                    any_fixed = any_fixed || (r[2] & LMR_XHDR_FIXED);
+                    nowait = nowait && (r[2] & LMR_XHDR_FIXED) && (r[2] & LMR_XHDR_DEVCOUNT);
+                }
+            }
+        }
         if (split && j + 1 < nchunks) {                 // the next header before this chunk's records
             if ((st = pack_until(j + 2)) != LMR_OK) return st;
             if ((st = post_header(j + 1)) != LMR_OK) return st;
         }
         const uint64_t lo = chunk_lo(j), hi = chunk_hi(j);
-        if (!mvsi && j < my_k && hi > lo && free_pack) {
-            const uint32_t cap = uint32_t(region_cap(hi - lo));
-            bool over = false;
-            for (uint32_t p = 0; p < npes; p++) over = over || h_send[p * LMR_XHDR_WORDS] > int64_t(cap);
-            if (over) {                                 // same counts, contiguous layout: the plan's offsets
-                st = counted_pack(j);
-                if (st != LMR_OK) return st;
-                if (hipEventRecord(x->ev_packed[b], x->sp) != hipSuccess ||
-                    hipStreamWaitEvent(x->sx, x->ev_packed[b], 0) != hipSuccess)
-                    return LMR_E_HIP;
-            } else {                                    // sends start at each PE's region
-                for (uint32_t p = 0; p < npes; p++) {
-                    iso[p] = uint64_t(p) * cap * iw;
-                    vso[p] = uint64_t(p) * cap * eb;
+        const uint64_t my_cap = free_pack ? cap_of(m, chunk, j) : 0;
+        std::vector<uint64_t> capr(npes, 0), cnt(npes, 0);
+        for (uint32_t p = 0; p < npes; p++)
+            if (src_fl[p] & LMR_XHDR_FIXED) capr[p] = cap_of(uint64_t(std::max<int64_t>(src_m[p], 0)),
+                                                          uint64_t(std::max<int64_t>(src_ch[p], 0)), j);
+        if (nowait) {
+            // whole fixed regions both ways: every size follows from chunk 0's rows
+            uint64_t a = 0, c = 0;
+            for (uint32_t p = 0; p < npes; p++) {
+                isb[p] = my_cap * iw;
+                iso[p] = uint64_t(p) * my_cap * iw;
+                vsb[p] = scalar ? 0 : my_cap * eb;
+                vso[p] = scalar ? 0 : uint64_t(p) * my_cap * eb;
+                irb[p] = capr[p] * iw;
+                iro[p] = a; a += irb[p];
+                vrb[p] = (src_fl[p] & LMR_XHDR_SCALAR) ? 0 : capr[p] * eb;
+                vro[p] = c; c += vrb[p];
+            }
+        } else {
+            // exact counts; a FIXED sender's region holds at most its capacity (the rest is in its
+            // overflow list) and starts at the region's base
+            for (uint32_t p = 0; p < npes; p++) {
+                const uint64_t sc_ = uint64_t(std::max<int64_t>(h_send[p * LMR_XHDR_WORDS], 0));
+                const uint64_t rc_ = uint64_t(std::max<int64_t>(h_recv[p * LMR_XHDR_WORDS], 0));
+                if (free_pack && !mvsi && j < my_k && hi > lo) {
+                    const uint64_t s1 = std::min(sc_, my_cap);
+                    isb[p] = s1 * iw;
+                    iso[p] = uint64_t(p) * my_cap * iw;
+                    vsb[p] = scalar ? 0 : s1 * eb;
+                    vso[p] = scalar ? 0 : uint64_t(p) * my_cap * eb;
                 }
+                if (h_recv[p * LMR_XHDR_WORDS + 2] & LMR_XHDR_FIXED) {
+                    const uint64_t r1 = std::min(rc_, capr[p]);
+                    irb[p] = h_recv[p * LMR_XHDR_WORDS + 1] < 0 ? r1 * iw : 0;
+                    vrb[p] = (h_recv[p * LMR_XHDR_WORDS + 2] & LMR_XHDR_SCALAR) ? 0 : r1 * eb;
+                }
+                cnt[p] = (h_recv[p * LMR_XHDR_WORDS + 2] & LMR_XHDR_FIXED) ? std::min(rc_, capr[p]) : rc_;
+            }
+            uint64_t a = 0, c = 0;
+            for (uint32_t p = 0; p < npes; p++) {
+                iro[p] = a; a += irb[p];
+                vro[p] = c; c += vrb[p];
             }
         }
         // own records: out of the transport's splits (the receive layout keeps their gap)
@@ -698,17 +912,21 @@ lmr_status_t lmr_batch_exchange(lmr_ctx_t* ctx, const lmr_transport_t* tp, const
         cr.send_cnt.resize(npes);
         cr.recv_cnt.resize(npes);
         cr.total = 0;
-        for (uint32_t p = 0; p < npes; p++) {
-            cr.send_cnt[p] = uint64_t(std::max<int64_t>(h_send[p * LMR_XHDR_WORDS], 0));
-            cr.recv_cnt[p] = uint64_t(std::max<int64_t>(h_recv[p * LMR_XHDR_WORDS], 0));
-            cr.total += cr.recv_cnt[p];
-        }
+        if (!nowait)
+            for (uint32_t p = 0; p < npes; p++) {
+                cr.send_cnt[p] = uint64_t(std::max<int64_t>(h_send[p * LMR_XHDR_WORDS], 0));
+                cr.recv_cnt[p] = cnt[p];
+                cr.total += cr.recv_cnt[p];
+            }
         // ---- receive buffers of this chunk (double-buffered against the apply stream)
         if (x->recv_used[b] && hipStreamWaitEvent(x->sx, x->ev_recv_free[b], 0) != hipSuccess) return LMR_E_HIP;
         const uint64_t ib = iro[npes - 1] + irb[npes - 1], vb = vro[npes - 1] + vrb[npes - 1];
         if (x->recv_idx[b].need(ib + 8, x) != hipSuccess || x->recv_vals[b].need(vb + 8, x) != hipSuccess)
             return LMR_E_HIP;
         const uint8_t* send_vals = mvsi ? static_cast<const uint8_t*>(d_vals) : x->send_vals[b].as<uint8_t>();
+        // the records after the chunk's header rows (and so after its pack): with no host read of
+        // the rows in between, only this orders them (and the owner's staging, which reads the rows)
+        if (nowait && hipStreamWaitEvent(x->sx, x->ev_hdr[b], 0) != hipSuccess) return LMR_E_HIP;
         st = tp_alltoallv(tp, x, x->send_idx[b].p, isb.data(), iso.data(), x->recv_idx[b].p, irb.data(), iro.data(),
                           unit_for(iw), x->sx);
         if (st == LMR_OK)
@@ -725,57 +943,29 @@ lmr_status_t lmr_batch_exchange(lmr_ctx_t* ctx, const lmr_transport_t* tp, const
             if (x->res[j].need(cr.total * eb + 8, x) != hipSuccess) return LMR_E_HIP;
             if (want_ok && x->rok[j].need(cr.total + 8, x) != hipSuccess) return LMR_E_HIP;
         }
-        uint64_t io = 0, vo = 0, ro = 0;
-        lmr_stream_t sa = reinterpret_cast<lmr_stream_t>(x->sa);
-        for (uint32_t p = 0; p < npes;) {
-            const int64_t* r = h_recv + uint64_t(p) * LMR_XHDR_WORDS;
-            const uint64_t c = cr.recv_cnt[p];
-            if (c == 0) { p++; continue; }
-            void* res = returning ? x->res[j].as<uint8_t>() + ro * eb : nullptr;
-            uint8_t* okp = want_ok ? x->rok[j].as<uint8_t>() + ro : nullptr;
-            const bool own = bypass && p == me;         // this PE's own records: from the send buffer
-            const uint8_t* src_i = own ? x->send_idx[b].as<uint8_t>() + self_io : x->recv_idx[b].as<uint8_t>() + io;
-            const uint8_t* src_v = own ? send_vals + self_vo : x->recv_vals[b].as<uint8_t>() + vo;
-            if (r[1] >= 0) {                            // MVSI: one atomic block at its index
-                lmr_apply_desc_t d = *desc;
-                st = lmr_apply_mvsi(ctx, &d, src_v, c, uint64_t(r[1]), res, okp, sa);
+        if (nowait) {
+            // fixed regions with their counts in the header rows (device), each its own stream
+            for (uint32_t p = 0; p < npes; p++) {
+                const bool own = bypass && p == me;
+                const uint64_t cap = own ? my_cap : capr[p];
+                if (cap == 0) continue;
+                const uint8_t* src_i = own ? x->send_idx[b].as<uint8_t>() + self_io : x->recv_idx[b].as<uint8_t>() + iro[p];
+                const bool sc = (src_fl[p] & LMR_XHDR_SCALAR) != 0;
+                const uint8_t* src_v = sc ? nullptr : own ? send_vals + self_vo : x->recv_vals[b].as<uint8_t>() + vro[p];
+                const int64_t* d_n = own ? x->hdr_send[b].as<int64_t>() + uint64_t(me) * LMR_XHDR_WORDS
+                                         : x->hdr_recv[b].as<int64_t>() + uint64_t(p) * LMR_XHDR_WORDS;
+                const uint64_t ch = uint64_t(std::max<int64_t>(src_ch[p], 1));
+                const uint64_t expect = (std::min(ch, uint64_t(std::max<int64_t>(src_m[p], 0))) + npes - 1) / npes;
+                const uint64_t ubits = uint64_t(src_bits[p]);
+                st = stage_soa_dev(ctx, src_i, iw, src_v, sc ? &ubits : nullptr, cap, expect, d_n, x->sa);
                 if (st != LMR_OK) return st;
-                vo += c * eb;
-                ro += c;
-                p++;
-                continue;
             }
-            // consecutive sources with the same value form and order flag go in one stream (an
-            // ordered stream of several sources keeps each source's records in its order)
-            const int64_t fl = r[2], bits = r[3];
-            const bool sc = (fl & LMR_XHDR_SCALAR) != 0, ord = (fl & LMR_XHDR_ORDERED) != 0;
-            uint32_t e = p;
-            uint64_t tot = 0;
-            while (e < npes) {
-                const int64_t* q = h_recv + uint64_t(e) * LMR_XHDR_WORDS;
-                if (cr.recv_cnt[e] == 0) { e++; continue; }
-                if (q[1] >= 0 || q[2] != fl || (sc && q[3] != bits)) break;
-                if (bypass && (e == me) != own) break;  // own records are a stream of their own
-                tot += cr.recv_cnt[e];
-                e++;
-                if (own) break;
-            }
-            const uint64_t ubits = uint64_t(bits);
-            if (ord) {                                  // applied now, each element's records in stream order
-                lmr_apply_desc_t d = *desc;
-                d.strategy = LMR_STRATEGY_ORDERED;
-                st = lmr_apply_soa(ctx, &d, src_i, iw, sc ? nullptr : src_v, sc ? &ubits : nullptr, tot, res, okp, sa);
-            } else {
-                st = lmr_stage_soa(ctx, src_i, iw, sc ? nullptr : src_v, sc ? &ubits : nullptr, tot, res, okp, sa);
-            }
+        } else {
+            st = stage_host(b, h_recv, cnt, self_io, self_vo, send_vals, j);
             if (st != LMR_OK) return st;
-            io += tot * iw;
-            if (!sc) vo += tot * eb;
-            ro += tot;
-            p = e;
         }
         // this chunk's streams partitioned now (fused), before its receive buffers are reused
-        if ((st = lmr_stage_flush(ctx, sa)) != LMR_OK) return st;
+        if ((st = lmr_stage_flush(ctx, reinterpret_cast<lmr_stream_t>(x->sa))) != LMR_OK) return st;
         if (hipEventRecord(x->ev_recv_free[b], x->sa) != hipSuccess) return LMR_E_HIP;
         x->recv_used[b] = true;
         chunks.push_back(std::move(cr));
@@ -788,6 +978,73 @@ lmr_status_t lmr_batch_exchange(lmr_ctx_t* ctx, const lmr_transport_t* tp, const
                 if ((st = post_header(j + 1)) != LMR_OK) return st;
             }
             if ((st = pack_until(std::min<uint64_t>(j + 3, nchunks))) != LMR_OK) return st;
+        }
+    }
+    }   // (not push)
+    // ---- overflow round (some PE packed fixed regions): the records that did not fit their
+    // region, from every FIXED sender's overflow list, packed by the counted pack and exchanged
+    // with exact counts (one more header exchange, read by the host once per batch)
+    if (any_fixed) {
+        const uint64_t J = nchunks;
+        const int b = int(J & 1);
+        uint64_t novf = 0;
+        if (free_pack) {
+            uint32_t c32 = 0;
+            if (hipMemcpyAsync(&c32, x->ovf_count.p, 4, hipMemcpyDeviceToHost, x->sp) != hipSuccess ||
+                hipStreamSynchronize(x->sp) != hipSuccess)
+                return LMR_E_HIP;
+            novf = std::min<uint64_t>(c32, m);
+        }
+        if ((st = wait_send_slot(b)) != LMR_OK) return st;
+        if (novf > 0) {
+            if (x->send_idx[b].need(novf * iw + 8, x) != hipSuccess ||
+                x->send_vals[b].need(novf * eb + 8, x) != hipSuccess)
+                return LMR_E_HIP;
+            st = lmr_pack_unordered(ctx, layout, x->ovf_idx.as<uint64_t>(), novf, scalar ? nullptr : x->ovf_vals.p,
+                                    desc->dtype, iw, x->send_idx[b].p, scalar ? nullptr : x->send_vals[b].p, nullptr,
+                                    x->counts.as<uint64_t>(), x->offsets.as<uint64_t>(),
+                                    reinterpret_cast<lmr_stream_t>(x->sp));
+            if (st != LMR_OK) return st;
+        }
+        hipLaunchKernelGGL(k_xhdr, dim3((npes + 255) / 256), dim3(256), 0, x->sp,
+                           novf > 0 ? x->counts.as<uint64_t>() : nullptr, npes, int64_t(-1), int64_t(0), int64_t(0),
+                           int64_t(scalar ? LMR_XHDR_SCALAR : 0), sbits, int64_t(1), int64_t(novf), int64_t(novf),
+                           x->hdr_send[b].as<int64_t>());
+        if (hipGetLastError() != hipSuccess || hipEventRecord(x->ev_packed[b], x->sp) != hipSuccess) return LMR_E_HIP;
+        if ((st = post_header(J)) != LMR_OK) return st;
+        if (hipEventSynchronize(x->ev_hdr[b]) != hipSuccess) return LMR_E_HIP;
+        const int64_t* h_send = h_send_rows(b);
+        const int64_t* h_recv = h_recv_rows(b);
+        (void)lmr_exchange_plan(npes, iw, eb, h_send, h_recv, isb.data(), iso.data(), irb.data(), iro.data(),
+                                vsb.data(), vso.data(), vrb.data(), vro.data());
+        std::vector<uint64_t> cnt(npes);
+        uint64_t any = 0;
+        for (uint32_t p = 0; p < npes; p++) {
+            cnt[p] = uint64_t(std::max<int64_t>(h_recv[p * LMR_XHDR_WORDS], 0));
+            any += cnt[p] + uint64_t(std::max<int64_t>(h_send[p * LMR_XHDR_WORDS], 0));
+        }
+        if (any) {                                      // (pairwise: both sides see the same counts)
+            const uint64_t self_io = iso[me], self_vo = vso[me];
+            if (bypass) isb[me] = irb[me] = vsb[me] = vrb[me] = 0;
+            if (x->recv_used[b] && hipStreamWaitEvent(x->sx, x->ev_recv_free[b], 0) != hipSuccess) return LMR_E_HIP;
+            const uint64_t ib = iro[npes - 1] + irb[npes - 1], vb = vro[npes - 1] + vrb[npes - 1];
+            if (x->recv_idx[b].need(ib + 8, x) != hipSuccess || x->recv_vals[b].need(vb + 8, x) != hipSuccess)
+                return LMR_E_HIP;
+            const uint8_t* send_vals = x->send_vals[b].as<uint8_t>();
+            st = tp_alltoallv(tp, x, x->send_idx[b].p, isb.data(), iso.data(), x->recv_idx[b].p, irb.data(),
+                              iro.data(), unit_for(iw), x->sx);
+            if (st == LMR_OK)
+                st = tp_alltoallv(tp, x, send_vals, vsb.data(), vso.data(), x->recv_vals[b].p, vrb.data(), vro.data(),
+                                  unit_for(eb), x->sx);
+            if (st != LMR_OK) { guard.tp_failed = true; return st; }
+            if (hipEventRecord(x->ev_send_free[b], x->sx) != hipSuccess) return LMR_E_HIP;
+            x->send_used[b] = true;
+            if (hipEventRecord(x->ev_x[b], x->sx) != hipSuccess || hipStreamWaitEvent(x->sa, x->ev_x[b], 0) != hipSuccess)
+                return LMR_E_HIP;
+            if ((st = stage_host(b, h_recv, cnt, self_io, self_vo, send_vals, J)) != LMR_OK) return st;
+            if ((st = lmr_stage_flush(ctx, reinterpret_cast<lmr_stream_t>(x->sa))) != LMR_OK) return st;
+            if (hipEventRecord(x->ev_recv_free[b], x->sa) != hipSuccess) return LMR_E_HIP;
+            x->recv_used[b] = true;
         }
     }
     // ---- one shard sweep, then results back to their senders

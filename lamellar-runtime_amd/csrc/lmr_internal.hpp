@@ -6,6 +6,7 @@
 #include <stdint.h>
 #include <stddef.h>
 #include <functional>
+#include <vector>
 #include "../../include/lamellar_gpu_ops.h"
 
 namespace lmr { struct Prof; }
@@ -206,6 +207,7 @@ struct StageRegion {
 struct PendingRegion {
     ApplyArgs a;         // the region's records (caller buffers, valid until the region is partitioned)
     int iw;
+    const int64_t* n_dev = nullptr;   // count-free only: record count in device memory (a.n: capacity)
 };
 struct StageSession {
     ApplyArgs a;         // op / kind / shard / ret of the session's current op (record fields unused)
@@ -233,8 +235,41 @@ bool stage_free_applies(int dtype, int op, int ret, uint64_t shard_len, uint64_t
 hipError_t launch_stage_region(int dtype, int index_size, const ApplyArgs& a, const TiledWs& w,
                                StageSession& s, hipStream_t st);
 hipError_t launch_stage_partition(const TiledWs& w, StageSession& s, hipStream_t st);
+// a count-free session's region whose record count is in device memory (*n_dev, clamped to a.n,
+// the region's capacity), accounted as `expect` records (the exchange's fixed receive regions)
+hipError_t launch_stage_region_dev(int dtype, int index_size, const ApplyArgs& a, const int64_t* n_dev,
+                                   uint64_t expect, const TiledWs& w, StageSession& s, hipStream_t st);
 // apply every staged region in one tile sweep, results back to each region's caller
 hipError_t launch_stage_finish(const TiledWs& w, StageSession& s, hipStream_t st);
+
+// exchange-internal staging (lmr_capi.hip): the context's open session is count-free; a
+// region of `cap` records at d_indices / d_vals whose record count is *d_n (device), accounted as
+// `expect` records
+bool stage_session_free(const lmr_ctx* ctx);
+lmr_status_t stage_soa_dev(lmr_ctx* ctx, const void* d_indices, uint32_t index_size, const void* d_vals,
+                           const void* val, uint64_t cap, uint64_t expect, const int64_t* d_n, hipStream_t s);
+
+// the exchange's default chunk (LAMELLAR_EXCHANGE_CHUNK records; lmr_exchange.hip)
+uint64_t exchange_chunk_records();
+
+// peer-memory transport (lmr_peer.hip): receive regions of R records per (source, parity) on every
+// PE, IPC-mapped; a /dev/shm mailbox of per-chunk counts and sequence numbers
+struct PeerTransport;
+PeerTransport* peer_of(const lmr_transport_t* tp);               // null unless a peer transport
+uint64_t peer_region_records(const PeerTransport* t);
+// one host handshake per batch: every PE's 8 info words (all[p * 8 + i]); also advances the batch
+// sequence that peer_chunk_seq numbers chunks from
+lmr_status_t peer_handshake(PeerTransport* t, const int64_t* my_info, std::vector<int64_t>& all);
+uint64_t peer_chunk_seq(const PeerTransport* t, uint64_t j);
+uint8_t* const* peer_idx_table(const PeerTransport* t, int b);   // device: destination q's region (this PE the source)
+uint8_t* const* peer_vals_table(const PeerTransport* t, int b);
+const uint8_t* peer_recv_idx(const PeerTransport* t, uint32_t src, int b);   // this PE's region for `src`
+const uint8_t* peer_recv_vals(const PeerTransport* t, uint32_t src, int b);
+const int64_t* peer_recv_count(const PeerTransport* t, uint32_t src, int b); // device view of its count
+hipError_t peer_wait_freed(PeerTransport* t, int b, uint32_t* err, hipStream_t s);     // parity b's regions reusable
+hipError_t peer_publish(PeerTransport* t, int b, const uint32_t* fill, uint64_t seq, hipStream_t s);
+hipError_t peer_wait_published(PeerTransport* t, int b, uint64_t seq, uint32_t* err, hipStream_t s);
+hipError_t peer_mark_free(PeerTransport* t, int b, uint64_t seq, hipStream_t s);
 
 // pack (lmr_pack.hip)
 struct PackArgs {
@@ -252,11 +287,23 @@ struct PackArgs {
     uint32_t* err;
     Prof* prof;
     bool stable;             // true: input order within a PE (lmr_pack); false: LDS-staged runs
+    // count-free pack only: records past their destination's region go to this list (global
+    // index, value) instead of being dropped; ovf_count (device) counts them (null: no list)
+    uint64_t* ovf_gidx = nullptr;
+    uint8_t* ovf_vals = nullptr;
+    uint32_t* ovf_count = nullptr;
+    uint64_t ovf_cap = 0;
+    // count-free pack only: destination i's region at out_idx_tab[i] / out_vals_tab[i] (device arrays;
+    // the peer transport's IPC-mapped receive regions) instead of out_idx / out_vals + i * cap
+    uint8_t* const* out_idx_tab = nullptr;
+    uint8_t* const* out_vals_tab = nullptr;
 };
 hipError_t launch_pack(const PackArgs& a, uint32_t* counts, uint32_t* partials, uint32_t* total,
                        hipStream_t s);
 // count-free unordered pack into fixed per-destination regions of `cap` records (nothing
-// returned; dest_counts[i] > cap: region i overflowed, pack again with launch_pack)
+// returned; dest_counts[i] > cap: region i overflowed: without an overflow list the output is
+// incomplete (pack again with launch_pack); with one, region i holds its first cap records and the
+// rest are in the list)
 hipError_t launch_pack_free(const PackArgs& a, uint32_t* fill, uint32_t cap, hipStream_t s);
 constexpr int kReduceBlocks = 1024;
 hipError_t launch_reduce(int dtype, int op, const void* x, uint64_t n, uint64_t* out, uint8_t* has,

@@ -40,6 +40,17 @@ struct PackK {
     uint32_t* err;
     uint32_t* fill;         // count-free pack: records reserved in each destination's region
     uint32_t cap;           // count-free pack: records per destination region
+    // count-free pack with an overflow list (the exchange's fixed-region mode): a record past its
+    // destination's region goes to ovf_gidx / ovf_vals[*ovf_count] (global index, value), not lost
+    uint64_t* ovf_gidx;
+    uint8_t* ovf_vals;
+    uint32_t* ovf_count;
+    uint64_t ovf_cap;
+    // count-free pack into other PEs' memory (the peer transport's push): destination i's region
+    // starts at out_idx_tab[i] / out_vals_tab[i] (device arrays of npes pointers, IPC-mapped peer
+    // regions), and every wave ends with a system-scope release so the owners see the records
+    uint8_t* const* out_idx_tab;
+    uint8_t* const* out_vals_tab;
 };
 
 // Wave-aggregated LDS counting: one atomic per distinct key in the wave instead
@@ -246,6 +257,8 @@ __global__ __launch_bounds__(1024) void k_pack_stage(PackK p) {
     const uint32_t np = p.npes;
     const int bits = key_bits(np);
     __shared__ uint32_t s_over;
+    __shared__ uint32_t s_room[FREE ? kStageMaxPes : 1], s_obase[FREE ? kStageMaxPes : 1];
+    const bool ovf = FREE && p.ovf_count != nullptr;
     if constexpr (!FREE)
         for (uint32_t i = threadIdx.x; i < np; i += blockDim.x) cursor[i] = p.counts[uint64_t(i) * p.G + blockIdx.x];
     const uint64_t lo = uint64_t(blockIdx.x) * p.chunk;
@@ -285,6 +298,11 @@ __global__ __launch_bounds__(1024) void k_pack_stage(PackK p) {
                 const uint32_t r = h ? atomicAdd(&p.fill[i], h) : 0u;
                 if (uint64_t(r) + h > p.cap) s_over = 1;
                 cursor[i] = i * p.cap + r;
+                if (ovf) {                                 // the part past the region: the overflow list
+                    const uint32_t room = r >= p.cap ? 0u : min(h, p.cap - r);
+                    s_room[i] = room;
+                    s_obase[i] = h > room ? atomicAdd(p.ovf_count, h - room) : 0u;
+                }
             }
         }
         __syncthreads();
@@ -292,22 +310,53 @@ __global__ __launch_bounds__(1024) void k_pack_stage(PackK p) {
         for (int j = 0; j < RPT; j++) {
             if (m_pe[j] == 0xFFFFFFFFu) continue;
             const uint32_t q = base[m_pe[j]] + m_rank[j];
+            if (ovf && s_over && m_rank[j] >= s_room[m_pe[j]]) {
+                const uint64_t o = uint64_t(s_obase[m_pe[j]]) + (m_rank[j] - s_room[m_pe[j]]);
+                if (o < p.ovf_cap) {
+                    p.ovf_gidx[o] = m_g[j];
+                    if (vals) reinterpret_cast<V*>(p.ovf_vals)[o] = m_v[j];
+                }
+                continue;
+            }
             s_off[q] = I(m_off[j]);
             s_val[q] = m_v[j];
             if (!FREE && p.out_pos) s_pos[q] = uint32_t(r0 + uint64_t(j) * 1024 + threadIdx.x);
         }
         if (r0 + kRound < hi) load_round(r0 + kRound);
         __syncthreads();
-        if (!FREE || !s_over)
-            bucket_writeout(hist, base, cursor, np, [&](uint32_t q, uint32_t dst) {
-                reinterpret_cast<I*>(p.out_idx)[dst] = s_off[q];
-                if (vals) reinterpret_cast<V*>(p.out_vals)[dst] = s_val[q];
-                if (!FREE && p.out_pos) p.out_pos[dst] = s_pos[q];
-            });
+        auto put = [&](uint32_t q, uint32_t dst) {
+            reinterpret_cast<I*>(p.out_idx)[dst] = s_off[q];
+            if (vals) reinterpret_cast<V*>(p.out_vals)[dst] = s_val[q];
+            if (!FREE && p.out_pos) p.out_pos[dst] = s_pos[q];
+        };
+        if (FREE && p.out_idx_tab) {                       // per-destination regions elsewhere
+            const uint32_t nw = blockDim.x >> 6, wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+            const uint32_t wpb = np >= nw ? 1u : nw / np, bstep = nw / wpb;
+            for (uint32_t c = wave / wpb; c < np; c += bstep) {
+                const uint32_t len = ovf ? s_room[c] : (s_over ? 0u : hist[c]), b = base[c];
+                const uint32_t d = cursor[c] - c * p.cap;   // offset in destination c's region
+                I* oi = reinterpret_cast<I*>(p.out_idx_tab[c]);
+                V* ov = vals ? reinterpret_cast<V*>(p.out_vals_tab[c]) : nullptr;
+                for (uint32_t i = (wave % wpb) * 64 + lane; i < len; i += wpb * 64) {
+                    oi[d + i] = s_off[b + i];
+                    if (ov) ov[d + i] = s_val[b + i];
+                }
+            }
+        } else if (!FREE || !s_over) {
+            bucket_writeout(hist, base, cursor, np, put);
+        } else if (ovf) {                                  // each destination's run up to its room
+            const uint32_t nw = blockDim.x >> 6, wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+            const uint32_t wpb = np >= nw ? 1u : nw / np, bstep = nw / wpb;
+            for (uint32_t c = wave / wpb; c < np; c += bstep) {
+                const uint32_t len = s_room[c], b = base[c], d = cursor[c];
+                for (uint32_t i = (wave % wpb) * 64 + lane; i < len; i += wpb * 64) put(b + i, d + i);
+            }
+        }
         __syncthreads();
         if constexpr (!FREE)
             for (uint32_t i = threadIdx.x; i < np; i += blockDim.x) cursor[i] += hist[i];
     }
+    if (FREE && p.out_idx_tab) __threadfence_system();    // the owners read the regions next
 }
 
 __global__ void k_fill_counts(const uint32_t* fill, uint32_t npes, uint64_t* dest_counts) {
@@ -359,6 +408,9 @@ hipError_t launch_pack(const PackArgs& a, uint32_t* counts, uint32_t* partials, 
     p.iw = a.index_size; p.chunk = (a.n + G - 1) / G; if (p.chunk == 0) p.chunk = 1;
     p.G = uint32_t(G); p.npes = npes; p.counts = counts;
     p.out_idx = a.out_idx; p.out_vals = a.out_vals; p.out_pos = a.out_pos; p.err = a.err;
+    p.fill = nullptr; p.cap = 0;
+    p.ovf_gidx = nullptr; p.ovf_vals = nullptr; p.ovf_count = nullptr; p.ovf_cap = 0;
+    p.out_idx_tab = nullptr; p.out_vals_tab = nullptr;
     ProfScope ps(a.prof, LMR_STAGE_PACK, s, a.n);
     const int mode = layout_map_mode(a.layout);
     auto by_mode = [&](auto f) {
@@ -420,6 +472,8 @@ hipError_t launch_pack_free(const PackArgs& a, uint32_t* fill, uint32_t cap, hip
     p.G = uint32_t(G); p.npes = npes; p.counts = nullptr;
     p.out_idx = a.out_idx; p.out_vals = a.out_vals; p.out_pos = nullptr; p.err = a.err;
     p.fill = fill; p.cap = cap;
+    p.ovf_gidx = a.ovf_gidx; p.ovf_vals = a.ovf_vals; p.ovf_count = a.ovf_count; p.ovf_cap = a.ovf_cap;
+    p.out_idx_tab = a.out_idx_tab; p.out_vals_tab = a.out_vals_tab;
     ProfScope ps(a.prof, LMR_STAGE_PACK, s, a.n);
     hipError_t e = hipMemsetAsync(fill, 0, size_t(npes) * 4, s);
     if (e != hipSuccess) return e;

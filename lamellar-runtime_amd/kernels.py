@@ -14,7 +14,7 @@ import numpy as np
 import torch
 
 from . import _capi
-from .types import (ERRBIT_DIVZERO, ERRBIT_OOB, ERRBIT_OVERFLOW, ERRBIT_UNSUPPORTED,
+from .types import (ERRBIT_DIVZERO, ERRBIT_OOB, ERRBIT_OVERFLOW, ERRBIT_TRANSPORT, ERRBIT_UNSUPPORTED,
                     LmrStatus, Strategy)
 
 
@@ -40,6 +40,8 @@ def errbits_to_status(bits: int) -> int:
         return LmrStatus.OVERFLOW
     if bits & ERRBIT_UNSUPPORTED:
         return LmrStatus.UNSUPPORTED
+    if bits & ERRBIT_TRANSPORT:
+        return LmrStatus.HIP
     return LmrStatus.OK
 
 

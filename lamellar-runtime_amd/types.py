@@ -82,6 +82,7 @@ ERRBIT_OOB = 0x1
 ERRBIT_DIVZERO = 0x2
 ERRBIT_OVERFLOW = 0x4
 ERRBIT_UNSUPPORTED = 0x8
+ERRBIT_TRANSPORT = 0x10
 
 
 class DType:

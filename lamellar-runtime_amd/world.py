@@ -123,6 +123,47 @@ class RcclTransport:
             self.ptr = ctypes.c_void_p()
 
 
+class PeerTransport:
+    """lmr_transport_peer_create over a base transport (RCCL or host callbacks): the exchange
+    pushes count-free records straight into the owners' IPC-mapped receive regions, with a
+    /dev/shm mailbox for counts and flags (the reference's shmem heap, shmem_comm.rs:47-80);
+    every other batch uses the base transport's collectives. PE 0 names the job's mailbox."""
+
+    def __init__(self, base, num_pes, my_pe, device, group):
+        import uuid
+        from . import _capi
+        from .kernels import check
+        self.base = base
+        obj = [uuid.uuid4().hex[:16] if my_pe == 0 else None]
+        dist.broadcast_object_list(obj, src=0, group=group)
+        recs = int(os.environ.get("LAMELLAR_PEER_REGION_RECORDS", "0"))
+        self.ptr = ctypes.c_void_p()
+        check(_capi.lib().lmr_transport_peer_create(base.ptr, obj[0].encode(), recs, device.index or 0,
+                                                     ctypes.byref(self.ptr)), "lmr_transport_peer_create")
+
+    @property
+    def self_bytes(self):
+        return getattr(self.base, "self_bytes", -1)
+
+    def stats(self):
+        """(batches handshaken, chunks pushed) -- lmr_transport_peer_stats."""
+        from . import _capi
+        b, c = ctypes.c_uint64(), ctypes.c_uint64()
+        _capi.lib().lmr_transport_peer_stats(self.ptr, ctypes.byref(b), ctypes.byref(c))
+        return b.value, c.value
+
+    def raise_pending(self):
+        self.base.raise_pending()
+
+    def close(self):
+        from . import _capi
+        if self.ptr:
+            _capi.lib().lmr_transport_peer_destroy(self.ptr)
+            self.ptr = ctypes.c_void_p()
+        if hasattr(self.base, "close"):
+            self.base.close()
+
+
 def _widen(send, recv, send_splits, recv_splits, unit):
     """View 1-D uint8 buffers as `unit`-byte integers (the record field width,
     the same on every PE, so all ranks agree on the element type) so per-peer
@@ -164,14 +205,18 @@ class LamellarTeam:
     # ---- exchange step (collective) ----
     def transport(self):
         """The lmr_transport_t of lmr_batch_exchange (made on first use, collective):
-        RCCL when the process group is "nccl", host callbacks over the group otherwise."""
+        RCCL when the process group is "nccl", host callbacks over the group otherwise;
+        LAMELLAR_TRANSPORT=peer puts the peer-memory push transport over it."""
         if self._transport is None:
             if self.group is None:
                 raise RuntimeError("the exchange needs a process group (num_pes > 1 or LAMELLAR_FORCE_EXCHANGE=1)")
             if dist.get_backend(self.group) == "nccl":
-                self._transport = RcclTransport(self._num_pes, self._my_pe, self.device, self.group)
+                t = RcclTransport(self._num_pes, self._my_pe, self.device, self.group)
             else:
-                self._transport = HostTransport(self._num_pes, self._my_pe, self.group)
+                t = HostTransport(self._num_pes, self._my_pe, self.group)
+            if os.environ.get("LAMELLAR_TRANSPORT", "") == "peer":
+                t = PeerTransport(t, self._num_pes, self._my_pe, self.device, self.group)
+            self._transport = t
         return self._transport
 
     def all_gather_object(self, obj):

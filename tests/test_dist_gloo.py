@@ -138,7 +138,7 @@ class CpuTestKernels:
         n = 0 if (i_len == 0 or v_len == 0) else max(i_len, v_len)
         mvsi, scalar = i_len == 1 and v_len > 1, v_len == 1 and not (i_len == 1 and v_len > 1)
         t = transport.t
-        hdr = np.zeros((npes, 5), np.int64)
+        hdr = np.zeros((npes, _capi_mod().XHDR_WORDS), np.int64)
         hdr[:, 1], hdr[:, 4] = -1, 1
         pos = None
         if mvsi:
@@ -155,7 +155,7 @@ class CpuTestKernels:
         if scalar:
             hdr[:, 2], hdr[:, 3] = 1, np.array([h_val_bits], np.uint64).view(np.int64)[0]
         rh = np.zeros_like(hdr)
-        assert t.alltoall(t.self, hdr.ctypes.data, rh.ctypes.data, 40, None) == 0
+        assert t.alltoall(t.self, hdr.ctypes.data, rh.ctypes.data, 8 * hdr.shape[1], None) == 0
         plan = [np.zeros(npes, np.uint64) for _ in range(8)]
         assert lib.lmr_exchange_plan(npes, iw, eb, hdr.ctypes.data, rh.ctypes.data, *[a.ctypes.data for a in plan]) == 1
         isb, iso, irb, iro, vsb, vso, vrb, vro = plan
@@ -363,9 +363,16 @@ def test_two_pe_exchange_gloo(orc, dist_kind, ragged):
 
 
 # ---------------------------------------------------------------- lmr_exchange_plan
+def _capi_mod():
+    from lamellar_runtime_amd import _capi
+    return _capi
+
+
 def _plan(_capi, npes, iw, eb, sh, rh):
     out = [np.zeros(npes, np.uint64) for _ in range(8)]
-    sh, rh = np.ascontiguousarray(sh, np.int64), np.ascontiguousarray(rh, np.int64)
+    sh, rh = np.asarray(sh, np.int64), np.asarray(rh, np.int64)
+    pad = ((0, 0), (0, _capi_mod().XHDR_WORDS - sh.shape[1]))       # words past the chunk count: 0
+    sh, rh = np.ascontiguousarray(np.pad(sh, pad)), np.ascontiguousarray(np.pad(rh, pad))
     k = _capi.lmr_exchange_plan(npes, iw, eb, sh.ctypes.data, rh.ctypes.data, *[a.ctypes.data for a in out])
     return k, out
 

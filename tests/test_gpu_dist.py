@@ -110,6 +110,15 @@ def test_two_pes_one_gpu_gloo_exchange(orc, dist_kind):
         _check(orc, d, 2, dist_kind)
 
 
+def test_peer_transport_falls_back_to_base(orc):
+    """LAMELLAR_TRANSPORT=peer with shards of <= 128 tiles (counted owner sessions), fetch_add,
+    MVSI and f64 batches: nothing here takes the push, every batch goes through the base
+    transport's collectives under the peer transport's handshake."""
+    with tempfile.TemporaryDirectory() as d:
+        _run(2, {"LAMELLAR_COMM_BACKEND": "gloo", "LAMELLAR_TRANSPORT": "peer", "LAMELLAR_PEER_TIMEOUT": "60"}, d, 0)
+        _check(orc, d, 2, 0)
+
+
 @pytest.mark.parametrize("chunk", [None, 7000], ids=["one-chunk", "chunked"])
 def test_rccl_exchange_calls_one_rank(orc, chunk):
     """chunked: LAMELLAR_EXCHANGE_CHUNK=7000 pipelines 29 chunks of the add and 3
