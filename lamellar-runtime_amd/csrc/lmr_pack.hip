@@ -356,7 +356,11 @@ __global__ __launch_bounds__(1024) void k_pack_stage(PackK p) {
         if constexpr (!FREE)
             for (uint32_t i = threadIdx.x; i < np; i += blockDim.x) cursor[i] += hist[i];
     }
-    if (FREE && p.out_idx_tab) __threadfence_system();    // the owners read the regions next
+    if (FREE && p.out_idx_tab) {                          // the owners read the regions next:
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every wave's stores done,
+        __syncthreads();                                  // then one system-scope release per block
+        if (threadIdx.x == 0) __threadfence_system();
+    }
 }
 
 __global__ void k_fill_counts(const uint32_t* fill, uint32_t npes, uint64_t* dest_counts) {

@@ -38,15 +38,19 @@ constexpr uint64_t kPeerMagic = 0x4c4d52504545520aull;   // "LMRPEER\n"
 constexpr uint32_t kPeerMaxPes = 64;
 constexpr int kInfoWords = 8;
 
+// one IPC allocation per (source, parity, index | values) region: every allocation stays far below
+// 2 GiB (a 2.4 GB receive block stalled hipIpcOpenMemHandle in the importing process; 1 GB did not)
+constexpr int kRegionAllocs = 4;          // per source: parity 0 / 1 x index / values
 struct PeSlot {
-    hipIpcMemHandle_t handle;
+    hipIpcMemHandle_t handle[kPeerMaxPes][kRegionAllocs];
     uint64_t region_recs;
     uint64_t ready;                       // 1: handle valid
-    uint64_t opened;                      // 1: this PE has mapped every peer's regions
+    uint64_t opened;                      // 1: this PE has mapped every peer's regions and built its tables
     uint64_t bseq[2];                     // batch handshake, double-buffered by batch parity
     int64_t info[2][kInfoWords];
     uint64_t closing;
-    uint64_t pad[5];
+    uint64_t mapped;                      // 1: this PE's hipIpcOpenMemHandle calls are done
+    uint64_t pad[4];
 };
 
 struct MbHeader {
@@ -167,9 +171,10 @@ struct PeerTransport {
     size_t shm_bytes = 0;
     Mailbox mb{};                         // host view
     Mailbox mbd{};                        // device view (registered mapping)
-    // receive regions: this PE's, and every PE's as mapped here
-    uint8_t* local = nullptr;
-    std::vector<uint8_t*> peer;
+    // receive regions: this PE's [source][parity * 2 + kind] (R x 8 bytes each), and, per peer q,
+    // q's regions for this PE as the source, as mapped here
+    std::vector<uint8_t*> local;
+    std::vector<uint8_t*> mapped;         // [q][parity * 2 + kind]; own entries point into `local`
     uint8_t** d_tab = nullptr;            // [2 parities][idx | vals][npes] device pointer tables
     uint64_t bseq = 0;                    // batches handshaken so far
     uint64_t last_pub[2] = {0, 0};        // sequence number last published into each parity's regions
@@ -182,9 +187,6 @@ inline size_t flag_index(uint32_t npes, uint32_t q, uint32_t p, int b) {
     return (size_t(q) * npes + p) * 2 + size_t(b);
 }
 
-uint8_t* region_of(uint8_t* base, uint64_t R, uint32_t src, int b) {
-    return base + (uint64_t(src) * 2 + uint64_t(b)) * R * 16;
-}
 
 // forwarded collectives (the base transport's): every path other than the push
 lmr_status_t peer_alltoall(void* self, const void* send, void* recv, uint64_t bytes, lmr_stream_t s) {
@@ -198,10 +200,11 @@ lmr_status_t peer_alltoallv(void* self, const void* send, const uint64_t* sb, co
 }
 
 void peer_teardown(PeerTransport* t) {
-    for (uint32_t p = 0; p < t->peer.size(); p++)
-        if (p != t->me && t->peer[p]) (void)hipIpcCloseMemHandle(t->peer[p]);
+    for (size_t i = 0; i < t->mapped.size(); i++)
+        if (i / kRegionAllocs != t->me && t->mapped[i]) (void)hipIpcCloseMemHandle(t->mapped[i]);
     if (t->d_tab) (void)hipFree(t->d_tab);
-    if (t->local) (void)hipFree(t->local);
+    for (uint8_t* l : t->local)
+        if (l) (void)hipFree(l);
     if (t->shm) {
         (void)hipHostUnregister(t->shm);
         munmap(t->shm, t->shm_bytes);
@@ -238,9 +241,11 @@ lmr_status_t peer_handshake(PeerTransport* t, const int64_t* my_info, std::vecto
 uint8_t* const* peer_idx_table(const PeerTransport* t, int b) { return t->d_tab + size_t(b) * 2 * t->npes; }
 uint8_t* const* peer_vals_table(const PeerTransport* t, int b) { return t->d_tab + (size_t(b) * 2 + 1) * t->npes; }
 
-const uint8_t* peer_recv_idx(const PeerTransport* t, uint32_t src, int b) { return region_of(t->local, t->R, src, b); }
+const uint8_t* peer_recv_idx(const PeerTransport* t, uint32_t src, int b) {
+    return t->local[size_t(src) * kRegionAllocs + size_t(b) * 2];
+}
 const uint8_t* peer_recv_vals(const PeerTransport* t, uint32_t src, int b) {
-    return region_of(t->local, t->R, src, b) + t->R * 8;
+    return t->local[size_t(src) * kRegionAllocs + size_t(b) * 2 + 1];
 }
 const int64_t* peer_recv_count(const PeerTransport* t, uint32_t src, int b) {
     return t->mbd.cnt + flag_index(t->npes, t->me, src, b);
@@ -304,12 +309,18 @@ lmr_status_t lmr_transport_peer_create(const lmr_transport_t* base, const char* 
     t->R = region_records;
     snprintf(t->name, sizeof t->name, "/lmr_peer_%s", job);
     const double to = peer_timeout_s();
+    static const bool dbg = getenv("LMR_PEER_DEBUG") != nullptr;
+    const double t_start = now_s();
+    auto step = [&](const char* what) {
+        if (dbg) fprintf(stderr, "[lmr_peer pe%u %.3f s] %s\n", t->me, now_s() - t_start, what);
+    };
     auto fail = [&](lmr_status_t st) {
         peer_teardown(t);
         if (t->me == 0 && t->shm) shm_unlink(t->name);
         delete t;
         return st;
     };
+    step("mailbox");
     // ---- the mailbox: PE 0 creates the segment, the others open it
     t->shm_bytes = mailbox_bytes(t->npes);
     int fd = -1;
@@ -323,6 +334,7 @@ lmr_status_t lmr_transport_peer_create(const lmr_transport_t* base, const char* 
     } else if (!host_wait([&] { return (fd = shm_open(t->name, O_RDWR, 0600)) >= 0; }, to)) {
         return fail(LMR_E_HIP);
     }
+    step("opened shm");
     void* m = mmap(nullptr, t->shm_bytes, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
     close(fd);
     if (m == MAP_FAILED) return fail(LMR_E_HIP);
@@ -338,6 +350,7 @@ lmr_status_t lmr_transport_peer_create(const lmr_transport_t* base, const char* 
             t->mb.hdr->npes != t->npes)
             return fail(LMR_E_HIP);
     }
+    step("mailbox ready");
     // device view of the mailbox (fine-grained: system-scope loads / stores cross GPUs and processes)
     if (hipHostRegister(m, t->shm_bytes, hipHostRegisterMapped) != hipSuccess) {
         t->shm = nullptr;
@@ -347,39 +360,57 @@ lmr_status_t lmr_transport_peer_create(const lmr_transport_t* base, const char* 
     void* md = nullptr;
     if (hipHostGetDevicePointer(&md, m, 0) != hipSuccess) return fail(LMR_E_HIP);
     t->mbd = carve(md, t->npes);
-    // ---- receive regions: [source][parity] x R records of (8-byte index slot, 8-byte value slot)
-    const size_t rbytes = size_t(t->npes) * 2 * t->R * 16;
-    if (hipMalloc(&t->local, rbytes) != hipSuccess) return fail(LMR_E_HIP);
+    step("registered");
+    // ---- receive regions: [source][parity][index | values], R x 8 bytes each
+    t->local.assign(size_t(t->npes) * kRegionAllocs, nullptr);
+    for (auto& l : t->local)
+        if (hipMalloc(reinterpret_cast<void**>(&l), t->R * 8) != hipSuccess) return fail(LMR_E_HIP);
+    step("regions allocated");
     PeSlot* mine = &t->mb.slots[t->me];
-    if (hipIpcGetMemHandle(&mine->handle, t->local) != hipSuccess) return fail(LMR_E_HIP);
+    for (uint32_t src = 0; src < t->npes; src++)
+        for (int k = 0; k < kRegionAllocs; k++)
+            if (hipIpcGetMemHandle(&mine->handle[src][k], t->local[size_t(src) * kRegionAllocs + k]) != hipSuccess)
+                return fail(LMR_E_HIP);
     mine->region_recs = t->R;
     st_rel(&mine->ready, 1);
-    t->peer.assign(t->npes, nullptr);
+    step("handles exported");
     for (uint32_t p = 0; p < t->npes; p++) {
         PeSlot* s = &t->mb.slots[p];
         if (!host_wait([&] { return ld_acq(&s->ready) == 1; }, to) || s->region_recs != t->R) return fail(LMR_E_HIP);
-        if (p == t->me) {
-            t->peer[p] = t->local;
-            continue;
-        }
-        void* pp = nullptr;
-        if (hipIpcOpenMemHandle(&pp, s->handle, hipIpcMemLazyEnablePeerAccess) != hipSuccess) return fail(LMR_E_HIP);
-        t->peer[p] = static_cast<uint8_t*>(pp);
     }
-    // pointer tables: destination q's region for this PE as the source, per parity
+    // the PEs map their regions at each other one PE at a time, in PE order
+    for (uint32_t p = 0; p < t->me; p++)
+        if (!host_wait([&] { return ld_acq(&t->mb.slots[p].mapped) == 1; }, to)) return fail(LMR_E_HIP);
+    t->mapped.assign(size_t(t->npes) * kRegionAllocs, nullptr);
+    for (uint32_t q = 0; q < t->npes; q++)
+        for (int k = 0; k < kRegionAllocs; k++) {
+            uint8_t*& dst = t->mapped[size_t(q) * kRegionAllocs + k];
+            if (q == t->me) {
+                dst = t->local[size_t(t->me) * kRegionAllocs + k];
+                continue;
+            }
+            void* pp = nullptr;
+            if (hipIpcOpenMemHandle(&pp, t->mb.slots[q].handle[t->me][k], hipIpcMemLazyEnablePeerAccess) != hipSuccess)
+                return fail(LMR_E_HIP);
+            dst = static_cast<uint8_t*>(pp);
+        }
+    st_rel(&mine->mapped, 1);
+    step("peers mapped");
+    // pointer tables: destination q's regions for this PE as the source, per parity
     std::vector<uint8_t*> tab(size_t(4) * t->npes);
     for (int b = 0; b < 2; b++)
         for (uint32_t q = 0; q < t->npes; q++) {
-            uint8_t* r = region_of(t->peer[q], t->R, t->me, b);
-            tab[size_t(b) * 2 * t->npes + q] = r;
-            tab[(size_t(b) * 2 + 1) * t->npes + q] = r + t->R * 8;
+            tab[size_t(b) * 2 * t->npes + q] = t->mapped[size_t(q) * kRegionAllocs + size_t(b) * 2];
+            tab[(size_t(b) * 2 + 1) * t->npes + q] = t->mapped[size_t(q) * kRegionAllocs + size_t(b) * 2 + 1];
         }
     if (hipMalloc(&t->d_tab, tab.size() * sizeof(uint8_t*)) != hipSuccess ||
         hipMemcpy(t->d_tab, tab.data(), tab.size() * sizeof(uint8_t*), hipMemcpyHostToDevice) != hipSuccess)
         return fail(LMR_E_HIP);
+    step("tables");
     st_rel(&mine->opened, 1);
     for (uint32_t p = 0; p < t->npes; p++)
         if (!host_wait([&] { return ld_acq(&t->mb.slots[p].opened) == 1; }, to)) return fail(LMR_E_HIP);
+    step("all opened");
     t->tp.num_pes = t->npes;
     t->tp.my_pe = t->me;
     t->tp.host_buffers = base->host_buffers;
