@@ -91,6 +91,11 @@ struct HostBuf {
 struct XState {
     hipStream_t sp = nullptr, sx = nullptr, sa = nullptr;
     hipStream_t sh = nullptr;            // header exchanges of split-header transports
+    // the peer push's device-side waits, each on a high-priority stream of its own (so a wave
+    // polling the mailbox holds no hardware queue the pack or the staging runs on); the pack and
+    // apply streams wait for them through events
+    hipStream_t sw_free = nullptr, sw_pub = nullptr;
+    hipEvent_t ev_free_ok[2] = {nullptr, nullptr}, ev_pub_ok[2] = {nullptr, nullptr}, ev_marked[2] = {nullptr, nullptr};
     hipEvent_t ev_begin = nullptr, ev_pack_done = nullptr, ev_apply_done = nullptr, ev_x_done = nullptr,
                ev_h_done = nullptr;
     hipEvent_t ev_hdr[2] = {nullptr, nullptr}, ev_x[2] = {nullptr, nullptr};
@@ -108,7 +113,7 @@ struct XState {
     // waits for the three internal streams (not the whole device: other work may share it)
     hipError_t drain() const {
         hipError_t e = hipSuccess, r;
-        for (hipStream_t s : {sp, sx, sa, sh})
+        for (hipStream_t s : {sp, sx, sa, sh, sw_free, sw_pub})
             if (s && (r = hipStreamSynchronize(s)) != hipSuccess && e == hipSuccess) e = r;
         return e;
     }
@@ -132,8 +137,11 @@ void xstate_free(XState* x) {
     for (hipEvent_t e : {x->ev_begin, x->ev_pack_done, x->ev_apply_done, x->ev_x_done, x->ev_h_done, x->ev_hdr[0],
                          x->ev_hdr[1],
                          x->ev_x[0], x->ev_x[1], x->ev_recv_free[0], x->ev_recv_free[1], x->ev_send_free[0],
-                         x->ev_send_free[1], x->ev_packed[0], x->ev_packed[1]})
+                         x->ev_send_free[1], x->ev_packed[0], x->ev_packed[1], x->ev_free_ok[0], x->ev_free_ok[1],
+                         x->ev_pub_ok[0], x->ev_pub_ok[1], x->ev_marked[0], x->ev_marked[1]})
         if (e) (void)hipEventDestroy(e);
+    if (x->sw_free) (void)hipStreamDestroy(x->sw_free);
+    if (x->sw_pub) (void)hipStreamDestroy(x->sw_pub);
     if (x->sp) (void)hipStreamDestroy(x->sp);
     if (x->sx) (void)hipStreamDestroy(x->sx);
     if (x->sa) (void)hipStreamDestroy(x->sa);
@@ -147,10 +155,16 @@ static hipError_t xstate_init(XState* x) {
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&x->sx, hipStreamNonBlocking);
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&x->sa, hipStreamNonBlocking);
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&x->sh, hipStreamNonBlocking);
+    int lo_prio = 0, hi_prio = 0;
+    if (e == hipSuccess) e = hipDeviceGetStreamPriorityRange(&lo_prio, &hi_prio);
+    if (e == hipSuccess) e = hipStreamCreateWithPriority(&x->sw_free, hipStreamNonBlocking, hi_prio);
+    if (e == hipSuccess) e = hipStreamCreateWithPriority(&x->sw_pub, hipStreamNonBlocking, hi_prio);
     for (hipEvent_t* ev : {&x->ev_begin, &x->ev_pack_done, &x->ev_apply_done, &x->ev_x_done, &x->ev_h_done,
                            &x->ev_hdr[0],
                            &x->ev_hdr[1], &x->ev_x[0], &x->ev_x[1], &x->ev_recv_free[0], &x->ev_recv_free[1],
-                           &x->ev_send_free[0], &x->ev_send_free[1], &x->ev_packed[0], &x->ev_packed[1]})
+                           &x->ev_send_free[0], &x->ev_send_free[1], &x->ev_packed[0], &x->ev_packed[1],
+                           &x->ev_free_ok[0], &x->ev_free_ok[1], &x->ev_pub_ok[0], &x->ev_pub_ok[1], &x->ev_marked[0],
+                           &x->ev_marked[1]})
         if (e == hipSuccess) e = hipEventCreateWithFlags(ev, hipEventDisableTiming);
     return e;
 }
@@ -777,7 +791,11 @@ lmr_status_t lmr_batch_exchange(lmr_ctx_t* ctx, const lmr_transport_t* tp, const
             const uint64_t seq = peer_chunk_seq(peer, j);
             // sender (pack stream): every owner has consumed this parity's region, then the pack
             // writes each owner's runs into it and the counts are published
-            if (peer_wait_freed(peer, b, ctx->d_err, x->sp) != hipSuccess) return LMR_E_HIP;
+            if (hipStreamWaitEvent(x->sw_free, x->ev_begin, 0) != hipSuccess ||
+                peer_wait_freed(peer, b, ctx->d_err, x->sw_free) != hipSuccess ||
+                hipEventRecord(x->ev_free_ok[b], x->sw_free) != hipSuccess ||
+                hipStreamWaitEvent(x->sp, x->ev_free_ok[b], 0) != hipSuccess)
+                return LMR_E_HIP;
             const uint64_t lo = chunk_lo(j), cnt = chunk_hi(j) - lo;
             if (j < my_k && cnt > 0) {
                 PackArgs pa;
@@ -807,7 +825,11 @@ lmr_status_t lmr_batch_exchange(lmr_ctx_t* ctx, const lmr_transport_t* tp, const
             }
             if (peer_publish(peer, b, fill, seq, x->sp) != hipSuccess) return LMR_E_HIP;
             // owner (apply stream): every source has published, each region staged with its count
-            if (peer_wait_published(peer, b, seq, ctx->d_err, x->sa) != hipSuccess) return LMR_E_HIP;
+            if (hipStreamWaitEvent(x->sw_pub, x->ev_begin, 0) != hipSuccess ||
+                peer_wait_published(peer, b, seq, ctx->d_err, x->sw_pub) != hipSuccess ||
+                hipEventRecord(x->ev_pub_ok[b], x->sw_pub) != hipSuccess ||
+                hipStreamWaitEvent(x->sa, x->ev_pub_ok[b], 0) != hipSuccess)
+                return LMR_E_HIP;
             for (uint32_t p = 0; p < npes; p++) {
                 const uint64_t cap = cap_of(uint64_t(std::max<int64_t>(src_m[p], 0)),
                                             uint64_t(std::max<int64_t>(src_ch[p], 0)), j);
@@ -1101,6 +1123,11 @@ lmr_status_t lmr_batch_exchange(lmr_ctx_t* ctx, const lmr_transport_t* tp, const
         hipEventRecord(x->ev_apply_done, x->sa) != hipSuccess || hipEventRecord(x->ev_h_done, x->sh) != hipSuccess ||
         hipStreamWaitEvent(s0, x->ev_pack_done, 0) != hipSuccess || hipStreamWaitEvent(s0, x->ev_x_done, 0) != hipSuccess ||
         hipStreamWaitEvent(s0, x->ev_apply_done, 0) != hipSuccess || hipStreamWaitEvent(s0, x->ev_h_done, 0) != hipSuccess)
+        return LMR_E_HIP;
+    if (push && (hipEventRecord(x->ev_marked[0], x->sw_free) != hipSuccess ||
+                 hipEventRecord(x->ev_marked[1], x->sw_pub) != hipSuccess ||
+                 hipStreamWaitEvent(s0, x->ev_marked[0], 0) != hipSuccess ||
+                 hipStreamWaitEvent(s0, x->ev_marked[1], 0) != hipSuccess))
         return LMR_E_HIP;
     return LMR_OK;
 }

@@ -362,9 +362,16 @@ lmr_status_t lmr_transport_peer_create(const lmr_transport_t* base, const char* 
     t->mbd = carve(md, t->npes);
     step("registered");
     // ---- receive regions: [source][parity][index | values], R x 8 bytes each
+    // memory kind (LMR_PEER_REGION_MEM): uncached by default -- the owner's loads never meet a line
+    // its L2 kept from the region's previous use while a peer rewrote it over xGMI; "fine"
+    // (fine-grained, coherent) or "coarse" (plain HBM) on request. On one GPU the three gave the
+    // same C4 rehearsal within 1 % (6.22 / 6.26 / 6.27 ms, profiles/r5/c4/peer_region_mem.txt)
+    const char* mk = getenv("LMR_PEER_REGION_MEM");
+    const unsigned mflags = (mk && mk[0] == 'f') ? hipDeviceMallocFinegrained
+                          : (mk && mk[0] == 'c') ? hipDeviceMallocDefault : hipDeviceMallocUncached;
     t->local.assign(size_t(t->npes) * kRegionAllocs, nullptr);
     for (auto& l : t->local)
-        if (hipMalloc(reinterpret_cast<void**>(&l), t->R * 8) != hipSuccess) return fail(LMR_E_HIP);
+        if (hipExtMallocWithFlags(reinterpret_cast<void**>(&l), t->R * 8, mflags) != hipSuccess) return fail(LMR_E_HIP);
     step("regions allocated");
     PeSlot* mine = &t->mb.slots[t->me];
     for (uint32_t src = 0; src < t->npes; src++)
