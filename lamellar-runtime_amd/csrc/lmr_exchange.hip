@@ -155,10 +155,6 @@ static hipError_t xstate_init(XState* x) {
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&x->sx, hipStreamNonBlocking);
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&x->sa, hipStreamNonBlocking);
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&x->sh, hipStreamNonBlocking);
-    int lo_prio = 0, hi_prio = 0;
-    if (e == hipSuccess) e = hipDeviceGetStreamPriorityRange(&lo_prio, &hi_prio);
-    if (e == hipSuccess) e = hipStreamCreateWithPriority(&x->sw_free, hipStreamNonBlocking, hi_prio);
-    if (e == hipSuccess) e = hipStreamCreateWithPriority(&x->sw_pub, hipStreamNonBlocking, hi_prio);
     for (hipEvent_t* ev : {&x->ev_begin, &x->ev_pack_done, &x->ev_apply_done, &x->ev_x_done, &x->ev_h_done,
                            &x->ev_hdr[0],
                            &x->ev_hdr[1], &x->ev_x[0], &x->ev_x[1], &x->ev_recv_free[0], &x->ev_recv_free[1],
@@ -166,6 +162,17 @@ static hipError_t xstate_init(XState* x) {
                            &x->ev_free_ok[0], &x->ev_free_ok[1], &x->ev_pub_ok[0], &x->ev_pub_ok[1], &x->ev_marked[0],
                            &x->ev_marked[1]})
         if (e == hipSuccess) e = hipEventCreateWithFlags(ev, hipEventDisableTiming);
+    return e;
+}
+
+// the peer push's wait streams, made on the first pushed batch only (a context that never
+// pushes holds no extra hardware queue)
+static hipError_t xstate_wait_streams(XState* x) {
+    if (x->sw_pub) return hipSuccess;
+    int lo_prio = 0, hi_prio = 0;
+    hipError_t e = hipDeviceGetStreamPriorityRange(&lo_prio, &hi_prio);
+    if (e == hipSuccess && !x->sw_free) e = hipStreamCreateWithPriority(&x->sw_free, hipStreamNonBlocking, hi_prio);
+    if (e == hipSuccess) e = hipStreamCreateWithPriority(&x->sw_pub, hipStreamNonBlocking, hi_prio);
     return e;
 }
 
@@ -784,6 +791,7 @@ lmr_status_t lmr_batch_exchange(lmr_ctx_t* ctx, const lmr_transport_t* tp, const
         }
     }
     if (push) {
+        if (xstate_wait_streams(x) != hipSuccess) return LMR_E_HIP;
         any_fixed = true;
         uint32_t* fill = x->fill.as<uint32_t>();
         for (uint64_t j = 0; j < nchunks; j++) {
@@ -1040,12 +1048,9 @@ lmr_status_t lmr_batch_exchange(lmr_ctx_t* ctx, const lmr_transport_t* tp, const
         (void)lmr_exchange_plan(npes, iw, eb, h_send, h_recv, isb.data(), iso.data(), irb.data(), iro.data(),
                                 vsb.data(), vso.data(), vrb.data(), vro.data());
         std::vector<uint64_t> cnt(npes);
-        uint64_t any = 0;
-        for (uint32_t p = 0; p < npes; p++) {
-            cnt[p] = uint64_t(std::max<int64_t>(h_recv[p * LMR_XHDR_WORDS], 0));
-            any += cnt[p] + uint64_t(std::max<int64_t>(h_send[p * LMR_XHDR_WORDS], 0));
-        }
-        if (any) {                                      // (pairwise: both sides see the same counts)
+        for (uint32_t p = 0; p < npes; p++) cnt[p] = uint64_t(std::max<int64_t>(h_recv[p * LMR_XHDR_WORDS], 0));
+        {   // every PE takes part even with nothing to send or receive: a transport's all-to-all-v
+            // may be a collective (the host transports' are)
             const uint64_t self_io = iso[me], self_vo = vso[me];
             if (bypass) isb[me] = irb[me] = vsb[me] = vrb[me] = 0;
             if (x->recv_used[b] && hipStreamWaitEvent(x->sx, x->ev_recv_free[b], 0) != hipSuccess) return LMR_E_HIP;

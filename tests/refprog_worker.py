@@ -19,6 +19,10 @@ import os
 import sys
 
 import numpy as np
+import faulthandler
+
+# a PE stuck in a collective dumps where it is (and exits) before the parent's wait runs out
+faulthandler.dump_traceback_later(int(os.environ.get("LMR_WORKER_DUMP_S", "150")), exit=True)
 
 sys.path.insert(0, os.environ["LMR_ROOT"])
 sys.path.insert(0, os.path.join(os.environ["LMR_ROOT"], "tests"))

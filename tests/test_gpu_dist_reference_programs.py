@@ -29,7 +29,7 @@ def test_reference_payloads_multi_pe(ws, dist_kind):
                                   env=dict(env, RANK=str(r), WORLD_SIZE=str(ws), LOCAL_RANK=str(r)))
                  for r in range(ws)]
         try:
-            rcs = [p.wait(timeout=280) for p in procs]
+            rcs = [p.wait(timeout=170) for p in procs]
         finally:
             for p in procs:
                 if p.poll() is None:
