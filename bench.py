@@ -80,14 +80,22 @@ def parse():
     return p.parse_args()
 
 
-def stage_bytes_per_op(stage, iw, vb, eb, n, shard_len, fetch):
+def stage_bytes_per_op(stage, iw, vb, eb, n, shard_len, fetch, wide=False):
     """Algorithmic HBM bytes per op of each kernel stage (Kernels):
     the bytes a stage must read and write per record, shard traffic amortised.
     Returned values travel binned -> temp -> input order through stored u32 maps
     (qpos written by the coarse pass, rpos by the fine pass). fetch: the share of records
-    whose op returns a value (C5: 2 of 5 batches); the un-partition counts only those."""
+    whose op returns a value (C5: 2 of 5 batches); the un-partition counts only those.
+    wide: the one-level staged partition (lmr_wide.hip: 8-byte elements, <= 2^24 of them):
+    the scatter writes u16 tile offsets and a u16 staging position per record, one gather
+    brings the olds back."""
     pos = 4 * float(fetch)
     res = eb * float(fetch)
+    if wide:
+        return {"bin_count": iw,
+                "bin_scatter": iw + vb + 2 + vb + 2 * float(fetch),
+                "tile_apply": 2 + vb + res + 2.0 * eb * shard_len / max(n, 1),
+                "unpartition": (2 + 2 * eb) if fetch else 0.0}.get(stage, 0.0)
     tile_elems = 65536 // max(eb, 4)
     two_level = (shard_len + tile_elems - 1) // tile_elems > 128
     return {
@@ -574,9 +582,11 @@ def main():
             "scope": "whole step (every kernel of the op path), SURVEY 8(d) bytes per op",
             "bytes_per_op": W.survey_bpo, "ops_per_step": W.ops_per_step, "dominant_kernel": dom}
     stage_rows = {}
+    # the wide one-level staged path (no fine pass for an 8-byte shard of <= 2^24 elements)
+    wide = W.eb == 8 and W.elems <= (1 << 24) and "fine_scatter" not in per and "tile_apply" in per
     for st, (avg_ms, lps, rpl) in per.items():
         ops_per_launch = rpl if rpl else W.ops_per_step / lps
-        bpo = stage_bytes_per_op(st, iw, W.vb, W.eb, ops_per_launch, W.elems, W.fetch)
+        bpo = stage_bytes_per_op(st, iw, W.vb, W.eb, ops_per_launch, W.elems, W.fetch, wide)
         row = {"ms_per_step": avg_ms * lps, "launches_per_step": lps, "avg_launch_ms": avg_ms,
                "records_per_launch": ops_per_launch, "bytes_per_op": bpo}
         if bpo:

@@ -2403,6 +2403,11 @@ hipError_t launch_stage_region(int dtype, int index_size, const ApplyArgs& a, co
 // regions of one index width whose count rows fit the workspace
 hipError_t launch_stage_partition(const TiledWs& w, StageSession& s, hipStream_t st) {
     if (s.free) return stage_partition_free(w, s, st);
+    if (!s.wide_set && s.parted < s.nreg) {               // one partition layout per session
+        s.wide = s.parted == 0 && wide_applies(s.dtype, s.pend[0].a.shard_len, w.cap);
+        s.wide_set = true;
+    }
+    if (s.wide) return wide_partition(w, s, st);
     const int dtype = s.dtype, vb = dtype_bytes(dtype);
     const int shift = tile_shift_for(dtype);
     while (s.parted < s.nreg) {
@@ -2543,9 +2548,12 @@ hipError_t launch_stage_finish(const TiledWs& w, StageSession& s, hipStream_t st
         if (ep != hipSuccess) {
             s.nreg = s.parted = 0;
             s.staged = s.rounds = s.crounds = 0;
+            s.wide = s.wide_set = false;
+            s.wcnt = s.wrh = 0;
             return ep;
         }
     }
+    const bool wide = s.wide;
     // the regions' op: every region's, or per region (mixed: op phases in staging order)
     ApplyArgs a = s.a;
     a.op = s.reg[0].op; a.ret = s.reg[0].ret; a.cmp_bits = s.reg[0].cmp_bits; a.eps_bits = s.reg[0].eps_bits;
@@ -2556,7 +2564,7 @@ hipError_t launch_stage_finish(const TiledWs& w, StageSession& s, hipStream_t st
         if (s.reg[r].ret != LMR_RET_NONE && (a.ret == LMR_RET_NONE || s.reg[r].ret == LMR_RET_RESULT))
             a.ret = s.reg[r].ret;                                 // maps kept if any region returns
     const int dtype = s.dtype;
-    const int shift = tile_shift_for(dtype);
+    const int shift = wide ? kWideShift8 : tile_shift_for(dtype);
     const uint32_t T = uint32_t((a.shard_len + (uint64_t(1) << shift) - 1) >> shift);
     const int vb = dtype_bytes(dtype);
     const uint32_t stride = uint32_t(kMaxTiles + 1);
@@ -2592,9 +2600,15 @@ hipError_t launch_stage_finish(const TiledWs& w, StageSession& s, hipStream_t st
         const bool delta = !mixed && op_combines(a.op) && s.staged > thresh;
         const unsigned dgrid = unsigned(std::min<uint64_t>(2 * ((s.staged + kSplit - 1) / kSplit) + 2 * uint64_t(s.nreg),
                                                            uint64_t(tile_grid_cap())));
-        e = launch_tile_kernels(dtype, mixed ? -1 : a.op, t, delta, dgrid, st, w.side);
+        e = launch_tile_kernels(dtype, mixed ? -1 : a.op, t, delta, dgrid, st, w.side, wide ? kWideBytes : kTileBytes);
     }
-    if (e == hipSuccess && has_res) {
+    if (e == hipSuccess && has_res && wide) {
+        uint64_t n_ret = 0;
+        for (int r = 0; r < s.nreg; r++)
+            if (s.reg[r].results && s.reg[r].ret != LMR_RET_NONE) n_ret += s.reg[r].n;
+        ProfScope pu(a.prof, LMR_STAGE_UNPARTITION, st, n_ret);
+        e = wide_unpartition(w, s, res_bin, ok_bin, T, st);
+    } else if (e == hipSuccess && has_res) {
         // binned -> temp slot (in-bounds slots of each region) -> arrival order
         uint64_t n_ret = 0;                                       // records whose op returns a value
         for (int r = 0; r < s.nreg; r++)
@@ -2662,6 +2676,8 @@ hipError_t launch_stage_finish(const TiledWs& w, StageSession& s, hipStream_t st
     s.staged = 0;
     s.rounds = 0;
     s.crounds = 0;
+    s.wide = s.wide_set = false;
+    s.wcnt = s.wrh = 0;
     return e;
 }
 

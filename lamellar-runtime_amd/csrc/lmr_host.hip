@@ -23,22 +23,20 @@
 // pageable memory land in a pinned slot and the host copies them out (the call then returns
 // once they are written).
 //
-// Registration contract (round 5). Three device faults (rounds 3 and 4) surfaced at the first
-// pageable host-to-device copy after host tests had registered two ranges that shared a page
-// (slices of one numpy arena, or two heap neighbours), unregistered both and freed the memory;
-// the runs that kept registered ranges allocated for the life of the process never faulted, and
-// single page-aligned registrations that are unregistered, unmapped and mapped again at the same
-// address copy cleanly (tools/hostreg_probe2.cpp, profiles/r5/hostreg_probe2.txt, scenarios 4-5).
-// What differs is one page pinned by two registrations and released by two unpins. The registry
-// therefore pins page-aligned segments only, one per set of overlapping page ranges,
-// reference-counted by the caller ranges they cover: registering a range whose pages touch an
-// existing segment re-pins the union once (after draining the library's host streams), and a
-// segment is unpinned, with its own page-aligned base, when its last caller range is unregistered.
-// No page is ever pinned twice, and no unpin leaves a page that another registration still covers.
-// Caller ranges keep their byte bounds: a copy is DMA'd in place only when it lies inside one
-// registered caller range (hipHostRegister with a pointer inside a registered range aborts the
-// process, probe scenario E: the registry refuses it with LMR_E_INVALID). Short-lived pinned
-// buffers come from lmr_host_alloc / lmr_host_free (hipHostMalloc: no user page pinning at all).
+// Registration contract (round 5). Device faults (rounds 3, 4 and once more in round 5) surfaced at
+// the first pageable host-to-device copy after host tests had registered two ranges whose pages
+// overlapped (slices of one numpy arena), unregistered both and freed the memory. Both earlier
+// registries pinned page-rounded ranges, so the shared page was locked twice (round 4) or locked,
+// unlocked and locked again inside a grown union (round 5's merged segments); single page-aligned
+// registrations that are unregistered, unmapped and mapped again at the same address copy cleanly
+// (tools/hostreg_probe2.cpp, profiles/r5/hostreg_probe2.txt, scenarios 4-5). The registry therefore
+// pins only the whole pages inside a caller's range ("inner pages": page_up(lo) .. page_down(hi)),
+// each with one hipHostRegister at a page-aligned address and one hipHostUnregister at the same
+// address: no page is ever locked by two registrations, locked twice, or locked beyond the caller's
+// own bytes. A copy DMAs the part of a buffer on those pages in place and stages the rest (under a
+// page at each end of a registered range, all of a pageable buffer) through the pinned bounce slots.
+// Overlapping caller ranges are refused (LMR_E_INVALID). Short-lived pinned buffers come from
+// lmr_host_alloc / lmr_host_free (hipHostMalloc: no user page pinning at all).
 #include "lmr_internal.hpp"
 #include "../../include/lamellar_gpu_ops.h"
 #include <stdlib.h>
@@ -55,20 +53,14 @@ namespace lmr {
 
 static const uintptr_t kHostPage = 4096;
 
-// page-aligned pinned segment [lo, hi): refs = caller ranges inside it
-struct HostSeg {
-    uintptr_t hi;
-    uint32_t refs;
-};
-// a caller range [lo, hi) and the segment holding it
+// a caller range [lo, hi) and the whole pages inside it that are pinned, [plo, phi) (plo == phi:
+// a range within two pages, nothing pinned)
 struct HostRange {
-    uintptr_t hi;
-    uintptr_t seg;
+    uintptr_t hi, plo, phi;
 };
 struct HostRegistry {
     std::mutex mu;                                   // registry maps and the stage list
-    std::shared_mutex pin;                           // shared: a call DMAs through a segment; unique: re-pin / unpin
-    std::map<uintptr_t, HostSeg> segs;
+    std::shared_mutex pin;                           // shared: a call DMAs through a range; unique: unpin
     std::map<uintptr_t, HostRange> ranges;
     std::set<HostStage*> stages;                     // every context's host stage (drained before an unpin)
     std::set<void*> allocs;                          // lmr_host_alloc blocks
@@ -76,20 +68,6 @@ struct HostRegistry {
 HostRegistry& reg() {
     static HostRegistry r;
     return r;
-}
-// true when [p, p + bytes) lies inside one registered caller range (caller holds reg().mu)
-static bool in_range_locked(uintptr_t lo, uintptr_t hi) {
-    auto& R = reg().ranges;
-    auto it = R.upper_bound(lo);
-    if (it == R.begin()) return false;
-    --it;
-    return it->first <= lo && hi <= it->second.hi;
-}
-bool host_range_registered(const void* p, uint64_t bytes) {
-    if (!p || bytes == 0) return false;
-    const uintptr_t lo = reinterpret_cast<uintptr_t>(p);
-    std::lock_guard<std::mutex> g(reg().mu);
-    return in_range_locked(lo, lo + bytes);
 }
 // memory the runtime allocated pinned (hipHostMalloc, torch's pinned allocator) covering the
 // whole range: DMA'd in place as well
@@ -106,8 +84,27 @@ static bool runtime_pinned(const void* p, uint64_t bytes) {
     if (hipPointerGetAttributes(&b, last) != hipSuccess) { (void)hipGetLastError(); return false; }
     return b.type == hipMemoryTypeHost && b.hostPointer == a.hostPointer;
 }
-static bool host_dma_ok(const void* p, uint64_t bytes) {
-    return host_range_registered(p, bytes) || runtime_pinned(p, bytes);
+// the part of [p, p + bytes) a DMA may touch in place, as offsets [*a, *b) (*a == *b: none): the
+// pinned inner pages of the registered range holding it, or all of it when the runtime allocated
+// it pinned
+static void pinned_span(const void* p, uint64_t bytes, uint64_t* a, uint64_t* b) {
+    *a = *b = 0;
+    if (!p || bytes == 0) return;
+    const uintptr_t lo = reinterpret_cast<uintptr_t>(p), hi = lo + bytes;
+    {
+        std::lock_guard<std::mutex> g(reg().mu);
+        auto& R = reg().ranges;
+        auto it = R.upper_bound(lo);
+        if (it != R.begin()) {
+            --it;
+            if (it->first <= lo && hi <= it->second.hi) {
+                const uintptr_t x = std::max(lo, it->second.plo), y = std::min(hi, it->second.phi);
+                if (x < y) { *a = x - lo; *b = y - lo; }
+                return;
+            }
+        }
+    }
+    if (runtime_pinned(p, bytes)) *b = bytes;
 }
 
 struct HostStage {
@@ -222,55 +219,13 @@ lmr_status_t lmr_host_register(void* ptr, uint64_t bytes) {
     auto it = R.ranges.lower_bound(lo);                  // overlapping an earlier caller range: refused
     if (it != R.ranges.end() && it->first < hi) return LMR_E_INVALID;
     if (it != R.ranges.begin() && std::prev(it)->second.hi > lo) return LMR_E_INVALID;
-    // the page range, grown to every segment it shares a page with
-    uintptr_t plo = page_down(lo), phi = page_up(hi);
-    std::vector<uintptr_t> merged;
-    uint32_t refs = 1;
-    for (bool grew = true; grew;) {
-        grew = false;
-        auto s = R.segs.upper_bound(plo);
-        if (s != R.segs.begin()) --s;
-        for (; s != R.segs.end() && s->first < phi; ++s) {
-            if (s->second.hi <= plo) continue;
-            if (std::find(merged.begin(), merged.end(), s->first) != merged.end()) continue;
-            merged.push_back(s->first);
-            refs += s->second.refs;
-            if (s->first < plo) { plo = s->first; grew = true; }
-            if (s->second.hi > phi) { phi = s->second.hi; grew = true; }
-        }
-    }
-    if (merged.size() == 1 && merged[0] == plo && R.segs[plo].hi == phi) {   // inside one segment's pages
-        R.segs[plo].refs = refs;
-        R.ranges[lo] = HostRange{hi, plo};
-        return LMR_OK;
-    }
-    std::vector<uintptr_t> unpinned;
-    auto restore = [&]() {                               // the old segments as they were
-        for (uintptr_t m : unpinned)
-            (void)hipHostRegister(reinterpret_cast<void*>(m), R.segs[m].hi - m, hipHostRegisterDefault);
-    };
-    if (!merged.empty()) {
-        // re-pin the union once: the library's copies through the old segments are done first
-        if (drain_host_stages_locked() != hipSuccess) return LMR_E_HIP;
-        for (uintptr_t m : merged) {
-            if (hipHostUnregister(reinterpret_cast<void*>(m)) != hipSuccess) {
-                (void)hipGetLastError();
-                restore();
-                return LMR_E_HIP;
-            }
-            unpinned.push_back(m);
-        }
-    }
-    if (hipHostRegister(reinterpret_cast<void*>(plo), phi - plo, hipHostRegisterDefault) != hipSuccess) {
+    // the whole pages inside the range: no other range's bytes share them
+    const uintptr_t plo = page_up(lo), phi = std::max(plo, page_down(hi));
+    if (phi > plo && hipHostRegister(reinterpret_cast<void*>(plo), phi - plo, hipHostRegisterDefault) != hipSuccess) {
         (void)hipGetLastError();
-        restore();
         return LMR_E_HIP;
     }
-    for (uintptr_t m : merged) R.segs.erase(m);
-    R.segs[plo] = HostSeg{phi, refs};
-    for (auto& r : R.ranges)
-        if (std::find(merged.begin(), merged.end(), r.second.seg) != merged.end()) r.second.seg = plo;
-    R.ranges[lo] = HostRange{hi, plo};
+    R.ranges[lo] = HostRange{hi, plo, phi};
     return LMR_OK;
 }
 
@@ -281,35 +236,31 @@ lmr_status_t lmr_host_unregister(void* ptr) {
     std::lock_guard<std::mutex> g(R.mu);
     auto it = R.ranges.find(reinterpret_cast<uintptr_t>(ptr));
     if (it == R.ranges.end()) return LMR_E_INVALID;      // not the start of a registration
-    auto s = R.segs.find(it->second.seg);
-    if (s == R.segs.end()) return LMR_E_INVALID;
-    if (s->second.refs > 1) {                            // the segment still covers other ranges
-        s->second.refs--;
-        R.ranges.erase(it);
-        return LMR_OK;
+    if (it->second.phi > it->second.plo) {
+        // the library's copies through the pages are done before they are unpinned
+        if (drain_host_stages_locked() != hipSuccess) return LMR_E_HIP;
+        if (hipHostUnregister(reinterpret_cast<void*>(it->second.plo)) != hipSuccess) {
+            (void)hipGetLastError();
+            return LMR_E_HIP;                            // registry unchanged: still registered
+        }
     }
-    if (drain_host_stages_locked() != hipSuccess) return LMR_E_HIP;
-    if (hipHostUnregister(reinterpret_cast<void*>(s->first)) != hipSuccess) {
-        (void)hipGetLastError();
-        return LMR_E_HIP;                                // registry unchanged: still registered
-    }
-    R.segs.erase(s);
     R.ranges.erase(it);
     return LMR_OK;
 }
 
-lmr_status_t lmr_host_registered(const void* ptr, uint64_t bytes, uint64_t* seg_base, uint64_t* seg_bytes,
-                                 uint32_t* seg_ranges) {
+lmr_status_t lmr_host_registered(const void* ptr, uint64_t bytes, uint64_t* pin_base, uint64_t* pin_bytes,
+                                 uint32_t* ranges) {
     if (!ptr || bytes == 0) return LMR_E_INVALID;
-    const uintptr_t lo = reinterpret_cast<uintptr_t>(ptr);
+    const uintptr_t lo = reinterpret_cast<uintptr_t>(ptr), hi = lo + bytes;
     HostRegistry& R = reg();
     std::lock_guard<std::mutex> g(R.mu);
-    if (!in_range_locked(lo, lo + bytes)) return LMR_E_INVALID;
-    auto r = std::prev(R.ranges.upper_bound(lo));
-    const auto& sg = R.segs.at(r->second.seg);
-    if (seg_base) *seg_base = r->second.seg;
-    if (seg_bytes) *seg_bytes = sg.hi - r->second.seg;
-    if (seg_ranges) *seg_ranges = sg.refs;
+    auto it = R.ranges.upper_bound(lo);
+    if (it == R.ranges.begin()) return LMR_E_INVALID;
+    --it;
+    if (!(it->first <= lo && hi <= it->second.hi)) return LMR_E_INVALID;
+    if (pin_base) *pin_base = it->second.plo;
+    if (pin_bytes) *pin_bytes = it->second.phi - it->second.plo;
+    if (ranges) *ranges = 1;
     return LMR_OK;
 }
 
@@ -369,20 +320,62 @@ lmr_status_t lmr_apply_mvmi_host(lmr_ctx_t* ctx, const lmr_apply_desc_t* desc, c
     const bool want_res = h_results && ret != LMR_RET_NONE;
     const bool want_ok = h_ok && ret == LMR_RET_RESULT;
     // pageable buffers go through the pinned bounce slots
-    const bool rec_pinned = host_dma_ok(h_idx_vals, n * rb);
-    const bool res_pinned = !want_res || host_dma_ok(h_results, n * eb);
-    const bool ok_pinned = !want_ok || host_dma_ok(h_ok, n);
-    if ((!rec_pinned || !res_pinned || !ok_pinned) && host_bounce_get(h) != hipSuccess) return LMR_E_HIP;
     const uint8_t* src = reinterpret_cast<const uint8_t*>(h_idx_vals);
-    // results of a bounced piece are copied out by the host once its download is done
-    struct Out { bool live = false; uint64_t r0 = 0, m = 0; };
+    // the pinned bounce slots, made on the first copy that stages anything
+    auto stage_ready = [&]() -> bool { return h->h_rec[0] || host_bounce_get(h) == hipSuccess; };
+    // host -> device: the bytes on pinned pages DMA'd in place, the rest (under a page at each end
+    // of a registered range, or all of a pageable buffer) copied by the host into slot b's bounce
+    // buffer first (once that slot's previous upload is done)
+    auto upload = [&](uint8_t* dev, const uint8_t* hp, uint64_t bytes, int b, uint64_t piece) -> lmr_status_t {
+        uint64_t x, y;
+        pinned_span(hp, bytes, &x, &y);
+        if (y > x && hipMemcpyAsync(dev + x, hp + x, y - x, hipMemcpyHostToDevice, h->h2d) != hipSuccess)
+            return LMR_E_HIP;
+        if (x == 0 && y == bytes) return LMR_OK;
+        if (!stage_ready()) return LMR_E_HIP;
+        if (piece >= 2 && hipEventSynchronize(h->copied[b]) != hipSuccess) return LMR_E_HIP;
+        if (x == y) x = y = bytes;                      // nothing pinned: one staged copy of the whole
+        uint8_t* slot = h->h_rec[b];
+        memcpy(slot, hp, x);
+        memcpy(slot + x, hp + y, bytes - y);
+        if (x > 0 && hipMemcpyAsync(dev, slot, x, hipMemcpyHostToDevice, h->h2d) != hipSuccess) return LMR_E_HIP;
+        if (bytes > y && hipMemcpyAsync(dev + y, slot + x, bytes - y, hipMemcpyHostToDevice, h->h2d) != hipSuccess)
+            return LMR_E_HIP;
+        return LMR_OK;
+    };
+    // device -> host: the pinned part in place, the rest into a bounce buffer of slot b (copied
+    // out by the host once the download is done: Part)
+    struct Part { uint8_t* dst = nullptr; const uint8_t* slot = nullptr; uint64_t x = 0, y = 0, bytes = 0; };
+    auto download = [&](uint8_t* hp, const uint8_t* dev, uint64_t bytes, uint8_t* const* slots, int b,
+                        Part* part) -> lmr_status_t {
+        uint64_t x, y;
+        pinned_span(hp, bytes, &x, &y);
+        *part = Part{};
+        if (y > x && hipMemcpyAsync(hp + x, dev + x, y - x, hipMemcpyDeviceToHost, h->d2h) != hipSuccess)
+            return LMR_E_HIP;
+        if (x == 0 && y == bytes) return LMR_OK;
+        if (!stage_ready()) return LMR_E_HIP;
+        if (x == y) x = y = bytes;
+        uint8_t* slot = slots[b];
+        if (x > 0 && hipMemcpyAsync(slot, dev, x, hipMemcpyDeviceToHost, h->d2h) != hipSuccess) return LMR_E_HIP;
+        if (bytes > y && hipMemcpyAsync(slot + x, dev + y, bytes - y, hipMemcpyDeviceToHost, h->d2h) != hipSuccess)
+            return LMR_E_HIP;
+        *part = Part{hp, slot, x, y, bytes};
+        return LMR_OK;
+    };
+    // results of a piece staged through a slot are copied out by the host once its download is done
+    struct Out { bool live = false; Part res, ok; };
     Out pend[2];
+    auto copy_out = [](const Part& q) {
+        if (!q.dst) return;
+        memcpy(q.dst, q.slot, q.x);
+        memcpy(q.dst + q.y, q.slot + q.x, q.bytes - q.y);
+    };
     auto drain_out = [&](int b) -> lmr_status_t {
         if (!pend[b].live) return LMR_OK;
         if (hipEventSynchronize(h->drained[b]) != hipSuccess) return LMR_E_HIP;
-        if (want_res && !res_pinned)
-            memcpy(static_cast<uint8_t*>(h_results) + pend[b].r0 * eb, h->h_res[b], pend[b].m * eb);
-        if (want_ok && !ok_pinned) memcpy(h_ok + pend[b].r0, h->h_ok[b], pend[b].m);
+        copy_out(pend[b].res);
+        copy_out(pend[b].ok);
         pend[b].live = false;
         return LMR_OK;
     };
@@ -390,36 +383,31 @@ lmr_status_t lmr_apply_mvmi_host(lmr_ctx_t* ctx, const lmr_apply_desc_t* desc, c
     for (uint64_t r0 = 0; r0 < n; r0 += P, i++) {
         const int b = int(i & 1);
         const uint64_t m = (n - r0 < P) ? n - r0 : P;
-        // upload: the slot's previous apply must have consumed its records
+        // upload: the slot's previous apply must have consumed its records, and the bounce slot's
+        // previous upload must be done before the host writes it again
         if (hipStreamWaitEvent(h->h2d, h->applied[b], 0) != hipSuccess) return LMR_E_HIP;
-        const uint8_t* up = src + r0 * rb;
-        if (!rec_pinned) {                             // the bounce slot's previous upload is done
-            if (i >= 2 && hipEventSynchronize(h->copied[b]) != hipSuccess) return LMR_E_HIP;
-            memcpy(h->h_rec[b], up, m * rb);
-            up = h->h_rec[b];
-        }
-        if (hipMemcpyAsync(h->d_rec[b], up, m * rb, hipMemcpyHostToDevice, h->h2d) != hipSuccess)
-            return LMR_E_HIP;
+        lmr_status_t st = upload(h->d_rec[b], src + r0 * rb, m * rb, b, i);
+        if (st != LMR_OK) return st;
         if (hipEventRecord(h->copied[b], h->h2d) != hipSuccess) return LMR_E_HIP;
         // apply on the caller's stream (after the upload and the slot's previous download)
         if (hipStreamWaitEvent(s, h->copied[b], 0) != hipSuccess) return LMR_E_HIP;
         if (hipStreamWaitEvent(s, h->drained[b], 0) != hipSuccess) return LMR_E_HIP;
-        lmr_status_t st = lmr_apply_mvmi(ctx, desc, h->d_rec[b], m * rb, index_size,
-                                         want_res ? h->d_res[b] : nullptr, want_ok ? h->d_ok[b] : nullptr, stream);
+        st = lmr_apply_mvmi(ctx, desc, h->d_rec[b], m * rb, index_size, want_res ? h->d_res[b] : nullptr,
+                            want_ok ? h->d_ok[b] : nullptr, stream);
         if (st != LMR_OK) return st;
         if (hipEventRecord(h->applied[b], s) != hipSuccess) return LMR_E_HIP;
-        // download of the returned values (into the caller's registered memory or a bounce slot)
+        // download of the returned values (into the caller's pinned pages or a bounce slot)
         if (want_res || want_ok) {
             if ((st = drain_out(b)) != LMR_OK) return st;   // the slot's previous results are out
             if (hipStreamWaitEvent(h->d2h, h->applied[b], 0) != hipSuccess) return LMR_E_HIP;
-            uint8_t* res_dst = res_pinned ? static_cast<uint8_t*>(h_results) + r0 * eb : h->h_res[b];
-            uint8_t* ok_dst = ok_pinned ? h_ok + r0 : h->h_ok[b];
-            if (want_res && hipMemcpyAsync(res_dst, h->d_res[b], m * eb, hipMemcpyDeviceToHost, h->d2h) != hipSuccess)
-                return LMR_E_HIP;
-            if (want_ok && hipMemcpyAsync(ok_dst, h->d_ok[b], m, hipMemcpyDeviceToHost, h->d2h) != hipSuccess)
-                return LMR_E_HIP;
+            Out o;
+            if (want_res && (st = download(static_cast<uint8_t*>(h_results) + r0 * eb, h->d_res[b], m * eb,
+                                           h->h_res, b, &o.res)) != LMR_OK)
+                return st;
+            if (want_ok && (st = download(h_ok + r0, h->d_ok[b], m, h->h_ok, b, &o.ok)) != LMR_OK) return st;
             if (hipEventRecord(h->drained[b], h->d2h) != hipSuccess) return LMR_E_HIP;
-            pend[b] = Out{!(res_pinned && ok_pinned), r0, m};
+            o.live = o.res.dst || o.ok.dst;
+            pend[b] = o;
         }
     }
     for (int b = 0; b < 2; b++) {

@@ -66,6 +66,10 @@ constexpr int kMaxWindows = 256;          // tiled windows per shard (lmr_window
 constexpr int kMaxRegions = 32;           // staged-apply regions per session
 constexpr int kStageInfoWords = 512;      // staged-apply piece table + per-region totals (u32)
 constexpr uint64_t kStageMaxRegion = uint64_t(1) << 30;   // records per staged region
+// the one-level ("wide") staged partition (lmr_wide.hip): 8-byte elements, 128 KiB tiles
+constexpr int kWideShift8 = 14;           // elements per wide tile: 2^14 x 8 B
+constexpr uint32_t kWideBytes = 128 * 1024;
+constexpr uint32_t kWideMaxTiles = 1024;  // a shard of at most 2^24 elements
 
 // ---- stage timing: HIP events around kernel stages (see lmr_ctx_profile) ----
 // n: records the stage processes (reported per stage by lmr_ctx_profile_read)
@@ -203,6 +207,11 @@ struct StageRegion {
     uint32_t rpb = 0;          // coarse rounds per producer block
     uint32_t kcround = 0;      // the coarse pass's LDS round (records)
     uint64_t chunk = 0;        // records per producer block
+    // wide sessions (lmr_wide.hip): the region's scanned (tile, block) slices in counts, its
+    // per-round tile counts in rpos (u16 offset), producer blocks, the group's binned base
+    uint64_t wcnt = 0, wrh = 0;
+    uint32_t wg = 0, wbase = 0;
+    bool wres = false;         // qpos / round counts kept (a returning region)
 };
 struct PendingRegion {
     ApplyArgs a;         // the region's records (caller buffers, valid until the region is partitioned)
@@ -221,6 +230,10 @@ struct StageSession {
     bool free_armed = false;
     uint32_t free_rows = 0;  // count-free sessions: tile-count rows the coarse launches used
     bool switched = false;  // the op changed with records staged (lmr_stage_op): later phases counted
+    bool wide = false;      // counted regions partitioned one-level into 128 KiB tiles (wide_applies)
+    bool wide_set = false;  //   decided at the session's first partition
+    uint64_t wcnt = 0;      // wide: count entries in use
+    uint64_t wrh = 0;       // wide: round-count entries (u16) in use
     StageRegion reg[kMaxRegions];
     PendingRegion pend[kMaxRegions];
 };
@@ -241,6 +254,13 @@ hipError_t launch_stage_region_dev(int dtype, int index_size, const ApplyArgs& a
                                    uint64_t expect, const TiledWs& w, StageSession& s, hipStream_t st);
 // apply every staged region in one tile sweep, results back to each region's caller
 hipError_t launch_stage_finish(const TiledWs& w, StageSession& s, hipStream_t st);
+// the wide path (lmr_wide.hip): applies to 8-byte element shards of <= kWideMaxTiles wide tiles
+// with a workspace whose rpos holds the round counts; partition of the pending regions; the
+// returning regions' results from binned order back to arrival order after the tile sweep
+bool wide_applies(int dtype, uint64_t shard_len, uint64_t cap);
+hipError_t wide_partition(const TiledWs& w, StageSession& s, hipStream_t st);
+hipError_t wide_unpartition(const TiledWs& w, const StageSession& s, const uint8_t* res_bin, const uint8_t* ok_bin,
+                            uint32_t num_tiles, hipStream_t st);
 
 // exchange-internal staging (lmr_capi.hip): the context's open session is count-free; a
 // region of `cap` records at d_indices / d_vals whose record count is *d_n (device), accounted as

@@ -298,7 +298,7 @@ __global__ __launch_bounds__(1024, 8) void k_tile_owner(TileArgs a) {
 // over the delta list: combine kSplit records in an identity-initialised LDS
 // tile, push one device-scope atomic per touched element, rebuild fetch
 // results as base (+) the record's LDS prefix.
-template <typename T, int OPT>
+template <typename T, int OPT, int TB = kTileBytes>
 __global__ __launch_bounds__(1024) void k_tile_delta(TileArgs a) {
     using U = typename bits_of<T>::U;
     using W = typename word_of<T>::W;
@@ -327,6 +327,7 @@ __global__ __launch_bounds__(1024) void k_tile_delta(TileArgs a) {
     const int fop = fsub ? int(LMR_OP_FETCH_ADD) : op;
     // elements some record of the piece touched (fetch forms: only those need their base)
     __shared__ uint32_t touched[16384 / 32];
+    static_assert(TB / int(sizeof(W)) <= 16384, "touched[] covers 16K elements");
     for (uint32_t it = blockIdx.x; it < nitems; it += gridDim.x) {
         const TileItem w = a.delta[it];
         const uint64_t base = uint64_t(w.tile) << a.tile_shift;
@@ -365,7 +366,7 @@ __global__ __launch_bounds__(1024) void k_tile_delta(TileArgs a) {
         __syncthreads();
         // one device-scope atomic per changed element, a load per touched unchanged one;
         // every element's operation is issued before any result is waited for
-        constexpr int kPer = kTileBytes / int(sizeof(W)) / 1024;   // elements per thread (a tile's words / 1024)
+        constexpr int kPer = TB / int(sizeof(W)) / 1024;   // elements per thread (a tile's words / 1024)
         T b[kPer];
         bool need[kPer];
 #pragma unroll
@@ -459,25 +460,50 @@ static bool delta_side_enabled() {
     return on;
 }
 
+// dynamic LDS above the default limit is declared once per kernel instantiation
+template <typename K>
+static hipError_t allow_lds(K kernel, uint32_t bytes) {
+    if (bytes <= 64 * 1024) return hipSuccess;
+    return hipFuncSetAttribute(reinterpret_cast<const void*>(kernel), hipFuncAttributeMaxDynamicSharedMemorySize,
+                               int(bytes));
+}
+
 hipError_t launch_tile_kernels(int dtype, int opt, const TileArgs& t, bool delta, unsigned dgrid, hipStream_t s,
-                               const SideLane& side) {
+                               const SideLane& side, uint32_t tile_bytes) {
     const bool lane = delta && side.s && delta_side_enabled();
+    if (tile_bytes != kTileBytes && tile_bytes != kWideBytes) return hipErrorInvalidValue;
     if (lane && (hipEventRecord(side.fork, s) != hipSuccess || hipStreamWaitEvent(side.s, side.fork, 0) != hipSuccess))
         return hipErrorUnknown;
     const hipError_t e = dispatch_dtype_t(dtype, [&](auto tag) {
         using Ty = decltype(tag);
-        auto go = [&](auto optc) {
-            constexpr int OPT = decltype(optc)::value;
+        auto go = [&](auto optc, auto tbc) {
+            constexpr int OPT = decltype(optc)::value, TB = decltype(tbc)::value;
+            auto* kd = k_tile_delta<Ty, OPT, TB>;
+            auto* ko = k_tile_owner<Ty, OPT>;
+            hipError_t ea = allow_lds(kd, TB);
+            if (ea == hipSuccess) ea = allow_lds(ko, TB);
+            if (ea != hipSuccess) return ea;
             if (lane)          // first, so its blocks start while the owner grid fills the chip
-                hipLaunchKernelGGL((k_tile_delta<Ty, OPT>), dim3(dgrid), dim3(1024), size_t(kTileBytes), side.s, t);
-            hipLaunchKernelGGL((k_tile_owner<Ty, OPT>), dim3(t.num_tiles), dim3(1024), size_t(kTileBytes), s, t);
+                hipLaunchKernelGGL(kd, dim3(dgrid), dim3(1024), size_t(TB), side.s, t);
+            hipLaunchKernelGGL(ko, dim3(t.num_tiles), dim3(1024), size_t(TB), s, t);
             if (delta && !lane)
-                hipLaunchKernelGGL((k_tile_delta<Ty, OPT>), dim3(dgrid), dim3(1024), size_t(kTileBytes), s, t);
+                hipLaunchKernelGGL(kd, dim3(dgrid), dim3(1024), size_t(TB), s, t);
+            return hipSuccess;
         };
-        if (opt == LMR_OP_ADD) go(std::integral_constant<int, LMR_OP_ADD>{});
-        else if (opt == LMR_OP_FETCH_ADD) go(std::integral_constant<int, LMR_OP_FETCH_ADD>{});
-        else go(std::integral_constant<int, -1>{});
-        return hipGetLastError();
+        auto by_op = [&](auto tbc) {
+            if (opt == LMR_OP_ADD) return go(std::integral_constant<int, LMR_OP_ADD>{}, tbc);
+            if (opt == LMR_OP_FETCH_ADD) return go(std::integral_constant<int, LMR_OP_FETCH_ADD>{}, tbc);
+            return go(std::integral_constant<int, -1>{}, tbc);
+        };
+        hipError_t el;
+        if constexpr (sizeof(Ty) == 8) {
+            if (tile_bytes == kWideBytes) el = by_op(std::integral_constant<int, int(kWideBytes)>{});
+            else el = by_op(std::integral_constant<int, kTileBytes>{});
+        } else {
+            if (tile_bytes != kTileBytes) return hipErrorInvalidValue;
+            el = by_op(std::integral_constant<int, kTileBytes>{});
+        }
+        return el != hipSuccess ? el : hipGetLastError();
     });
     // the launch stream continues after both (joined even when a launch failed)
     if (lane && (hipEventRecord(side.join, side.s) != hipSuccess || hipStreamWaitEvent(s, side.join, 0) != hipSuccess))

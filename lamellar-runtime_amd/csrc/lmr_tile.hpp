@@ -70,7 +70,8 @@ __host__ __device__ constexpr bool op_combines(int op) {
 // side lane when there is one: the two kernels touch disjoint tiles and records);
 // opt: LMR_OP_ADD / LMR_OP_FETCH_ADD select the specialised kernels, anything else the
 // generic op switch
+// tile_bytes: kTileBytes, or kWideBytes for 8-byte elements (the wide staged path's tiles)
 hipError_t launch_tile_kernels(int dtype, int opt, const TileArgs& t, bool delta, unsigned dgrid, hipStream_t s,
-                               const SideLane& side);
+                               const SideLane& side, uint32_t tile_bytes = kTileBytes);
 
 }  // namespace lmr

@@ -93,7 +93,10 @@ class DeviceKernels:
     def errors(self, clear=True) -> int:
         self.flush()
         bits = c_uint32(0)
-        self.lib.lmr_ctx_error(self.ctx, self.stream(), byref(bits), 1 if clear else 0)
+        st = self.lib.lmr_ctx_error(self.ctx, self.stream(), byref(bits), 1 if clear else 0)
+        if st == LmrStatus.HIP and not bits.value:
+            # the stream or the error-word read failed: a runtime error, not a device error bit
+            check(st, "lmr_ctx_error")
         return bits.value
 
     def check_errors(self):
@@ -272,8 +275,8 @@ class DeviceKernels:
         check(self.lib.lmr_host_unregister(arr.ctypes.data), "lmr_host_unregister")
 
     def host_registered(self, arr):
-        """(segment base, segment bytes, caller ranges in the segment) of a registered buffer,
-        or None (lmr_host_registered)."""
+        """(first pinned page, pinned bytes, 1) of the registered range holding the buffer -- the
+        whole pages inside that range, DMA'd in place -- or None (lmr_host_registered)."""
         base, nb, refs = c_uint64(0), c_uint64(0), c_uint32(0)
         st = self.lib.lmr_host_registered(arr.ctypes.data, int(arr.nbytes), byref(base), byref(nb), byref(refs))
         return (base.value, nb.value, refs.value) if st == 0 else None
