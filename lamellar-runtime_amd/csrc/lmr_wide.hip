@@ -28,8 +28,14 @@ namespace lmr {
 
 namespace {
 
+#ifndef LMR_WIDE_RPT
+#define LMR_WIDE_RPT 8
+#endif
+#ifndef LMR_WIDE_BLOCKS
+#define LMR_WIDE_BLOCKS 512
+#endif
 constexpr uint32_t kWT = 1024;                        // threads per block
-constexpr int kWideRpt = 8;                           // records per thread per round
+constexpr int kWideRpt = LMR_WIDE_RPT;                // records per thread per round
 constexpr uint32_t kWideRound = kWideRpt * kWT;       // 8K records: 96 KB of LDS staging
 static_assert(kWideRound <= 0xFFFFu, "staging positions and round counts are u16");
 static_assert(kWideMaxTiles <= kWT, "one tile counter per thread");
@@ -308,7 +314,7 @@ int wide_env() {
 }
 
 // producer blocks of a region: one per 64K records (at least), at most kWideBlocks
-constexpr uint32_t kWideBlocks = 512;
+constexpr uint32_t kWideBlocks = LMR_WIDE_BLOCKS;
 uint32_t wide_blocks(uint64_t n) {
     return uint32_t(std::max<uint64_t>(1, std::min<uint64_t>((n + 65535) / 65536, kWideBlocks)));
 }
