@@ -567,7 +567,11 @@ def main():
     pmc = os.path.join(ROOT, "profiles", f"pmc_traffic_{cfg}.json")
     if os.path.exists(pmc) and per:
         tr = json.load(open(pmc))
-        if all(st in tr for st in per if st not in ("scan",)):
+        if "_per_record" in tr and all(st in tr["_per_record"] for st in per if st not in ("scan",)):
+            # bytes per record x this run's records per launch x launches per step
+            pr = tr["_per_record"]
+            traffic = sum(pr.get(st, 0.0) * (per[st][2] or W.ops_per_step / per[st][1]) * per[st][1] for st in per)
+        elif all(st in tr for st in per if st not in ("scan",)):
             traffic = sum(tr.get(st, 0.0) * per[st][1] for st in per)
             if "pack" in per and "_transport_per_pack" in tr:     # the exchange's RCCL copies
                 traffic += tr["_transport_per_pack"] * per["pack"][1]

@@ -32,7 +32,7 @@ namespace {
 #define LMR_WIDE_RPT 8
 #endif
 #ifndef LMR_WIDE_BLOCKS
-#define LMR_WIDE_BLOCKS 512
+#define LMR_WIDE_BLOCKS 256
 #endif
 constexpr uint32_t kWT = 1024;                        // threads per block
 constexpr int kWideRpt = LMR_WIDE_RPT;                // records per thread per round

@@ -5,7 +5,10 @@ gfx950 corrections (MI355X_MICROARCH.md §HBM): FETCH_SIZE reports half the byte
 a wide coalesced stream -> doubled here; WRITE_SIZE is taken as reported.
 Stage bytes are per stage invocation: the bytes of all the stage's kernels divided
 by the launch count of the stage's anchor kernel (one launch per invocation).
-usage: tools/pmc_summary.py <prof dir with pmc_fetch/ and pmc_write/> [out.json]
+usage: tools/pmc_summary.py <prof dir with pmc_fetch/ and pmc_write/> [out.json [records per invocation]]
+With the records each stage invocation processed in the profiled run (e.g. 2^28 for a C3 session of
+four 2^26-record batches), the json also holds "_per_record": bytes per record per stage, which
+bench.py scales by its own records per launch (a session's batch count depends on the run).
 """
 import collections
 import csv
@@ -17,16 +20,18 @@ import sys
 # to the stage). Staged sessions: one bin_scatter / fine_scatter invocation per region, one
 # tile_apply / unpartition invocation per tile sweep.
 STAGES = {
-    "bin_count": (("k_bin_count", "k_ccount", "k_ccount_stage"), ("k_bin_count", "k_ccount", "k_ccount_stage")),
-    "bin_scatter": (("k_coarse_free", "k_coarse_scatter", "k_bin_scatter", "k_coarse_stage", "k_coarse_free_stage"),
+    "bin_count": (("k_bin_count", "k_ccount", "k_ccount_stage", "k_wcount_stage"),
+                  ("k_bin_count", "k_ccount", "k_ccount_stage", "k_wcount_stage", "k_wide_starts")),
+    "bin_scatter": (("k_coarse_free", "k_coarse_scatter", "k_bin_scatter", "k_coarse_stage", "k_coarse_free_stage",
+                     "k_wide_stage"),
                     ("k_coarse_free", "k_coarse_scatter", "k_coarse_offsets", "k_bin_scatter", "k_coarse_stage",
-                     "k_coarse_free_stage")),
+                     "k_coarse_free_stage", "k_wide_stage")),
     "fine_scatter": (("k_fine_free", "k_fine_scatter", "k_fine_piece", "k_fine_stage"),
                      ("k_fine_free", "k_fine_scatter", "k_fine_piece", "k_piece_count", "k_free_tile_totals",
                       "k_fine_stage")),
     "tile_apply": (("k_tile_owner",), ("k_tile_owner", "k_tile_delta", "k_tile_plan", "k_stage_plan")),
     "unpartition": (("k_tile_owner",), ("k_unpartition", "k_unpartition_multi", "k_unpart_rounds",
-                                        "k_unpart_crounds")),
+                                        "k_unpart_crounds", "k_unpart_wide")),
     "direct": (("k_apply_direct",), ("k_apply_direct",)),
     "pack": (("k_pack_count", "k_pack_stage"), ("k_pack_count", "k_pack_scatter", "k_pack_stage", "k_dest_offsets",
                                                  "k_fill_counts")),
@@ -75,6 +80,11 @@ def main():
             inv = cnt["k_pack_count"]
         out["_transport_per_pack"] = rccl / inv
         print(f"transport (RCCL kernels)  {out['_transport_per_pack'] / 1e6:10.1f} MB per pack invocation")
+    if len(sys.argv) > 3:
+        recs = float(sys.argv[3])
+        out["_per_record"] = {st: v / recs for st, v in out.items() if not st.startswith("_")}
+        for st, v in out["_per_record"].items():
+            print(f"stage {st:16s} {v:10.2f} B per record")
     if len(sys.argv) > 2:
         json.dump(out, open(sys.argv[2], "w"), indent=1)
 
