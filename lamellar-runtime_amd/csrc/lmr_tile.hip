@@ -5,6 +5,10 @@
 #include "lmr_device.hpp"
 #include <cstdlib>
 
+// records in flight per thread in k_tile_owner's 8-byte loop (A/B builds: -DLMR_OWN_UNROLL=...)
+#ifndef LMR_OWN_UNROLL
+#define LMR_OWN_UNROLL 4
+#endif
 // k_tile_owner reads 4 binned records per thread with wide loads (0: one record at a time)
 #ifndef LMR_OWN_VEC
 #define LMR_OWN_VEC 1
@@ -181,7 +185,7 @@ __global__ __launch_bounds__(1024, 8) void k_tile_owner(TileArgs a) {
     }
     __syncthreads();
     // kOwnUnroll records per thread per round: all loads issued before the LDS atomics
-    constexpr int kOwnUnroll = 4;
+    constexpr int kOwnUnroll = LMR_OWN_UNROLL;
     constexpr bool kOwnVec = LMR_OWN_VEC != 0;
     const uint32_t nrg = a.nreg ? a.nreg : 1u;
     for (uint32_t rg = 0; rg < nrg; rg++) {

@@ -31,6 +31,9 @@ namespace {
 #ifndef LMR_WIDE_RPT
 #define LMR_WIDE_RPT 8
 #endif
+#ifndef LMR_WIDE_GATHER_U
+#define LMR_WIDE_GATHER_U 4          // olds loads in flight per thread in k_unpart_wide
+#endif
 #ifndef LMR_WIDE_BLOCKS
 #define LMR_WIDE_BLOCKS 256
 #endif
@@ -228,7 +231,7 @@ template <bool OK>
 __device__ __forceinline__ void wruns_to_lds(const uint32_t* cursor, const uint32_t* base, uint32_t T,
                                              uint32_t tot, const uint64_t* __restrict__ src,
                                              const uint8_t* __restrict__ oks, uint64_t* s_v, uint8_t* s_ok) {
-    constexpr int U = 4;
+    constexpr int U = LMR_WIDE_GATHER_U;
     for (uint32_t p0 = threadIdx.x; p0 < tot; p0 += U * kWT) {
         uint32_t sp[U];
 #pragma unroll
