@@ -163,6 +163,8 @@ SIGNATURES = {
     "lmr_stage_op": (c_int, [c_void_p, c_uint32, c_uint64, c_uint64, c_void_p]),
     "lmr_stage_flush": (c_int, [c_void_p, c_void_p]),
     "lmr_stage_finish": (c_int, [c_void_p, c_void_p]),
+    "lmr_ctx_exchange_defer": (c_int, [c_void_p, c_int]),
+    "lmr_exchange_flush": (c_int, [c_void_p, c_void_p]),
     "lmr_rccl_unique_id": (c_int, [c_void_p]),
     "lmr_transport_rccl_create": (c_int, [c_void_p, c_uint32, c_uint32, c_int, POINTER(c_void_p)]),
     "lmr_transport_rccl_destroy": (c_int, [c_void_p]),

@@ -292,6 +292,13 @@ lmr_status_t run_apply(lmr_ctx* ctx, const lmr_apply_desc_t* d, ApplyArgs a, int
 namespace lmr {
 
 bool stage_session_free(const lmr_ctx* ctx) { return ctx->stage && ctx->stage->open && ctx->stage->s.free; }
+bool stage_session_open(const lmr_ctx* ctx) { return ctx->stage && ctx->stage->open; }
+bool stage_session_of(const lmr_ctx* ctx, const lmr_apply_desc_t& d) {
+    if (!stage_session_open(ctx)) return false;
+    const lmr_apply_desc_t& c = ctx->stage->desc;
+    return c.shard == d.shard && c.shard_len == d.shard_len && c.kind == d.kind && c.dtype == d.dtype &&
+           c.op == d.op && c.strategy == d.strategy && c.cmp_bits == d.cmp_bits && c.eps_bits == d.eps_bits;
+}
 
 lmr_status_t stage_soa_dev(lmr_ctx* ctx, const void* d_indices, uint32_t index_size, const void* d_vals,
                            const void* val, uint64_t cap, uint64_t expect, const int64_t* d_n, hipStream_t s) {

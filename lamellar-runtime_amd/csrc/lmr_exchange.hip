@@ -592,8 +592,16 @@ lmr_status_t lmr_batch_exchange(lmr_ctx_t* ctx, const lmr_transport_t* tp, const
     hipStream_t const shd = split ? x->sh : x->sx;
     x->recv_used[0] = x->recv_used[1] = false;
     x->send_used[0] = x->send_used[1] = false;
-    lmr_status_t st = lmr_stage_begin(ctx, desc);
-    if (st != LMR_OK) return st;
+    // a deferred exchange session left open by an earlier call: this batch adds to it when it is
+    // the same op on the same shard and stages count-free; otherwise it is applied first
+    lmr_status_t st = LMR_OK;
+    bool cont = false;
+    if (ctx->xdefer_open && stage_session_open(ctx)) {
+        cont = !returning && !ordered && stage_session_free(ctx) && stage_session_of(ctx, *desc);
+        if (!cont && (st = lmr_stage_finish(ctx, reinterpret_cast<lmr_stream_t>(x->sa))) != LMR_OK) return st;
+    }
+    ctx->xdefer_open = false;
+    if (!cont && (st = lmr_stage_begin(ctx, desc)) != LMR_OK) return st;
     // fixed-region mode: a FIXED sender's regions go whole to DEVCOUNT receivers (their count-free
     // session stages each region with its record count read on the device from the header rows),
     // so when every PE is both the host reads no header after chunk 0
@@ -1074,9 +1082,14 @@ lmr_status_t lmr_batch_exchange(lmr_ctx_t* ctx, const lmr_transport_t* tp, const
             x->recv_used[b] = true;
         }
     }
-    // ---- one shard sweep, then results back to their senders
-    st = lmr_stage_finish(ctx, reinterpret_cast<lmr_stream_t>(x->sa));
-    if (st != LMR_OK) return st;
+    // ---- one shard sweep (or, deferred, the session left open for the next batch), then results
+    // back to their senders
+    if (ctx->xdefer_on && !returning && !ordered && stage_session_free(ctx)) {
+        ctx->xdefer_open = true;
+    } else {
+        st = lmr_stage_finish(ctx, reinterpret_cast<lmr_stream_t>(x->sa));
+        if (st != LMR_OK) return st;
+    }
     guard.armed = false;
     if (returning) {
         std::vector<uint64_t> sb(npes), so(npes), rb(npes), ro(npes), osb(npes), oso(npes), orb(npes), oro(npes);
@@ -1135,6 +1148,20 @@ lmr_status_t lmr_batch_exchange(lmr_ctx_t* ctx, const lmr_transport_t* tp, const
                  hipStreamWaitEvent(s0, x->ev_marked[1], 0) != hipSuccess))
         return LMR_E_HIP;
     return LMR_OK;
+}
+
+lmr_status_t lmr_ctx_exchange_defer(lmr_ctx_t* ctx, int on) {
+    if (!ctx) return LMR_E_INVALID;
+    ctx->xdefer_on = on != 0;
+    return LMR_OK;
+}
+
+lmr_status_t lmr_exchange_flush(lmr_ctx_t* ctx, lmr_stream_t stream) {
+    if (!ctx) return LMR_E_INVALID;
+    if (!ctx->xdefer_open) return LMR_OK;
+    ctx->xdefer_open = false;
+    if (!stage_session_open(ctx)) return LMR_OK;
+    return lmr_stage_finish(ctx, stream);
 }
 
 }  // extern "C"

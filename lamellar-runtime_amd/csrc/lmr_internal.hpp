@@ -31,6 +31,8 @@ struct lmr_ctx {
     lmr::HostStage* host = nullptr;  // host-buffer ingestion staging (lmr_apply_mvmi_host), lazily made
     lmr::StageState* stage = nullptr;  // staged-apply session (lmr_stage_*), lazily made
     lmr::XState* xch = nullptr;        // multi-PE exchange state (lmr_batch_exchange), lazily made
+    bool xdefer_on = false;            // lmr_ctx_exchange_defer
+    bool xdefer_open = false;          // the open staged session was left by a deferred exchange
     lmr::WinState* win = nullptr;      // window partition of shards above one tiled window, lazily made
     lmr::WireBufs* wire = nullptr;     // staging of lmr_apply_msg (AM wire format), lazily made
     lmr::OrdBufs* ord = nullptr;       // sort buffers of the ordered apply (n > 1024), see ord_reserve
@@ -266,6 +268,9 @@ hipError_t wide_unpartition(const TiledWs& w, const StageSession& s, const uint8
 // region of `cap` records at d_indices / d_vals whose record count is *d_n (device), accounted as
 // `expect` records
 bool stage_session_free(const lmr_ctx* ctx);
+// a session is open / open for this descriptor (shard, element type, kind, op and operands)
+bool stage_session_open(const lmr_ctx* ctx);
+bool stage_session_of(const lmr_ctx* ctx, const lmr_apply_desc_t& d);
 lmr_status_t stage_soa_dev(lmr_ctx* ctx, const void* d_indices, uint32_t index_size, const void* d_vals,
                            const void* val, uint64_t cap, uint64_t expect, const int64_t* d_n, hipStream_t s);
 

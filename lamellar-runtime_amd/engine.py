@@ -213,7 +213,8 @@ def _distributed(arr, k, dt, op, i_scalar, idx, i_len, v_scalar, vals, v_len, re
     team = arr.team
     m = 0 if (i_len == 0 or v_len == 0) else max(i_len, v_len)
     expect = 0 if (i_scalar and v_len > 1) else m + m // 8 + (1 << 16)   # about what this PE sends
-    k.batch_exchange(team.transport(), arr.layout, arr.local_shard(), arr.num_elems_local(), arr.kind, dt, op,
+    # (the shard view without a flush: batch_exchange applies or continues a deferred session itself)
+    k.batch_exchange(team.transport(), arr.layout, arr._shard_view(), arr.num_elems_local(), arr.kind, dt, op,
                      None if i_scalar else idx, idx if i_scalar else 0, i_len,
                      None if v_scalar else vals, vals if v_scalar else 0, v_len,
                      results, ok, cmp_bits, eps_bits, expect=expect)

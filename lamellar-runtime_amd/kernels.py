@@ -72,6 +72,12 @@ class DeviceKernels:
         self._deferred = None
         # record tensors of the open lmr_stage_* session, held until it is partitioned
         self._staged_refs = []
+        # deferred exchange sessions (lmr_ctx_exchange_defer): a batch exchange of an op that
+        # returns nothing leaves this PE's owner session open for the next such batch; flush()
+        # applies it (LAMELLAR_EXCHANGE_DEFER=0: every exchange sweeps its own batch)
+        self._xdeferred = None
+        if os.environ.get("LAMELLAR_EXCHANGE_DEFER", "1") != "0":
+            check(self.lib.lmr_ctx_exchange_defer(self.ctx, 1), "lmr_ctx_exchange_defer")
 
     # ---------------------------------------------------------------- infra
     def stream(self):
@@ -166,6 +172,12 @@ class DeviceKernels:
 
     def flush(self):
         """Apply the deferred batches (one sweep) on this stream."""
+        self._flush_local()
+        if self._xdeferred is not None:
+            self._xdeferred = None
+            check(self.lib.lmr_exchange_flush(self.ctx, self.stream()), "lmr_exchange_flush")
+
+    def _flush_local(self):
         d = self._deferred
         if d is None:
             return
@@ -355,8 +367,13 @@ class DeviceKernels:
         """lmr_batch_exchange: one batched op over every PE (collective). gidx: i_len
         global indices (device) unless i_len == 1 (h_index); vals: v_len elements
         (device) unless v_len == 1 (h_val_bits). `expect`: records this PE will likely
-        receive; the workspace grows to hold them before the call."""
-        self.flush()
+        receive; the workspace grows to hold them before the call. An op that returns nothing
+        may leave its owner session open (deferred, applied by flush() or by the next exchange
+        of another op); the next exchange of the same op on the same shard adds to it."""
+        self._flush_local()
+        key = (shard.data_ptr(), int(shard_len), int(kind), int(dt.code), int(op), int(cmp_bits), int(eps_bits))
+        if self._xdeferred is not None and (self._xdeferred != key or results is not None or ok is not None):
+            self.flush()
         if expect:
             self._maybe_reserve(int(expect))
         d = self._desc(shard, shard_len, kind, dt, op, cmp_bits, eps_bits)
@@ -366,7 +383,12 @@ class DeviceKernels:
                                          ctypes.cast(byref(hv), c_void_p), int(v_len), _p(results), _p(ok),
                                          self.stream())
         transport.raise_pending()
+        if st != 0:
+            self._xdeferred = None                # a failed exchange drops the open session
         check(st, "lmr_batch_exchange")
+        # (the library keeps the session open only for a count-free owner session; flushing a
+        # session it closed itself is a no-op)
+        self._xdeferred = key if results is None and ok is None else None
 
     def apply_msg(self, msg: bytes, resolve, shard_of, max_entries=1 << 16):
         """lmr_apply_msg over one lamellae message (single AM or batched) in host memory.

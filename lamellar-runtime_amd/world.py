@@ -196,6 +196,9 @@ class LamellarTeam:
         return self._my_pe
 
     def barrier(self):
+        flush = getattr(self.kernels, "flush", None)
+        if flush is not None:
+            flush()                           # batches deferred on this PE are applied first
         if self._num_pes > 1:
             if dist.get_backend(self.group) == "nccl":
                 dist.barrier(group=self.group, device_ids=[self.device.index])

@@ -31,7 +31,7 @@ def test_ctypes_binding_covers_header(lam):
 
 def test_abi_version_and_status_strings(capi, lam):
     from lamellar_runtime_amd import _capi
-    assert capi.lmr_abi_version() == 7
+    assert capi.lmr_abi_version() == 8
     assert _capi.status_string(2) == "index out of bounds"
     assert _capi.status_string(3).startswith("integer division")
 

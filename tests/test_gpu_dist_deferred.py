@@ -1,0 +1,124 @@
+"""Deferred exchange sessions (lmr_ctx_exchange_defer, on by default): a batch exchange of an op
+that returns nothing leaves each PE's owner session open, so consecutive such batches on one
+array share one shard sweep; another op, a barrier, wait_all or any read of the array applies it.
+PEs share the GPU over gloo (host-buffer transport), or one rank drives the 1-rank RCCL
+communicator (LAMELLAR_FORCE_EXCHANGE=1). Four spawned add batches are applied in fewer sweeps
+than batches (the stage profile's tile sweeps), then a fetch_add batch (returning: applies the open
+session first, its olds checked against the serial replay's per-element bounds), xor batches
+deferred again and read by to_numpy; every state equals numpy's replay (wrapping u64). The same
+program with LAMELLAR_EXCHANGE_DEFER=0 (one sweep per batch) gives the same arrays.
+Reference: batches are asynchronous until wait_all / a barrier (src/array/operations.rs,
+src/lamellar_world.rs wait_all)."""
+import os
+import subprocess
+import sys
+import tempfile
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+pytestmark = pytest.mark.gpu
+
+PER_PE = (1 << 21) + 3                # u64 elements per PE: > 128 tiles, a count-free owner session
+
+WORKER = r'''
+import os, sys
+import numpy as np
+sys.path.insert(0, os.environ["LMR_ROOT"])
+from _lamellar_bootstrap import load_package
+lam = load_package()
+world = lam.LamellarWorldBuilder().build()
+me, ws = world.my_pe(), world.num_pes()
+n_len = int(os.environ["LMR_LEN"])
+rng = np.random.default_rng(4100 + me)
+arr = lam.AtomicArray(world.team(), n_len, lam.Distribution.Block, "u64")
+k = world.team().kernels
+k.reserve(1 << 23)                    # the owner sessions hold several batches
+out = {}
+adds = []
+k.profile(True)
+k.profile_read(reset=True)
+for j in range(4):
+    gi = rng.integers(0, n_len, 700000 - 1111 * me).astype(np.uint64)
+    gv = rng.integers(0, 2**63, gi.size, dtype=np.uint64)
+    adds.append((gi, gv))
+    arr.batch_add(gi, gv).spawn()
+world.wait_all()
+st = k.profile_read(reset=True)
+out["sweeps"] = np.array([st.get("tile_apply", (0, 0))[1]])
+out["after_add"] = arr.to_numpy()
+fi = rng.integers(0, n_len, 300000).astype(np.uint64)
+fv = rng.integers(1, 1000, fi.size, dtype=np.uint64)
+arr.batch_add(fi, fv).spawn()                    # deferred ...
+olds = arr.batch_fetch_add(fi, fv).block()       # ... applied before the fetch_add exchange
+out["olds"] = olds.cpu().numpy().view(np.uint64)
+xi = rng.integers(0, n_len, 500000).astype(np.uint64)
+xv = rng.integers(0, 2**63, xi.size, dtype=np.uint64)
+arr.batch_bit_xor(xi, xv).spawn()
+arr.batch_bit_xor(xi[::2].copy(), xv[::2].copy()).spawn()
+world.barrier()
+out["after_xor"] = arr.to_numpy()
+for j, (gi, gv) in enumerate(adds):
+    out[f"gi{j}"], out[f"gv{j}"] = gi, gv
+out["fi"], out["fv"], out["xi"], out["xv"] = fi, fv, xi, xv
+np.savez(os.path.join(os.environ["LMR_OUT"], f"pe{me}.npz"), **out)
+world.barrier()
+'''
+
+
+def _run(ws, env_extra, outdir):
+    env = dict(os.environ)
+    env.update(env_extra)
+    env.update(LMR_ROOT=ROOT, LMR_OUT=outdir, LMR_LEN=str(PER_PE * ws), LAMELLAR_EXCHANGE_CHUNK=str(1 << 18),
+               MASTER_ADDR="127.0.0.1", MASTER_PORT=str(29400 + 11 * ws + (os.getpid() % 50)))
+    procs = [subprocess.Popen([sys.executable, "-c", WORKER],
+                              env=dict(env, RANK=str(r), WORLD_SIZE=str(ws), LOCAL_RANK=str(r)))
+             for r in range(ws)]
+    try:
+        rcs = [p.wait(timeout=170) for p in procs]
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+    assert rcs == [0] * ws, rcs
+    return [dict(np.load(os.path.join(outdir, f"pe{r}.npz"))) for r in range(ws)]
+
+
+@pytest.mark.parametrize("ws,backend,defer", [(1, "nccl", "1"), (2, "gloo", "1"), (3, "gloo", "1"), (2, "gloo", "0")],
+                         ids=["rccl-1rank", "gloo-2pe", "gloo-3pe", "gloo-2pe-nodefer"])
+def test_deferred_exchange_sessions(ws, backend, defer):
+    env = {"LAMELLAR_COMM_BACKEND": backend, "LAMELLAR_EXCHANGE_DEFER": defer}
+    if ws == 1:
+        env["LAMELLAR_FORCE_EXCHANGE"] = "1"
+    with tempfile.TemporaryDirectory() as d:
+        pe = _run(ws, env, d)
+    n_len = PER_PE * ws
+    a = np.zeros(n_len, np.uint64)
+    for j in range(4):
+        for r in range(ws):
+            np.add.at(a, pe[r][f"gi{j}"].astype(np.int64), pe[r][f"gv{j}"])
+    for r in range(ws):
+        assert np.array_equal(pe[r]["after_add"], a), r
+    start = a.copy()
+    for r in range(ws):
+        np.add.at(a, pe[r]["fi"].astype(np.int64), pe[r]["fv"])        # the deferred add batches
+    mid = a.copy()
+    for r in range(ws):
+        np.add.at(a, pe[r]["fi"].astype(np.int64), pe[r]["fv"])        # the fetch_add batches
+    for r in range(ws):
+        i = pe[r]["fi"].astype(np.int64)
+        o = pe[r]["olds"]
+        # every fetch_add saw every deferred add applied and at most the other fetch_adds
+        assert np.all(o >= mid[i]) and np.all(o < a[i]), r
+    for r in range(ws):
+        np.bitwise_xor.at(a, pe[r]["xi"].astype(np.int64), pe[r]["xv"])
+        np.bitwise_xor.at(a, pe[r]["xi"][::2].astype(np.int64), pe[r]["xv"][::2])
+    for r in range(ws):
+        assert np.array_equal(pe[r]["after_xor"], a), r
+    sweeps = [int(pe[r]["sweeps"][0]) for r in range(ws)]
+    if defer == "1":
+        assert all(s < 4 for s in sweeps), sweeps          # four batches, fewer sweeps
+    else:
+        assert all(s == 4 for s in sweeps), sweeps
+    del start
