@@ -748,8 +748,8 @@ def e2e(lam, team, W, args):
 def e2e_wire(lam, team, W, args):
     """The reference's own op-buffer bytes in host memory: IdxVal<u32,u64> records
     (16 B, repr(C)), applied by lmr_apply_mvmi_host (pieces uploaded / applied /
-    results downloaded on three streams); fetch_add olds land in a registered
-    host array. At one PE a global index is the local offset."""
+    results downloaded on three streams); fetch_add olds land in a pinned host array.
+    At one PE a global index is the local offset."""
     from lamellar_runtime_amd import _capi
     from lamellar_runtime_amd.types import ArrayOpCmd
     k = team.kernels
@@ -757,13 +757,14 @@ def e2e_wire(lam, team, W, args):
     iw = 4
     rb, vo = _capi.lib().lmr_record_bytes(iw, dt.code), _capi.lib().lmr_record_val_offset(iw, dt.code)
     assert (rb, vo) == (16, 8)
-    rec = np.zeros(W.n, dtype=[("i", "<u4"), ("pad", "<u4"), ("v", "<u8")])
+    # the op buffer and the olds in the library's pinned host heap (lmr_host_alloc: DMA'd in
+    # place, as the reference's lamellae heap is mapped once for the world)
+    rdt = np.dtype([("i", "<u4"), ("pad", "<u4"), ("v", "<u8")])
+    buf = k.host_alloc(W.n * rdt.itemsize)
+    olds = k.host_alloc(W.n * 8, np.uint64)
+    rec = buf.view(rdt)
     rec["i"] = W.idx.cpu().numpy().astype(np.uint32)
     rec["v"] = W.vals.cpu().numpy().view(np.uint64)
-    buf = rec.view(np.uint8).reshape(-1)
-    olds = np.empty(W.n, dtype=np.uint64)
-    k.host_register(buf)
-    k.host_register(olds)
     try:
         shard, slen = W.arr.local_shard(), W.arr.num_elems_local()
         kind = int(W.arr.kind)
@@ -776,12 +777,13 @@ def e2e_wire(lam, team, W, args):
             k.apply_mvmi_host(shard, slen, kind, dt, int(ArrayOpCmd.FetchAdd), buf, iw, olds)
         t2 = time.perf_counter()
     finally:
-        k.host_unregister(buf)
-        k.host_unregister(olds)
+        del rec
+        k.host_free(buf)
+        k.host_free(olds)
     return {"batch_add_ops_per_s": W.n * args.steps / (t1 - t0),
             "batch_fetch_add_ops_per_s": W.n * args.steps / (t2 - t1),
             "h2d_GBps": W.n * rb * args.steps / (t1 - t0) / 1e9,
-            "note": "host IdxVal<u32,u64> op buffer (registered) -> lmr_apply_mvmi_host; olds -> host"}
+            "note": "host IdxVal<u32,u64> op buffer (lmr_host_alloc) -> lmr_apply_mvmi_host; olds -> host"}
 
 
 if __name__ == "__main__":

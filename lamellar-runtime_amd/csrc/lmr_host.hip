@@ -23,20 +23,19 @@
 // pageable memory land in a pinned slot and the host copies them out (the call then returns
 // once they are written).
 //
-// Registration contract (round 5). Device faults (rounds 3, 4 and once more in round 5) surfaced at
-// the first pageable host-to-device copy after host tests had registered two ranges whose pages
-// overlapped (slices of one numpy arena), unregistered both and freed the memory. Both earlier
-// registries pinned page-rounded ranges, so the shared page was locked twice (round 4) or locked,
-// unlocked and locked again inside a grown union (round 5's merged segments); single page-aligned
-// registrations that are unregistered, unmapped and mapped again at the same address copy cleanly
-// (tools/hostreg_probe2.cpp, profiles/r5/hostreg_probe2.txt, scenarios 4-5). The registry therefore
-// pins only the whole pages inside a caller's range ("inner pages": page_up(lo) .. page_down(hi)),
-// each with one hipHostRegister at a page-aligned address and one hipHostUnregister at the same
-// address: no page is ever locked by two registrations, locked twice, or locked beyond the caller's
-// own bytes. A copy DMAs the part of a buffer on those pages in place and stages the rest (under a
-// page at each end of a registered range, all of a pageable buffer) through the pinned bounce slots.
-// Overlapping caller ranges are refused (LMR_E_INVALID). Short-lived pinned buffers come from
-// lmr_host_alloc / lmr_host_free (hipHostMalloc: no user page pinning at all).
+// Registration contract (round 5). Device faults (rounds 3 and 4, and twice more in round 5)
+// surfaced as "illegal memory access" at a host<->device copy that followed tests which had
+// registered (hipHostRegister) host ranges, unregistered them and freed the memory: first with two
+// registrations sharing a page (round 4), then with a reference-counted page-aligned union
+// (round 5, r5n, in a serialised run: every kernel had completed), then with only the whole pages
+// inside each range pinned, one lock per range (r5t, at the next device-to-host copy). No library
+// kernel was running at any of them, and the runs that never unpinned user memory (round 3's
+// `_KEEP`) never faulted. The library therefore no longer page-locks caller memory at all:
+// lmr_host_register records a caller range (refusing overlaps, as before) and copies through it
+// are staged through the library's pinned bounce slots like any pageable buffer. Memory the HIP
+// runtime allocated pinned -- lmr_host_alloc / hipHostMalloc, torch's pinned allocator -- is DMA'd
+// in place: that is the reference's own contract, a lamellae heap mapped once at world init and
+// dropped at shutdown (shmem_comm.rs:47-80), and the zero-copy path for callers.
 #include "lmr_internal.hpp"
 #include "../../include/lamellar_gpu_ops.h"
 #include <stdlib.h>
@@ -51,16 +50,14 @@
 
 namespace lmr {
 
-static const uintptr_t kHostPage = 4096;
 
-// a caller range [lo, hi) and the whole pages inside it that are pinned, [plo, phi) (plo == phi:
-// a range within two pages, nothing pinned)
+// a recorded caller range [lo, hi)
 struct HostRange {
-    uintptr_t hi, plo, phi;
+    uintptr_t hi;
 };
 struct HostRegistry {
     std::mutex mu;                                   // registry maps and the stage list
-    std::shared_mutex pin;                           // shared: a call DMAs through a range; unique: unpin
+    std::shared_mutex pin;                           // shared: a call DMAs through pinned memory; unique: lmr_host_free
     std::map<uintptr_t, HostRange> ranges;
     std::set<HostStage*> stages;                     // every context's host stage (drained before an unpin)
     std::set<void*> allocs;                          // lmr_host_alloc blocks
@@ -84,26 +81,10 @@ static bool runtime_pinned(const void* p, uint64_t bytes) {
     if (hipPointerGetAttributes(&b, last) != hipSuccess) { (void)hipGetLastError(); return false; }
     return b.type == hipMemoryTypeHost && b.hostPointer == a.hostPointer;
 }
-// the part of [p, p + bytes) a DMA may touch in place, as offsets [*a, *b) (*a == *b: none): the
-// pinned inner pages of the registered range holding it, or all of it when the runtime allocated
-// it pinned
+// the part of [p, p + bytes) a DMA may touch in place, as offsets [*a, *b) (*a == *b: none): all
+// of it when the runtime allocated it pinned, nothing otherwise (caller memory is never locked)
 static void pinned_span(const void* p, uint64_t bytes, uint64_t* a, uint64_t* b) {
     *a = *b = 0;
-    if (!p || bytes == 0) return;
-    const uintptr_t lo = reinterpret_cast<uintptr_t>(p), hi = lo + bytes;
-    {
-        std::lock_guard<std::mutex> g(reg().mu);
-        auto& R = reg().ranges;
-        auto it = R.upper_bound(lo);
-        if (it != R.begin()) {
-            --it;
-            if (it->first <= lo && hi <= it->second.hi) {
-                const uintptr_t x = std::max(lo, it->second.plo), y = std::min(hi, it->second.phi);
-                if (x < y) { *a = x - lo; *b = y - lo; }
-                return;
-            }
-        }
-    }
     if (runtime_pinned(p, bytes)) *b = bytes;
 }
 
@@ -200,8 +181,6 @@ static hipError_t drain_host_stages_locked() {
     return r;
 }
 
-static uintptr_t page_down(uintptr_t x) { return x & ~(kHostPage - 1); }
-static uintptr_t page_up(uintptr_t x) { return (x + kHostPage - 1) & ~(kHostPage - 1); }
 
 }  // namespace lmr
 
@@ -214,36 +193,20 @@ lmr_status_t lmr_host_register(void* ptr, uint64_t bytes) {
     const uintptr_t lo = reinterpret_cast<uintptr_t>(ptr), hi = lo + bytes;
     if (hi < lo) return LMR_E_INVALID;
     HostRegistry& R = reg();
-    std::unique_lock<std::shared_mutex> pin(R.pin);
     std::lock_guard<std::mutex> g(R.mu);
     auto it = R.ranges.lower_bound(lo);                  // overlapping an earlier caller range: refused
     if (it != R.ranges.end() && it->first < hi) return LMR_E_INVALID;
     if (it != R.ranges.begin() && std::prev(it)->second.hi > lo) return LMR_E_INVALID;
-    // the whole pages inside the range: no other range's bytes share them
-    const uintptr_t plo = page_up(lo), phi = std::max(plo, page_down(hi));
-    if (phi > plo && hipHostRegister(reinterpret_cast<void*>(plo), phi - plo, hipHostRegisterDefault) != hipSuccess) {
-        (void)hipGetLastError();
-        return LMR_E_HIP;
-    }
-    R.ranges[lo] = HostRange{hi, plo, phi};
+    R.ranges[lo] = HostRange{hi};
     return LMR_OK;
 }
 
 lmr_status_t lmr_host_unregister(void* ptr) {
     if (!ptr) return LMR_E_INVALID;
     HostRegistry& R = reg();
-    std::unique_lock<std::shared_mutex> pin(R.pin);
     std::lock_guard<std::mutex> g(R.mu);
     auto it = R.ranges.find(reinterpret_cast<uintptr_t>(ptr));
     if (it == R.ranges.end()) return LMR_E_INVALID;      // not the start of a registration
-    if (it->second.phi > it->second.plo) {
-        // the library's copies through the pages are done before they are unpinned
-        if (drain_host_stages_locked() != hipSuccess) return LMR_E_HIP;
-        if (hipHostUnregister(reinterpret_cast<void*>(it->second.plo)) != hipSuccess) {
-            (void)hipGetLastError();
-            return LMR_E_HIP;                            // registry unchanged: still registered
-        }
-    }
     R.ranges.erase(it);
     return LMR_OK;
 }
@@ -258,8 +221,8 @@ lmr_status_t lmr_host_registered(const void* ptr, uint64_t bytes, uint64_t* pin_
     if (it == R.ranges.begin()) return LMR_E_INVALID;
     --it;
     if (!(it->first <= lo && hi <= it->second.hi)) return LMR_E_INVALID;
-    if (pin_base) *pin_base = it->second.plo;
-    if (pin_bytes) *pin_bytes = it->second.phi - it->second.plo;
+    if (pin_base) *pin_base = 0;                         // nothing of caller memory is page-locked
+    if (pin_bytes) *pin_bytes = 0;
     if (ranges) *ranges = 1;
     return LMR_OK;
 }
@@ -313,8 +276,8 @@ lmr_status_t lmr_apply_mvmi_host(lmr_ctx_t* ctx, const lmr_apply_desc_t* desc, c
         lmr_status_t st = lmr_ctx_reserve(ctx, P);
         if (st != LMR_OK) return st;
     }
-    // registrations stay pinned while this call enqueues copies through them (lmr_host_unregister
-    // takes the lock exclusively and drains the host-stage streams before it unpins)
+    // lmr_host_alloc blocks stay allocated while this call enqueues copies through them
+    // (lmr_host_free takes the lock exclusively and drains the host-stage streams first)
     std::shared_lock<std::shared_mutex> pin(reg().pin);
     const uint32_t ret = lmr_op_ret_kind(desc->op);
     const bool want_res = h_results && ret != LMR_RET_NONE;
@@ -323,9 +286,9 @@ lmr_status_t lmr_apply_mvmi_host(lmr_ctx_t* ctx, const lmr_apply_desc_t* desc, c
     const uint8_t* src = reinterpret_cast<const uint8_t*>(h_idx_vals);
     // the pinned bounce slots, made on the first copy that stages anything
     auto stage_ready = [&]() -> bool { return h->h_rec[0] || host_bounce_get(h) == hipSuccess; };
-    // host -> device: the bytes on pinned pages DMA'd in place, the rest (under a page at each end
-    // of a registered range, or all of a pageable buffer) copied by the host into slot b's bounce
-    // buffer first (once that slot's previous upload is done)
+    // host -> device: runtime-pinned memory DMA'd in place, anything else (pageable or registered
+    // caller memory) copied by the host into slot b's bounce buffer first (once that slot's
+    // previous upload is done)
     auto upload = [&](uint8_t* dev, const uint8_t* hp, uint64_t bytes, int b, uint64_t piece) -> lmr_status_t {
         uint64_t x, y;
         pinned_span(hp, bytes, &x, &y);

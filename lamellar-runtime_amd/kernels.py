@@ -280,15 +280,16 @@ class DeviceKernels:
         torch.cuda.current_stream(self.device).synchronize()
 
     def host_register(self, arr):
-        """Page-lock a host numpy buffer for DMA (lmr_host_register)."""
+        """Record a host numpy buffer as an op / result buffer (lmr_host_register); zero-copy
+        DMA needs host_alloc memory."""
         check(self.lib.lmr_host_register(arr.ctypes.data, int(arr.nbytes)), "lmr_host_register")
 
     def host_unregister(self, arr):
         check(self.lib.lmr_host_unregister(arr.ctypes.data), "lmr_host_unregister")
 
     def host_registered(self, arr):
-        """(first pinned page, pinned bytes, 1) of the registered range holding the buffer -- the
-        whole pages inside that range, DMA'd in place -- or None (lmr_host_registered)."""
+        """(0, 0, 1) when a registered range holds the buffer (the library locks no caller memory:
+        its copies are staged through the bounce slots), else None (lmr_host_registered)."""
         base, nb, refs = c_uint64(0), c_uint64(0), c_uint32(0)
         st = self.lib.lmr_host_registered(arr.ctypes.data, int(arr.nbytes), byref(base), byref(nb), byref(refs))
         return (base.value, nb.value, refs.value) if st == 0 else None
