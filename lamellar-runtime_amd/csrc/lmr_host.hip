@@ -60,7 +60,7 @@ struct HostRegistry {
     std::shared_mutex pin;                           // shared: a call DMAs through pinned memory; unique: lmr_host_free
     std::map<uintptr_t, HostRange> ranges;
     std::set<HostStage*> stages;                     // every context's host stage (drained before an unpin)
-    std::set<void*> allocs;                          // lmr_host_alloc blocks
+    std::map<uintptr_t, uint64_t> allocs;            // lmr_host_alloc blocks: base -> bytes
 };
 HostRegistry& reg() {
     static HostRegistry r;
@@ -70,16 +70,26 @@ HostRegistry& reg() {
 // whole range: DMA'd in place as well
 static bool runtime_pinned(const void* p, uint64_t bytes) {
     if (!p || bytes == 0) return false;
+    const uintptr_t lo = reinterpret_cast<uintptr_t>(p), hi = lo + bytes;
     {
         std::lock_guard<std::mutex> g(reg().mu);
-        if (reg().allocs.count(const_cast<void*>(p))) return true;
+        auto& A = reg().allocs;
+        auto it = A.upper_bound(lo);
+        if (it != A.begin() && std::prev(it)->first + std::prev(it)->second >= hi) return true;
     }
+    // other runtime allocations (torch's pinned allocator): both ends host memory of one
+    // allocation (hipPointerGetAttributes reports the queried address itself, not the base)
     hipPointerAttribute_t a{}, b{};
     if (hipPointerGetAttributes(&a, p) != hipSuccess) { (void)hipGetLastError(); return false; }
-    if (a.type != hipMemoryTypeHost || !a.hostPointer) return false;
+    if (a.type != hipMemoryTypeHost) return false;
     const void* last = static_cast<const uint8_t*>(p) + bytes - 1;
     if (hipPointerGetAttributes(&b, last) != hipSuccess) { (void)hipGetLastError(); return false; }
-    return b.type == hipMemoryTypeHost && b.hostPointer == a.hostPointer;
+    if (b.type != hipMemoryTypeHost) return false;
+    hipDeviceptr_t base = nullptr;
+    size_t size = 0;
+    if (hipMemGetAddressRange(&base, &size, const_cast<void*>(p)) != hipSuccess) { (void)hipGetLastError(); return false; }
+    const uintptr_t bl = reinterpret_cast<uintptr_t>(base);
+    return bl <= lo && hi <= bl + size;
 }
 // the part of [p, p + bytes) a DMA may touch in place, as offsets [*a, *b) (*a == *b: none): all
 // of it when the runtime allocated it pinned, nothing otherwise (caller memory is never locked)
@@ -233,7 +243,7 @@ lmr_status_t lmr_host_alloc(uint64_t bytes, void** out) {
     void* p = nullptr;
     if (hipHostMalloc(&p, bytes, hipHostMallocDefault) != hipSuccess) { (void)hipGetLastError(); return LMR_E_HIP; }
     std::lock_guard<std::mutex> g(reg().mu);
-    reg().allocs.insert(p);
+    reg().allocs[reinterpret_cast<uintptr_t>(p)] = bytes;
     *out = p;
     return LMR_OK;
 }
@@ -243,10 +253,10 @@ lmr_status_t lmr_host_free(void* ptr) {
     HostRegistry& R = reg();
     std::unique_lock<std::shared_mutex> pin(R.pin);
     std::lock_guard<std::mutex> g(R.mu);
-    if (!R.allocs.count(ptr)) return LMR_E_INVALID;
+    if (!R.allocs.count(reinterpret_cast<uintptr_t>(ptr))) return LMR_E_INVALID;
     if (drain_host_stages_locked() != hipSuccess) return LMR_E_HIP;
     if (hipHostFree(ptr) != hipSuccess) { (void)hipGetLastError(); return LMR_E_HIP; }
-    R.allocs.erase(ptr);
+    R.allocs.erase(reinterpret_cast<uintptr_t>(ptr));
     return LMR_OK;
 }
 
