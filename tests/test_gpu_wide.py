@@ -241,3 +241,80 @@ def test_wide_non_add_ops(world, lam, orc, op):
     else:
         st, bad = orc.check_linearizable(1, CODE["u64"], np.uint64, op, s0, final, idx, vals, rets)
     assert st == 0, bad
+
+
+def test_wide_mixed_session_returning_phases(world, lam, orc):
+    """A mixed session on a wide shard (u64, 2^20 - 3 elements: <= 128 two-level tiles, so even
+    the first, order-insensitive phase is a counted region): and, swap, xor, compare_exchange,
+    fetch_add and add phases staged into one session, partitioned one-level and applied in one
+    sweep, op phase by op phase in staging order per element (as test_gpu_stage_mixed does on a
+    two-level shard). Each returning phase's olds / Results are a valid linearisation from the
+    state the earlier phases left."""
+    from opgen import AND, XOR
+    k = world.team().kernels
+    dt = lam.dtype_of("u64")
+    n_el, n = (1 << 20) - 3, 1 << 18
+    rng = np.random.default_rng(2024)
+    hot = rng.choice(n_el, 30000, replace=False)
+
+    def idx():
+        u = rng.integers(0, n_el, n)
+        h = hot[rng.integers(0, hot.size, n)]
+        return np.where(rng.random(n) < 0.5, u, h).astype(np.uint64)
+
+    r64 = lambda hi: rng.integers(0, hi, n, dtype=np.uint64)
+    s0 = rng.integers(0, 8, n_el, dtype=np.uint64)
+    iA, vA = idx(), r64(2**63) | np.uint64(0xFFFFFFFFFFFFFFF0)
+    iS, vS = idx(), r64(8)
+    iX, vX = idx(), r64(8)
+    iC, vC = idx(), r64(8)
+    iF, vF = idx(), r64(1000)
+    iD, vD = idx(), r64(2**63)
+    cur = 3
+    k.reserve(8 * n)
+    shard = to_dev(s0)
+    rS, rC, okC, rF = (k.empty(n, torch.int64), k.empty(n, torch.int64), k.empty(n, torch.uint8),
+                       k.empty(n, torch.int64))
+    k.profile(True)
+    k.profile_read(reset=True)
+    try:
+        k.stage_begin(shard, n_el, 1, dt, AND)
+        k.stage_soa(to_dev(iA), 8, to_dev(vA), 0, n)
+        k.stage_op(SWAP)
+        k.stage_soa(to_dev(iS), 8, to_dev(vS), 0, n, rS)
+        k.stage_op(XOR)
+        k.stage_soa(to_dev(iX), 8, to_dev(vX), 0, n)
+        k.stage_op(CAS, cur)
+        k.stage_soa(to_dev(iC), 8, to_dev(vC), 0, n, rC, okC)
+        k.stage_op(FETCH_ADD)
+        k.stage_soa(to_dev(iF), 8, to_dev(vF), 0, n, rF)
+        k.stage_op(ADD)
+        k.stage_soa(to_dev(iD), 8, to_dev(vD), 0, n)
+        k.stage_finish()
+        stages = _stages(k)
+    finally:
+        k.profile(False)
+    assert k.errors() == 0
+    _assert_wide(stages)
+    final = shard.cpu().numpy().view(np.uint64)
+    u = lambda t: t.cpu().numpy().view(np.uint64)
+    ii = lambda a: a.astype(np.int64)
+    s1 = s0.copy()
+    np.bitwise_and.at(s1, ii(iA), vA)
+    s2 = s1.copy()                                    # swap: init + sum(vals) - sum(returned)
+    np.add.at(s2, ii(iS), vS)
+    np.subtract.at(s2, ii(iS), u(rS))
+    st, bad = orc.check_linearizable(1, CODE["u64"], np.uint64, SWAP, s1, s2, iS, vS, u(rS))
+    assert st == 0, ("swap", st, bad)
+    s3 = s2.copy()
+    np.bitwise_xor.at(s3, ii(iX), vX)
+    s5 = final.copy()
+    np.subtract.at(s5, ii(iD), vD)                    # undo the last add phase
+    s4 = s5.copy()
+    np.subtract.at(s4, ii(iF), vF)                    # the fetch_add phase's start state
+    st, bad = orc.check_linearizable(1, CODE["u64"], np.uint64, FETCH_ADD, s4, s5, iF, vF, u(rF))
+    assert st == 0, ("fetch_add", st, bad)
+    st, bad = orc.check_linearizable(1, CODE["u64"], np.uint64, CAS, s3, s4, iC, vC, u(rC), okC.cpu().numpy(),
+                                     current=np.uint64(cur))
+    assert st == 0, ("compare_exchange", st, bad)
+    assert okC.cpu().numpy().any() and (~okC.cpu().numpy().astype(bool)).any()
