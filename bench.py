@@ -63,11 +63,14 @@ def parse():
     p.add_argument("--input-sets", type=int, default=0,
                    help="distinct input buffers rotated over the steps (0: one per step of a deferred "
                         "session, up to 8)")
-    p.add_argument("--reserve-log2", type=int, default=29,
+    p.add_argument("--reserve-log2", type=int, default=30,
                    help="tiled-apply workspace (records, log2; 0: the step's records). The engine defers "
                         "large 1-PE batches into one staged session until the workspace is full, so a "
-                        "2^29-record workspace (24 GB of HBM) sweeps the shard once per two C2 / eight C3 "
-                        "batches")
+                        "2^30-record workspace (49 GB of the 288 GB of HBM) sweeps the shard once per four "
+                        "C2 / sixteen C3 batches (2^29: two / eight; the C2 step then ran 3.16 or 3.37 ms "
+                        "from box to box, 2^30 3.165-3.167, profiles/r5/ab_reserve/)")
+    p.add_argument("--reserve-records", type=int, default=0,
+                   help="tiled-apply workspace in records (overrides --reserve-log2 when set)")
     p.add_argument("--inputs", default="owned", choices=["owned", "borrowed"],
                    help="owned: each batch's input tensors are handed over with Owned(...) (the "
                         "reference's by-value Vec input; the bench never changes them), so consecutive "
@@ -508,7 +511,12 @@ def main():
     cfg = args.config or ("c2" if npes == 1 else "c4")
     W = {"c2": AddUniform, "c4": AddUniform, "c3": FetchAddZipf, "c5": MixedU32}[cfg](lam, team, args)
     W.setup()
-    ws_records = max(W.n, 1 << args.reserve_log2) if args.reserve_log2 else W.n
+    ws_records = W.n
+    if args.reserve_records:
+        ws_records = max(W.n, args.reserve_records)
+    elif args.reserve_log2:
+        ws_records = max(W.n, 1 << args.reserve_log2)
+    k.max_ws_records = max(k.max_ws_records, ws_records)     # (the library caps it at lmr's max_rec_cap)
     k.reserve(ws_records)
     W.make_sets(input_sets(args, k.reserved, W.ops_per_step))
     world.barrier()
@@ -652,10 +660,10 @@ def main():
 
 
 def input_sets(args, ws_records, ops_per_step):
-    """Distinct input sets: one per step a deferred session can hold (up to 8), or --input-sets."""
+    """Distinct input sets: one per step a deferred session can hold (up to 16), or --input-sets."""
     if args.input_sets:
         return args.input_sets
-    return int(max(1, min(8, ws_records // max(1, ops_per_step))))
+    return int(max(1, min(16, ws_records // max(1, ops_per_step))))
 
 
 def other_configs(lam, world, team, args):
