@@ -137,6 +137,8 @@ SIGNATURES = {
                          c_uint32, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     "lmr_host_register": (c_int, [c_void_p, c_uint64]),
     "lmr_host_unregister": (c_int, [c_void_p]),
+    "lmr_host_register_heap": (c_int, [c_void_p, c_uint64]),
+    "lmr_host_unregister_heap": (c_int, [c_void_p]),
     "lmr_host_registered": (c_int, [c_void_p, c_uint64, POINTER(c_uint64), POINTER(c_uint64), POINTER(c_uint32)]),
     "lmr_host_alloc": (c_int, [c_uint64, POINTER(c_void_p)]),
     "lmr_host_free": (c_int, [c_void_p]),

@@ -55,10 +55,15 @@ namespace lmr {
 struct HostRange {
     uintptr_t hi;
 };
+// a heap [lo, hi) whose whole inner pages [plo, phi) are pinned from registration to shutdown
+struct HostHeap {
+    uintptr_t hi, plo, phi;
+};
 struct HostRegistry {
     std::mutex mu;                                   // registry maps and the stage list
     std::shared_mutex pin;                           // shared: a call DMAs through pinned memory; unique: lmr_host_free
     std::map<uintptr_t, HostRange> ranges;
+    std::map<uintptr_t, HostHeap> heaps;             // lmr_host_register_heap: pinned for their lifetime
     std::set<HostStage*> stages;                     // every context's host stage (drained before an unpin)
     std::map<uintptr_t, uint64_t> allocs;            // lmr_host_alloc blocks: base -> bytes
 };
@@ -95,7 +100,34 @@ static bool runtime_pinned(const void* p, uint64_t bytes) {
 // of it when the runtime allocated it pinned, nothing otherwise (caller memory is never locked)
 static void pinned_span(const void* p, uint64_t bytes, uint64_t* a, uint64_t* b) {
     *a = *b = 0;
+    if (!p || bytes == 0) return;
+    const uintptr_t lo = reinterpret_cast<uintptr_t>(p), hi = lo + bytes;
+    {   // inside a registered heap: its pinned inner pages in place, the partial end pages staged
+        std::lock_guard<std::mutex> g(reg().mu);
+        auto& H = reg().heaps;
+        auto it = H.upper_bound(lo);
+        if (it != H.begin()) {
+            --it;
+            if (it->first <= lo && hi <= it->second.hi) {
+                const uintptr_t x = std::max(lo, it->second.plo), y = std::min(hi, it->second.phi);
+                if (x < y) { *a = x - lo; *b = y - lo; }
+                return;
+            }
+        }
+    }
     if (runtime_pinned(p, bytes)) *b = bytes;
+}
+
+// [lo, hi) overlaps a recorded range or heap (caller holds reg().mu)
+static bool overlaps_locked(uintptr_t lo, uintptr_t hi) {
+    auto& R = reg().ranges;
+    auto it = R.lower_bound(lo);
+    if (it != R.end() && it->first < hi) return true;
+    if (it != R.begin() && std::prev(it)->second.hi > lo) return true;
+    auto& H = reg().heaps;
+    auto ht = H.lower_bound(lo);
+    if (ht != H.end() && ht->first < hi) return true;
+    return ht != H.begin() && std::prev(ht)->second.hi > lo;
 }
 
 struct HostStage {
@@ -204,10 +236,44 @@ lmr_status_t lmr_host_register(void* ptr, uint64_t bytes) {
     if (hi < lo) return LMR_E_INVALID;
     HostRegistry& R = reg();
     std::lock_guard<std::mutex> g(R.mu);
-    auto it = R.ranges.lower_bound(lo);                  // overlapping an earlier caller range: refused
-    if (it != R.ranges.end() && it->first < hi) return LMR_E_INVALID;
-    if (it != R.ranges.begin() && std::prev(it)->second.hi > lo) return LMR_E_INVALID;
+    if (overlaps_locked(lo, hi)) return LMR_E_INVALID;   // overlapping an earlier range or heap: refused
     R.ranges[lo] = HostRange{hi};
+    return LMR_OK;
+}
+
+lmr_status_t lmr_host_register_heap(void* ptr, uint64_t bytes) {
+    if (!ptr || bytes == 0) return LMR_E_INVALID;
+    const uintptr_t lo = reinterpret_cast<uintptr_t>(ptr), hi = lo + bytes;
+    if (hi < lo) return LMR_E_INVALID;
+    HostRegistry& R = reg();
+    std::unique_lock<std::shared_mutex> pin(R.pin);
+    std::lock_guard<std::mutex> g(R.mu);
+    if (overlaps_locked(lo, hi)) return LMR_E_INVALID;
+    const uintptr_t page = 4096;
+    const uintptr_t plo = (lo + page - 1) & ~(page - 1), phi = std::max(plo, hi & ~(page - 1));
+    if (phi > plo && hipHostRegister(reinterpret_cast<void*>(plo), phi - plo, hipHostRegisterDefault) != hipSuccess) {
+        (void)hipGetLastError();
+        return LMR_E_HIP;
+    }
+    R.heaps[lo] = HostHeap{hi, plo, phi};
+    return LMR_OK;
+}
+
+lmr_status_t lmr_host_unregister_heap(void* ptr) {
+    if (!ptr) return LMR_E_INVALID;
+    HostRegistry& R = reg();
+    std::unique_lock<std::shared_mutex> pin(R.pin);
+    std::lock_guard<std::mutex> g(R.mu);
+    auto it = R.heaps.find(reinterpret_cast<uintptr_t>(ptr));
+    if (it == R.heaps.end()) return LMR_E_INVALID;
+    if (it->second.phi > it->second.plo) {
+        if (drain_host_stages_locked() != hipSuccess) return LMR_E_HIP;
+        if (hipHostUnregister(reinterpret_cast<void*>(it->second.plo)) != hipSuccess) {
+            (void)hipGetLastError();
+            return LMR_E_HIP;
+        }
+    }
+    R.heaps.erase(it);
     return LMR_OK;
 }
 
@@ -227,11 +293,19 @@ lmr_status_t lmr_host_registered(const void* ptr, uint64_t bytes, uint64_t* pin_
     const uintptr_t lo = reinterpret_cast<uintptr_t>(ptr), hi = lo + bytes;
     HostRegistry& R = reg();
     std::lock_guard<std::mutex> g(R.mu);
+    auto ht = R.heaps.upper_bound(lo);
+    if (ht != R.heaps.begin() && std::prev(ht)->first <= lo && hi <= std::prev(ht)->second.hi) {
+        --ht;
+        if (pin_base) *pin_base = ht->second.plo;
+        if (pin_bytes) *pin_bytes = ht->second.phi - ht->second.plo;
+        if (ranges) *ranges = 1;
+        return LMR_OK;
+    }
     auto it = R.ranges.upper_bound(lo);
     if (it == R.ranges.begin()) return LMR_E_INVALID;
     --it;
     if (!(it->first <= lo && hi <= it->second.hi)) return LMR_E_INVALID;
-    if (pin_base) *pin_base = 0;                         // nothing of caller memory is page-locked
+    if (pin_base) *pin_base = 0;                         // a recorded range: nothing is page-locked
     if (pin_bytes) *pin_bytes = 0;
     if (ranges) *ranges = 1;
     return LMR_OK;

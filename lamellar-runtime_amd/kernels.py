@@ -284,6 +284,14 @@ class DeviceKernels:
         DMA needs host_alloc memory."""
         check(self.lib.lmr_host_register(arr.ctypes.data, int(arr.nbytes)), "lmr_host_register")
 
+    def host_register_heap(self, arr):
+        """Page-lock a host heap for its lifetime (lmr_host_register_heap): buffers inside it DMA in
+        place. Unregister only at shutdown."""
+        check(self.lib.lmr_host_register_heap(arr.ctypes.data, int(arr.nbytes)), "lmr_host_register_heap")
+
+    def host_unregister_heap(self, arr):
+        check(self.lib.lmr_host_unregister_heap(arr.ctypes.data), "lmr_host_unregister_heap")
+
     def host_unregister(self, arr):
         check(self.lib.lmr_host_unregister(arr.ctypes.data), "lmr_host_unregister")
 

@@ -162,3 +162,64 @@ def test_host_alloc_buffers_dma_in_place(world, orc, lam):
         finally:
             k.host_free(buf)
             k.host_free(h_res)
+
+
+_HEAP = []
+
+
+def _heap(k, nbytes=64 << 20):
+    """One page-aligned host heap for the whole test process, registered once and never
+    unregistered (the reference's lamellae heap lives from world init to shutdown)."""
+    if not _HEAP:
+        import mmap
+        m = mmap.mmap(-1, nbytes)
+        a = np.frombuffer(m, dtype=np.uint8)
+        k.host_register_heap(a)
+        _HEAP.extend([m, a])
+    return _HEAP[1]
+
+
+def test_heap_buffers_dma_in_place(world, orc, lam):
+    """A lamellae-style heap registered once (lmr_host_register_heap: its whole inner pages
+    page-locked for its lifetime): op buffers and fetch results placed at unaligned offsets inside
+    it DMA their pinned pages in place and stage the partial end pages; results bit-exact against
+    the oracle; a caller range inside the heap is refused (ranges never overlap)."""
+    from lamellar_runtime_amd.kernels import LamellarError
+    k = world.team().kernels
+    heap = _heap(k)
+    base = heap.ctypes.data
+    info = k.host_registered(heap[100:200])
+    assert info is not None and info[0] == base and info[1] == heap.nbytes and info[2] == 1
+    with pytest.raises(LamellarError):
+        k.host_register(heap[4096:8192])
+    for dt, op in (("u64", FETCH_ADD), ("u32", CAS), ("f64", FETCH_ADD)):
+        rng = np.random.default_rng(77 + CODE[dt])
+        shard_len, n = 300000, 3 * 65536 + 1234
+        shard0 = rand_elems(dt, shard_len, rng, op)
+        idx = rng.permutation(shard_len)[:n].astype(np.uint64)
+        vals = rand_vals(dt, n, rng, op)
+        cur = eps = None
+        if op == CAS:
+            cur, eps, shard0 = cas_operands(dt, shard0, vals, rng)
+        iw = 4
+        rb, vo = orc.record_bytes(iw, CODE[dt]), orc.record_val_offset(iw, CODE[dt])
+        recs = to_aos(idx, vals, iw, dt, rb, vo)
+        buf = heap[1000:1000 + recs.nbytes]
+        buf[:] = recs
+        eb = np.dtype(NP[dt]).itemsize
+        r0 = (1000 + recs.nbytes + 4095) // 4096 * 4096 + 24      # results start 24 B into a page
+        h_res = heap[r0:r0 + n * eb].view(NP[dt])
+        h_ok = heap[r0 + n * eb + 8:r0 + n * eb + 8 + n] if op == CAS else None
+        ref = shard0.copy()
+        kind = 2 if dt.startswith("f") else 1
+        st_o, res_o, ok_o = orc.apply_mvmi(ref, kind, CODE[dt], NP[dt], op, recs, iw, cur, eps)
+        assert st_o == 0
+        d_shard = to_dev(shard0)
+        dto = lam.dtype_of(dt)
+        k.apply_mvmi_host(d_shard, shard_len, kind, dto, op, buf, iw, h_res, h_ok,
+                          dto.to_bits(cur) if cur is not None else 0, 0)
+        assert k.errors() == 0
+        assert bits_equal(d_shard.cpu().numpy().view(NP[dt])[:shard_len], ref)
+        assert bits_equal(h_res.copy(), res_o)
+        if op == CAS:
+            assert np.array_equal(h_ok, ok_o)
