@@ -244,7 +244,7 @@ __device__ __forceinline__ void wruns_to_lds(const uint32_t* cursor, const uint3
             }
             // (an empty run starts where the next one does, so the last run starting at or
             // before p is never an empty one)
-            sp[u] =cursor[lo_x] + (p - base[lo_x]);
+            sp[u] = cursor[lo_x] + (p - base[lo_x]);
         }
         uint64_t v[U];
         uint8_t o[U];
