@@ -458,7 +458,9 @@ hipError_t launch_pack(const PackArgs& a, uint32_t* counts, uint32_t* partials, 
 }
 
 #ifndef LMR_PACK_FREE_LDS
-#define LMR_PACK_FREE_LDS 72   // KB of LDS per round buffer: 72 fits 2 blocks per CU (variant builds: -D...)
+#define LMR_PACK_FREE_LDS 100  // KB of LDS per round buffer: 8K-record rounds of 12-B records, one block per CU
+                               // (72: 4K rounds, 2 blocks per CU; alone 0.511 -> 0.460 ms per 2^26 records at 8
+                               // PEs, the one-rank rehearsal unchanged, profiles/r5/pack/ab_round.log)
 #endif
 
 // Count-free unordered pack (nothing returned): destination i's records land in
