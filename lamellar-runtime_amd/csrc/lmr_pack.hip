@@ -244,7 +244,7 @@ __device__ __forceinline__ void stage_scan(const uint32_t* hist, uint32_t* base,
 // each round reserves its run per destination with one atomicAdd on fill[i]. A round that
 // would overflow a region writes nothing (fill[i] still counts every record, so the caller
 // sees a count above cap and packs the chunk again with the counted pack).
-template <int IW, int VB, int RPT, int MODE, bool FREE>
+template <int IW, int VB, int RPT, int MODE, bool FREE, bool PAIRS = false>
 __global__ __launch_bounds__(1024) void k_pack_stage(PackK p) {
     using I = typename idx_t<IW>::I;
     using V = typename idx_t<VB>::I;
@@ -266,13 +266,39 @@ __global__ __launch_bounds__(1024) void k_pack_stage(PackK p) {
     const V* vals = reinterpret_cast<const V*>(p.vals);
     uint64_t m_g[RPT];
     V m_v[RPT];
+    bool m_in[RPT];
     auto load_round = [&](uint64_t r0) {
+        if constexpr (PAIRS) {
+            // two consecutive records per thread: one 16-B load of their global indices and one
+            // of their values (the round's order inside a destination is free: nothing returned)
 #pragma unroll
-        for (int j = 0; j < RPT; j++) {
-            const uint64_t k = r0 + uint64_t(j) * 1024 + threadIdx.x;
-            const bool in = k < hi;
-            m_g[j] = in ? p.gidx[k] : ~uint64_t(0);
-            m_v[j] = (in && vals) ? vals[k] : V(0);
+            for (int j = 0; j < RPT; j += 2) {
+                const uint64_t k = r0 + uint64_t(j) * 1024 + 2 * uint64_t(threadIdx.x);
+                if (k + 1 < hi) {
+                    const uint4 gq = *reinterpret_cast<const uint4*>(p.gidx + k);
+                    const uint4 vq = *reinterpret_cast<const uint4*>(vals + k);
+                    m_g[j] = uint64_t(gq.x) | (uint64_t(gq.y) << 32);
+                    m_g[j + 1] = uint64_t(gq.z) | (uint64_t(gq.w) << 32);
+                    m_v[j] = V(uint64_t(vq.x) | (uint64_t(vq.y) << 32));
+                    m_v[j + 1] = V(uint64_t(vq.z) | (uint64_t(vq.w) << 32));
+                    m_in[j] = m_in[j + 1] = true;
+                } else {
+                    m_in[j] = k < hi;
+                    m_in[j + 1] = false;
+                    m_g[j] = m_in[j] ? p.gidx[k] : ~uint64_t(0);
+                    m_v[j] = m_in[j] ? vals[k] : V(0);
+                    m_g[j + 1] = ~uint64_t(0);
+                    m_v[j + 1] = V(0);
+                }
+            }
+        } else {
+#pragma unroll
+            for (int j = 0; j < RPT; j++) {
+                const uint64_t k = r0 + uint64_t(j) * 1024 + threadIdx.x;
+                m_in[j] = k < hi;
+                m_g[j] = m_in[j] ? p.gidx[k] : ~uint64_t(0);
+                m_v[j] = (m_in[j] && vals) ? vals[k] : V(0);
+            }
         }
     };
     load_round(lo);
@@ -285,7 +311,7 @@ __global__ __launch_bounds__(1024) void k_pack_stage(PackK p) {
 #pragma unroll
         for (int j = 0; j < RPT; j++) {
             uint64_t pe = 0, off = 0;
-            const bool ok = (r0 + uint64_t(j) * 1024 + threadIdx.x < hi) && pe_and_offset_mode<MODE>(p.F, m_g[j], pe, off);
+            const bool ok = m_in[j] && pe_and_offset_mode<MODE>(p.F, m_g[j], pe, off);
             m_pe[j] = ok ? uint32_t(pe) : 0xFFFFFFFFu;
             m_off[j] = off;
             m_rank[j] = wave_match_rank(hist, ok ? uint32_t(pe) : 0u, ok, bits);
@@ -480,6 +506,12 @@ hipError_t launch_pack_free(const PackArgs& a, uint32_t* fill, uint32_t cap, hip
     p.fill = fill; p.cap = cap;
     p.ovf_gidx = a.ovf_gidx; p.ovf_vals = a.ovf_vals; p.ovf_count = a.ovf_count; p.ovf_cap = a.ovf_cap;
     p.out_idx_tab = a.out_idx_tab; p.out_vals_tab = a.out_vals_tab;
+    // paired 16-B loads: 8-byte values, 16-B aligned index and value arrays, even block ranges
+    // (LMR_PACK_PAIRS=0: one record per load)
+    static const bool pairs_on = [] { const char* v = getenv("LMR_PACK_PAIRS"); return !(v && v[0] == '0'); }();
+    if (pairs_on && (p.chunk & 1)) p.chunk += 1;
+    const bool pairs = pairs_on && a.vals && a.val_bytes == 8 &&
+                       ((reinterpret_cast<uintptr_t>(a.gidx) | reinterpret_cast<uintptr_t>(a.vals)) & 15) == 0;
     ProfScope ps(a.prof, LMR_STAGE_PACK, s, a.n);
     hipError_t e = hipMemsetAsync(fill, 0, size_t(npes) * 4, s);
     if (e != hipSuccess) return e;
@@ -489,7 +521,12 @@ hipError_t launch_pack_free(const PackArgs& a, uint32_t* fill, uint32_t cap, hip
         dispatch_pack_stage(int(a.index_size), vbk, [&](auto iw, auto vb) {
             constexpr int IWc = decltype(iw)::value, VBc = decltype(vb)::value;
             constexpr int RP = (IWc + VBc) * 8 <= LMR_PACK_FREE_LDS ? 8 : 4;   // rounds of RP * 1024 records
-            if (mode == LMR_MAP_BLOCK)
+            constexpr bool kP = VBc == 8;
+            if (kP && pairs && mode == LMR_MAP_BLOCK)
+                hipLaunchKernelGGL((k_pack_stage<IWc, VBc, RP, LMR_MAP_BLOCK, true, kP>), dim3(unsigned(G)), dim3(1024), 0, s, p);
+            else if (kP && pairs && mode == LMR_MAP_CYCLIC)
+                hipLaunchKernelGGL((k_pack_stage<IWc, VBc, RP, LMR_MAP_CYCLIC, true, kP>), dim3(unsigned(G)), dim3(1024), 0, s, p);
+            else if (mode == LMR_MAP_BLOCK)
                 hipLaunchKernelGGL((k_pack_stage<IWc, VBc, RP, LMR_MAP_BLOCK, true>), dim3(unsigned(G)), dim3(1024), 0, s, p);
             else if (mode == LMR_MAP_CYCLIC)
                 hipLaunchKernelGGL((k_pack_stage<IWc, VBc, RP, LMR_MAP_CYCLIC, true>), dim3(unsigned(G)), dim3(1024), 0, s, p);
