@@ -76,6 +76,8 @@ class DeviceKernels:
         # returns nothing leaves this PE's owner session open for the next such batch; flush()
         # applies it (LAMELLAR_EXCHANGE_DEFER=0: every exchange sweeps its own batch)
         self._xdeferred = None
+        # a deferred session's owned batches are partitioned every this many batches (0: at the flush)
+        self._partition_every = int(os.environ.get("LAMELLAR_DEFER_PARTITION_EVERY", "0"))
         if os.environ.get("LAMELLAR_EXCHANGE_DEFER", "1") != "0":
             check(self.lib.lmr_ctx_exchange_defer(self.ctx, 1), "lmr_ctx_exchange_defer")
 
@@ -167,7 +169,9 @@ class DeviceKernels:
             self._deferred = None
             self.lib.lmr_stage_finish(self.ctx, self.stream())
             check(st, "lmr_stage_soa")
-        if borrowed:
+        if borrowed or (self._partition_every and len(self._deferred[2]) % self._partition_every == 0):
+            # borrowed inputs are partitioned now; owned ones every few batches, so the device
+            # starts on a long session while the host stages its later batches
             check(self.lib.lmr_stage_flush(self.ctx, self.stream()), "lmr_stage_flush")
 
     def flush(self):
