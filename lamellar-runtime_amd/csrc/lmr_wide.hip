@@ -328,10 +328,10 @@ bool wide_applies(int dtype, uint64_t shard_len, uint64_t cap) {
     if (!wide_env() || dtype_bytes(dtype) != 8) return false;
     const uint64_t tiles = (shard_len + (uint64_t(1) << kWideShift8) - 1) >> kWideShift8;
     // the per-round tile counts live in the position map rpos (4 B per slot, unused by this path).
-    // A region of n records has G <= ceil(n / 64K) blocks of whole rounds: <= 1.125 n / 8K + 1
-    // rounds, so a session's counts fit when (1.125 cap / 8K + kMaxRegions) rounds of `tiles` u16
-    // do
-    const uint64_t rh_entries = (cap / kWideRound + cap / (8 * kWideRound) + kMaxRegions) * tiles;
+    // A region of n records has G <= ceil(n / 64K) blocks of whole rounds: <= n / R + n / 64K + 1
+    // rounds of R records, so a session's counts fit when (cap / R + cap / 64K + kMaxRegions)
+    // rounds of `tiles` u16 do
+    const uint64_t rh_entries = (cap / kWideRound + cap / 65536 + kMaxRegions) * tiles;
     return tiles >= 1 && tiles <= kWideMaxTiles && rh_entries <= cap * 2;
 }
 
