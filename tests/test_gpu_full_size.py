@@ -6,6 +6,9 @@ minutes of CPU time). Every check runs on the device with torch as the counter:
 - C2 (configs[1]): two deferred 2^28-record u64 batch_add batches from distinct buffers into a
   2^26-element shard — one shard sweep — against torch's index_add_ (wrapping int64 adds: exact in
   any order), bit for bit.
+- C4's exchange path (configs[3] at one rank): the same two batches forced through
+  lmr_batch_exchange over a 1-rank RCCL communicator (pack, all-to-all-v, the owner's deferred
+  count-free session), the same bit-exact check.
 - C3 (configs[2]): two 2^26-record f64 batch_fetch_add batches of 1.0 on Zipf(0.99) indices over
   2^24 elements (the wide one-level path), from an integer-valued start: per element, the olds of
   both batches are exactly start, start + 1, ..., start + c - 1 (every fetch saw a distinct
@@ -37,7 +40,7 @@ def _gen(seed):
     return g
 
 
-def c2_full_size_two_batch_session(world, lam):
+def c2_full_size_two_batch_session(world, lam, exchange=False):
     team = world.team()
     k = team.kernels
     n_el, n = 1 << 26, 1 << 28
@@ -61,6 +64,8 @@ def c2_full_size_two_batch_session(world, lam):
         k.profile(False)
     assert k.errors() == 0
     assert stages["tile_apply"][1] == 1, stages           # both batches in one shard sweep
+    if exchange:                                          # packed, sent and staged by the owner
+        assert stages.get("pack", (0, 0))[1] >= 2, stages
     ref = s0.clone()
     for i, v in batches:
         ref.index_add_(0, i, v)
@@ -160,6 +165,7 @@ def c5_full_size_bitwise_and_swap(world, lam):
 
 
 CHECKS = {"c2": c2_full_size_two_batch_session, "c3": c3_full_size_fetch_add_linearisable,
+          "c4": lambda w, lam_: c2_full_size_two_batch_session(w, lam_, exchange=True),
           "c5": c5_full_size_bitwise_and_swap}
 
 
@@ -167,6 +173,9 @@ CHECKS = {"c2": c2_full_size_two_batch_session, "c3": c3_full_size_fetch_add_lin
 @pytest.mark.parametrize("cfg", sorted(CHECKS))
 def test_full_size(cfg):
     env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK")}
+    if cfg == "c4":      # C2's batches through lmr_batch_exchange over a 1-rank RCCL communicator
+        env.update(LAMELLAR_COMM_BACKEND="nccl", LAMELLAR_FORCE_EXCHANGE="1", RANK="0", WORLD_SIZE="1",
+                   LOCAL_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(29600 + os.getpid() % 200))
     p = subprocess.run([sys.executable, os.path.abspath(__file__), cfg], env=env, timeout=170,
                        stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
     assert p.returncode == 0, p.stdout[-4000:]
