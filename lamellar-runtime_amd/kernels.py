@@ -178,8 +178,10 @@ class DeviceKernels:
         """Apply the deferred batches (one sweep) on this stream."""
         self._flush_local()
         if self._xdeferred is not None:
+            held = self._xdeferred
             self._xdeferred = None
             check(self.lib.lmr_exchange_flush(self.ctx, self.stream()), "lmr_exchange_flush")
+            del held                          # released once the sweep is enqueued (stream-ordered reuse)
 
     def _flush_local(self):
         d = self._deferred
@@ -385,7 +387,7 @@ class DeviceKernels:
         of another op); the next exchange of the same op on the same shard adds to it."""
         self._flush_local()
         key = (shard.data_ptr(), int(shard_len), int(kind), int(dt.code), int(op), int(cmp_bits), int(eps_bits))
-        if self._xdeferred is not None and (self._xdeferred != key or results is not None or ok is not None):
+        if self._xdeferred is not None and (self._xdeferred[0] != key or results is not None or ok is not None):
             self.flush()
         if expect:
             self._maybe_reserve(int(expect))
@@ -401,7 +403,9 @@ class DeviceKernels:
         check(st, "lmr_batch_exchange")
         # (the library keeps the session open only for a count-free owner session; flushing a
         # session it closed itself is a no-op)
-        self._xdeferred = key if results is None and ok is None else None
+        # the open session holds the shard: an array dropped before the flush keeps its memory until
+        # the sweep has run, so no new array can take its address (and its key) meanwhile
+        self._xdeferred = (key, shard) if results is None and ok is None else None
 
     def apply_msg(self, msg: bytes, resolve, shard_of, max_entries=1 << 16):
         """lmr_apply_msg over one lamellae message (single AM or batched) in host memory.

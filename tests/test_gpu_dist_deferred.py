@@ -122,3 +122,44 @@ def test_deferred_exchange_sessions(ws, backend, defer):
     else:
         assert all(s == 4 for s in sweeps), sweeps
     del start
+
+
+DROP_WORKER = r'''
+import os, sys
+import numpy as np
+import torch
+sys.path.insert(0, os.environ["LMR_ROOT"])
+from _lamellar_bootstrap import load_package
+lam = load_package()
+world = lam.LamellarWorldBuilder().build()
+n_len = int(os.environ["LMR_LEN"])
+rng = np.random.default_rng(77)
+k = world.team().kernels
+k.reserve(1 << 22)
+a = lam.AtomicArray(world.team(), n_len, lam.Distribution.Block, "u64")
+ai = rng.integers(0, n_len, 600000).astype(np.uint64)
+a.batch_add(ai, np.full(ai.size, 3, np.uint64)).spawn()      # left open: deferred exchange session
+del a                                                      # dropped before anything applies it
+b = lam.AtomicArray(world.team(), n_len, lam.Distribution.Block, "u64")
+bi = rng.integers(0, n_len, 500000).astype(np.uint64)
+b.batch_add(bi, np.full(bi.size, 5, np.uint64)).spawn()
+world.wait_all()
+ref = np.zeros(n_len, np.uint64)
+np.add.at(ref, bi.astype(np.int64), np.uint64(5))
+assert np.array_equal(b.to_numpy(), ref), "records of the dropped array reached the new one"
+print("drop ok", flush=True)
+world.barrier()
+'''
+
+
+def test_dropped_array_keeps_its_session():
+    """An array dropped while its exchange session is open: the session holds its shard until
+    the sweep runs, so a new array of the same size (which the caching allocator would place at
+    the freed address, continuing the session) sees none of the dropped array's records.
+    1-rank RCCL, forced exchange."""
+    env = dict(os.environ, LMR_ROOT=ROOT, LMR_LEN=str(PER_PE), LAMELLAR_COMM_BACKEND="nccl",
+               LAMELLAR_FORCE_EXCHANGE="1", LAMELLAR_EXCHANGE_CHUNK=str(1 << 18), RANK="0", WORLD_SIZE="1",
+               LOCAL_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(29500 + (os.getpid() % 50)))
+    p = subprocess.run([sys.executable, "-c", DROP_WORKER], env=env, timeout=170,
+                       stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
+    assert p.returncode == 0 and "drop ok" in p.stdout, p.stdout[-4000:]
