@@ -146,8 +146,8 @@ class DeviceKernels:
         returns -- the records are partitioned now (lmr_stage_flush, stream-ordered), so only
         the shard sweep waits for the flush."""
         key = (shard.data_ptr(), int(shard_len), int(kind), int(dt.code))
-        if self._deferred is not None and self._deferred[0] != key:
-            self.flush()
+        if (self._deferred is not None and self._deferred[0] != key) or self._xdeferred is not None:
+            self.flush()                      # (an open exchange session holds the context's session)
         if self.strategy != Strategy.Direct and n >= 65536 and self.reserved < min(n, self.max_ws_records):
             self.flush()                      # the workspace grows only with nothing staged
             self._maybe_reserve(n)
