@@ -579,6 +579,11 @@ def main():
             # bytes per record x this run's records per launch x launches per step
             pr = tr["_per_record"]
             traffic = sum(pr.get(st, 0.0) * (per[st][2] or W.ops_per_step / per[st][1]) * per[st][1] for st in per)
+            if "pack" in per and "_transport_per_record" in tr:
+                # RCCL's copies (send-buffer read, receive-buffer write) of the records that leave
+                # this PE: all of them in the one-rank rehearsal, (N - 1) / N of them at N PEs
+                share = 1.0 if npes == 1 else (npes - 1) / npes
+                traffic += tr["_transport_per_record"] * share * (per["pack"][2] or W.ops_per_step) * per["pack"][1]
         elif all(st in tr for st in per if st not in ("scan",)):
             traffic = sum(tr.get(st, 0.0) * per[st][1] for st in per)
             if "pack" in per and "_transport_per_pack" in tr:     # the exchange's RCCL copies
@@ -590,7 +595,9 @@ def main():
             "frac": achieved / HBM_PEAK, "traffic": traffic,
             "traffic_source": ("HBM bytes per step: committed rocprofv3 FETCH_SIZE/WRITE_SIZE passes "
                                f"(profiles/pmc_traffic_{cfg}.json, FETCH_SIZE x2 per the gfx950 note) x launches "
-                               "per step of this run; not measured in this run") if traffic else None,
+                               "per step of this run" + ("" if "pack" not in per else
+                                                         "; RCCL's copies x the share of records leaving this PE")
+                               + "; not measured in this run") if traffic else None,
             "scope": "whole step (every kernel of the op path), SURVEY 8(d) bytes per op",
             "bytes_per_op": W.survey_bpo, "ops_per_step": W.ops_per_step, "dominant_kernel": dom}
     stage_rows = {}
