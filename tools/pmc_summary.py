@@ -5,10 +5,12 @@ gfx950 corrections (MI355X_MICROARCH.md §HBM): FETCH_SIZE reports half the byte
 a wide coalesced stream -> doubled here; WRITE_SIZE is taken as reported.
 Stage bytes are per stage invocation: the bytes of all the stage's kernels divided
 by the launch count of the stage's anchor kernel (one launch per invocation).
-usage: tools/pmc_summary.py <prof dir with pmc_fetch/ and pmc_write/> [out.json [records per invocation]]
+usage: tools/pmc_summary.py <prof dir with pmc_fetch/ and pmc_write/> [out.json [records per invocation | bench log]]
 With the records each stage invocation processed in the profiled run (e.g. 2^28 for a C3 session of
 four 2^26-record batches), the json also holds "_per_record": bytes per record per stage, which
 bench.py scales by its own records per launch (a session's batch count depends on the run).
+Given instead the profiled bench command's log (its JSON line), each stage's records come from
+the line: records per step x the steps the command ran, so sessions of mixed sizes are fine.
 """
 import collections
 import csv
@@ -80,7 +82,23 @@ def main():
             inv = cnt["k_pack_count"]
         out["_transport_per_pack"] = rccl / inv
         print(f"transport (RCCL kernels)  {out['_transport_per_pack'] / 1e6:10.1f} MB per pack invocation")
-    if len(sys.argv) > 3:
+    if len(sys.argv) > 3 and not sys.argv[3][0].isdigit():
+        # the profiled bench command's own JSON line: its stage records per step (records per
+        # launch x launches per step) x every step the command ran (warmup, timed, profiled) are
+        # the records each stage processed, whatever the session sizes were
+        line = next(json.loads(x) for x in open(sys.argv[3]) if x.startswith('{"metric'))
+        steps = line["warmup"] + line["steps"] + line["apply_pipeline"]["profiled_steps"]
+        rps = {st: r["records_per_launch"] * r["launches_per_step"] for st, r in line["apply_pipeline"]["stages"].items()}
+        out["_per_record"] = {}
+        for st, (anchors, _) in STAGES.items():
+            inv = sum(cnt.get(a, 0) for a in anchors)
+            if st == "pack" and cnt.get("k_pack_count") and cnt.get("k_pack_stage"):
+                inv = cnt["k_pack_count"]
+            if st in out and rps.get(st):
+                out["_per_record"][st] = out[st] * inv / (steps * rps[st])
+        for st, v in out["_per_record"].items():
+            print(f"stage {st:16s} {v:10.2f} B per record")
+    elif len(sys.argv) > 3:
         recs = float(sys.argv[3])
         out["_per_record"] = {st: v / recs for st, v in out.items() if not st.startswith("_")}
         for st, v in out["_per_record"].items():
