@@ -62,7 +62,7 @@ def parse():
     p.add_argument("--no-verify", action="store_true")
     p.add_argument("--input-sets", type=int, default=0,
                    help="distinct input buffers rotated over the steps (0: one per step of a deferred "
-                        "session, up to 8)")
+                        "session, up to 16)")
     p.add_argument("--reserve-log2", type=int, default=30,
                    help="tiled-apply workspace (records, log2; 0: the step's records). The engine defers "
                         "large 1-PE batches into one staged session until the workspace is full, so a "
