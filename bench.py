@@ -89,7 +89,8 @@ def stage_bytes_per_op(stage, iw, vb, eb, n, shard_len, fetch, wide=False):
     Returned values travel binned -> temp -> input order through stored u32 maps
     (qpos written by the coarse pass, rpos by the fine pass). fetch: the share of records
     whose op returns a value (C5: 2 of 5 batches); the un-partition counts only those.
-    wide: the one-level staged partition (lmr_wide.hip: 8-byte elements, <= 2^24 of them):
+    wide: the one-level staged partition (lmr_wide.hip: 8-byte elements, <= 2^24 of them, or
+    1/2/4-byte elements, <= 2^26):
     the scatter writes u16 tile offsets and a u16 staging position per record, one gather
     brings the olds back."""
     pos = 4 * float(fetch)
@@ -601,8 +602,10 @@ def main():
             "scope": "whole step (every kernel of the op path), SURVEY 8(d) bytes per op",
             "bytes_per_op": W.survey_bpo, "ops_per_step": W.ops_per_step, "dominant_kernel": dom}
     stage_rows = {}
-    # the wide one-level staged path (no fine pass for an 8-byte shard of <= 2^24 elements)
-    wide = W.eb == 8 and W.elems <= (1 << 24) and "fine_scatter" not in per and "tile_apply" in per
+    # the wide one-level staged path (no fine pass: 8-byte shards of <= 2^24 elements, smaller
+    # elements up to 2^26)
+    wide = (W.elems <= (1 << 24) if W.eb == 8 else W.elems <= (1 << 26)) and "fine_scatter" not in per \
+        and "tile_apply" in per
     for st, (avg_ms, lps, rpl) in per.items():
         ops_per_launch = rpl if rpl else W.ops_per_step / lps
         bpo = stage_bytes_per_op(st, iw, W.vb, W.eb, ops_per_launch, W.elems, W.fetch, wide)

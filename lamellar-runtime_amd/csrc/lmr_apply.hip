@@ -2564,7 +2564,7 @@ hipError_t launch_stage_finish(const TiledWs& w, StageSession& s, hipStream_t st
         if (s.reg[r].ret != LMR_RET_NONE && (a.ret == LMR_RET_NONE || s.reg[r].ret == LMR_RET_RESULT))
             a.ret = s.reg[r].ret;                                 // maps kept if any region returns
     const int dtype = s.dtype;
-    const int shift = wide ? kWideShift8 : tile_shift_for(dtype);
+    const int shift = wide ? wide_shift(dtype_bytes(dtype)) : tile_shift_for(dtype);
     const uint32_t T = uint32_t((a.shard_len + (uint64_t(1) << shift) - 1) >> shift);
     const int vb = dtype_bytes(dtype);
     const uint32_t stride = uint32_t(kMaxTiles + 1);
@@ -2594,6 +2594,7 @@ hipError_t launch_stage_finish(const TiledWs& w, StageSession& s, hipStream_t st
         t.results = res_bin; t.ok = ok_bin; t.err = a.err;
         t.rts = w.rts; t.nreg = uint32_t(s.nreg); t.rstride = stride;
         t.mixed = mixed ? 1 : 0;
+        t.packed = wide && s.wpack ? 1 : 0;
         for (int r = 0; r < s.nreg; r++)
             t.rop[r] = RegionOp{s.reg[r].op, s.reg[r].ret, s.reg[r].cmp_bits, s.reg[r].eps_bits};
         // delta mode needs one combinable op; a mixed session's hot tiles stay with their owner

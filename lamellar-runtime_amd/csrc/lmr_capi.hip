@@ -56,6 +56,25 @@ void stage_abort(StageState* s) {
     s->open = false;
     s->s = StageSession();
 }
+// A count-free session whose regions are only recorded (none partitioned, none with a device-side
+// count) and whose shard takes the wide path becomes a counted session: its regions keep their op
+// and are the first phase of the mixed session that follows (lmr_stage_op).
+bool stage_free_to_wide(StageSession& s, uint64_t cap) {
+    if (!s.free || s.parted != 0 || s.nreg == 0 || !wide_applies(s.dtype, s.pend[0].a.shard_len, cap)) return false;
+    for (int r = 0; r < s.nreg; r++)
+        if (s.pend[r].n_dev) return false;
+    uint64_t b = 0;
+    for (int r = 0; r < s.nreg; r++) {
+        s.reg[r].base = b;
+        s.reg[r].results = nullptr;
+        s.reg[r].ok = nullptr;
+        s.reg[r].ret = LMR_RET_NONE;
+        b += s.reg[r].n;
+    }
+    s.staged = b;
+    s.free = false;
+    return true;
+}
 bool stage_pending_other_op(const StageSession& s, const ApplyArgs& a) {
     for (int r = 0; r < s.nreg; r++)
         if (s.reg[r].op != a.op || s.reg[r].cmp_bits != a.cmp_bits || s.reg[r].eps_bits != a.eps_bits) return true;
@@ -241,6 +260,11 @@ uint64_t staged_mode_split(int dtype, int op, int ret, uint64_t shard_len, uint6
 // Run a record stream with the chosen strategy, in workspace-sized pieces.
 lmr_status_t run_apply(lmr_ctx* ctx, const lmr_apply_desc_t* d, ApplyArgs a, int iw,
                        hipStream_t s) {
+    // a deferred exchange session's records live in the workspace this call may use: applied first
+    if (ctx->xdefer_open) {
+        const lmr_status_t st = lmr_exchange_flush(ctx, reinterpret_cast<lmr_stream_t>(s));
+        if (st != LMR_OK) return st;
+    }
     const int eb = dtype_bytes(int(d->dtype));
     if (d->strategy == LMR_STRATEGY_ORDERED || (d->strategy == LMR_STRATEGY_AUTO && a.n < kOrderedAuto))
         return hip_status(launch_apply_ordered(ctx, int(d->dtype), iw, a, s));
@@ -740,7 +764,7 @@ lmr_status_t lmr_apply_soa(lmr_ctx_t* ctx, const lmr_apply_desc_t* desc, const v
 
 // ---------------------------------------------------------------- staged apply
 lmr_status_t lmr_stage_begin(lmr_ctx_t* ctx, const lmr_apply_desc_t* desc) {
-    if (!ctx) return LMR_E_INVALID;
+    if (!ctx || ctx->xdefer_open) return LMR_E_INVALID;      // (a deferred exchange session: flush first)
     lmr_status_t st = check_desc(desc);
     if (st != LMR_OK) return st;
     if (!desc->shard) return LMR_E_INVALID;
@@ -760,7 +784,7 @@ lmr_status_t lmr_stage_begin(lmr_ctx_t* ctx, const lmr_apply_desc_t* desc) {
 
 lmr_status_t lmr_stage_soa(lmr_ctx_t* ctx, const void* d_indices, uint32_t index_size, const void* d_vals,
                            const void* val, uint64_t n, void* d_results, uint8_t* d_ok, lmr_stream_t stream) {
-    if (!ctx || !ctx->stage || !ctx->stage->open || !valid_iw(index_size)) return LMR_E_INVALID;
+    if (!ctx || ctx->xdefer_open || !ctx->stage || !ctx->stage->open || !valid_iw(index_size)) return LMR_E_INVALID;
     if (n == 0) return LMR_OK;
     if (!d_indices || (!d_vals && !val)) return LMR_E_INVALID;
     StageState* S = ctx->stage;
@@ -788,7 +812,7 @@ lmr_status_t lmr_stage_soa(lmr_ctx_t* ctx, const void* d_indices, uint32_t index
 }
 
 lmr_status_t lmr_stage_op(lmr_ctx_t* ctx, uint32_t op, uint64_t cmp_bits, uint64_t eps_bits, lmr_stream_t stream) {
-    if (!ctx || !ctx->stage || !ctx->stage->open) return LMR_E_INVALID;
+    if (!ctx || ctx->xdefer_open || !ctx->stage || !ctx->stage->open) return LMR_E_INVALID;
     StageState* S = ctx->stage;
     lmr_apply_desc_t d = S->desc;
     d.op = op;
@@ -799,8 +823,10 @@ lmr_status_t lmr_stage_op(lmr_ctx_t* ctx, uint32_t op, uint64_t cmp_bits, uint64
     const lmr_apply_desc_t& c = S->desc;
     if (c.op == op && c.cmp_bits == cmp_bits && c.eps_bits == eps_bits) return LMR_OK;
     if (S->s.nreg > 0) {
-        // count-free regions share their bucket regions: apply them before the next op phase
-        if (S->s.free) {
+        // count-free regions share their bucket regions: apply them before the next op phase,
+        // unless the session takes the wide path and nothing is partitioned yet: then they are
+        // counted regions of its first phase (one partition and one sweep for every phase)
+        if (S->s.free && !stage_free_to_wide(S->s, ctx->rec_cap)) {
             const hipError_t e = launch_stage_finish(ctx_ws(ctx, ctx->rec_cap), S->s,
                                                      reinterpret_cast<hipStream_t>(stream));
             if (e != hipSuccess) return hip_status(e);
@@ -818,7 +844,7 @@ lmr_status_t lmr_stage_op(lmr_ctx_t* ctx, uint32_t op, uint64_t cmp_bits, uint64
 }
 
 lmr_status_t lmr_stage_flush(lmr_ctx_t* ctx, lmr_stream_t stream) {
-    if (!ctx || !ctx->stage || !ctx->stage->open) return LMR_E_INVALID;
+    if (!ctx || ctx->xdefer_open || !ctx->stage || !ctx->stage->open) return LMR_E_INVALID;
     StageSession& ss = ctx->stage->s;
     if (ss.parted == ss.nreg) return LMR_OK;
     return hip_status(launch_stage_partition(ctx_ws(ctx, ctx->rec_cap), ss,
@@ -826,7 +852,7 @@ lmr_status_t lmr_stage_flush(lmr_ctx_t* ctx, lmr_stream_t stream) {
 }
 
 lmr_status_t lmr_stage_finish(lmr_ctx_t* ctx, lmr_stream_t stream) {
-    if (!ctx || !ctx->stage || !ctx->stage->open) return LMR_E_INVALID;
+    if (!ctx || ctx->xdefer_open || !ctx->stage || !ctx->stage->open) return LMR_E_INVALID;
     StageState* S = ctx->stage;
     S->open = false;
     if (S->s.nreg == 0) return LMR_OK;

@@ -596,11 +596,12 @@ lmr_status_t lmr_batch_exchange(lmr_ctx_t* ctx, const lmr_transport_t* tp, const
     // the same op on the same shard and stages count-free; otherwise it is applied first
     lmr_status_t st = LMR_OK;
     bool cont = false;
-    if (ctx->xdefer_open && stage_session_open(ctx)) {
+    const bool was_open = ctx->xdefer_open && stage_session_open(ctx);
+    ctx->xdefer_open = false;                   // (the staged-session calls refuse while it is set)
+    if (was_open) {
         cont = !returning && !ordered && stage_session_free(ctx) && stage_session_of(ctx, *desc);
         if (!cont && (st = lmr_stage_finish(ctx, reinterpret_cast<lmr_stream_t>(x->sa))) != LMR_OK) return st;
     }
-    ctx->xdefer_open = false;
     if (!cont && (st = lmr_stage_begin(ctx, desc)) != LMR_OK) return st;
     // fixed-region mode: a FIXED sender's regions go whole to DEVCOUNT receivers (their count-free
     // session stages each region with its record count read on the device from the header rows),
@@ -1161,6 +1162,13 @@ lmr_status_t lmr_exchange_flush(lmr_ctx_t* ctx, lmr_stream_t stream) {
     if (!ctx->xdefer_open) return LMR_OK;
     ctx->xdefer_open = false;
     if (!stage_session_open(ctx)) return LMR_OK;
+    // the session was staged on the exchange's apply stream: `stream` (any stream, per the
+    // header) waits for that staging before the sweep
+    if (XState* x = ctx->xch) {
+        if (hipEventRecord(x->ev_apply_done, x->sa) != hipSuccess ||
+            hipStreamWaitEvent(reinterpret_cast<hipStream_t>(stream), x->ev_apply_done, 0) != hipSuccess)
+            return LMR_E_HIP;
+    }
     return lmr_stage_finish(ctx, stream);
 }
 

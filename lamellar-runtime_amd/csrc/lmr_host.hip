@@ -12,13 +12,14 @@
 //   d2h stream : copy piece i's results / Ok flags out (waits for apply i)
 //
 // so piece i+1's upload and piece i-1's result download overlap piece i's
-// apply; PCIe (full duplex) is the bound. Registering the host buffer
-// (lmr_host_register = hipHostRegister of the lamellae heap) lets the DMA
-// engines read it in place.
+// apply; PCIe (full duplex) is the bound. The DMA engines read in place what is page-locked for
+// the library's purposes: a lamellae heap page-locked once for its lifetime
+// (lmr_host_register_heap) and memory the HIP runtime allocated pinned (lmr_host_alloc).
 //
-// The library DMAs only between the device and host memory it knows is page-locked: ranges
-// registered through lmr_host_register, memory the HIP runtime itself allocated pinned
-// (lmr_host_alloc / hipHostMalloc), and its own pinned bounce buffers. Records in pageable memory
+// The library DMAs only between the device and host memory it knows is page-locked: the inner
+// pages of a heap registered with lmr_host_register_heap, memory the HIP runtime itself allocated
+// pinned (lmr_host_alloc / hipHostMalloc), and its own pinned bounce buffers (lmr_host_register
+// only records a range: its buffers are staged like pageable ones). Records in pageable memory
 // are copied by the host into a pinned slot before their upload; results / Ok flags bound for
 // pageable memory land in a pinned slot and the host copies them out (the call then returns
 // once they are written).

@@ -68,10 +68,13 @@ constexpr int kMaxWindows = 256;          // tiled windows per shard (lmr_window
 constexpr int kMaxRegions = 32;           // staged-apply regions per session
 constexpr int kStageInfoWords = 512;      // staged-apply piece table + per-region totals (u32)
 constexpr uint64_t kStageMaxRegion = uint64_t(1) << 30;   // records per staged region
-// the one-level ("wide") staged partition (lmr_wide.hip): 8-byte elements, 128 KiB tiles
-constexpr int kWideShift8 = 14;           // elements per wide tile: 2^14 x 8 B
+// the one-level ("wide") staged partition (lmr_wide.hip): 128 KiB tiles of LDS words
+constexpr int kWideShift8 = 14;           // 8-byte elements per wide tile: 2^14 x 8 B
+constexpr int kWideShift4 = 15;           // 1/2/4-byte elements (32-bit LDS words): 2^15 x 4 B
 constexpr uint32_t kWideBytes = 128 * 1024;
-constexpr uint32_t kWideMaxTiles = 1024;  // a shard of at most 2^24 elements
+constexpr uint32_t kWideMaxTiles = 1024;  // 8-byte elements: a shard of at most 2^24 elements
+constexpr uint32_t kWideMaxTiles4 = 2048; // 1/2/4-byte elements: at most 2^26 elements
+inline int wide_shift(int dtype_b) { return dtype_b == 8 ? kWideShift8 : kWideShift4; }
 
 // ---- stage timing: HIP events around kernel stages (see lmr_ctx_profile) ----
 // n: records the stage processes (reported per stage by lmr_ctx_profile_read)
@@ -234,6 +237,7 @@ struct StageSession {
     bool switched = false;  // the op changed with records staged (lmr_stage_op): later phases counted
     bool wide = false;      // counted regions partitioned one-level into 128 KiB tiles (wide_applies)
     bool wide_set = false;  //   decided at the session's first partition
+    bool wpack = false;     // wide, 1/2/4-byte elements: packed uint2 records (TileArgs::packed)
     uint64_t wcnt = 0;      // wide: count entries in use
     uint64_t wrh = 0;       // wide: round-count entries (u16) in use
     StageRegion reg[kMaxRegions];
@@ -256,8 +260,10 @@ hipError_t launch_stage_region_dev(int dtype, int index_size, const ApplyArgs& a
                                    uint64_t expect, const TiledWs& w, StageSession& s, hipStream_t st);
 // apply every staged region in one tile sweep, results back to each region's caller
 hipError_t launch_stage_finish(const TiledWs& w, StageSession& s, hipStream_t st);
-// the wide path (lmr_wide.hip): applies to 8-byte element shards of <= kWideMaxTiles wide tiles
-// with a workspace whose rpos holds the round counts; partition of the pending regions; the
+// the wide path (lmr_wide.hip): applies to shards of <= kWideMaxTiles 128 KiB tiles of 8-byte
+// elements (kWideMaxTiles4 for 1/2/4-byte elements) with a workspace whose rpos holds the round
+// counts (LMR_WIDE=0 turns it off, LMR_WIDE4=0 for elements below 8 bytes, read per session);
+// partition of the pending regions; the
 // returning regions' results from binned order back to arrival order after the tile sweep
 bool wide_applies(int dtype, uint64_t shard_len, uint64_t cap);
 hipError_t wide_partition(const TiledWs& w, StageSession& s, hipStream_t st);

@@ -165,13 +165,20 @@ __global__ __launch_bounds__(1024, 8) void k_tile_owner(TileArgs a) {
             constexpr uint32_t per = 16 / sizeof(T);
             const uint32_t nv = len / per;
             // a full 64 KiB tile is 4 uint4 per thread: all four loads in flight, then the stores
-            // (a load / wait / LDS-store loop kept one in flight)
-            if (nv == 4 * 1024u) {
-                uint4 x[4];
-#pragma unroll
-                for (int i = 0; i < 4; i++) x[i] = reinterpret_cast<const uint4*>(shard)[threadIdx.x + i * 1024u];
-#pragma unroll
-                for (int i = 0; i < 4; i++) reinterpret_cast<uint4*>(tile)[threadIdx.x + i * 1024u] = x[i];
+            // (a load / wait / LDS-store loop kept one in flight); a 128 KiB wide tile is two such
+            // groups (eight in flight spilled the 4-byte kernel's registers)
+            if (nv == 4 * 1024u || nv == 8 * 1024u) {
+                // (named registers, not a uint4[4]: the array stayed a stack object in the 4-byte
+                // kernels, 48 B of dead scratch stores per thread and group)
+                const uint4* src4 = reinterpret_cast<const uint4*>(shard) + threadIdx.x;
+                uint4* dst4 = reinterpret_cast<uint4*>(tile) + threadIdx.x;
+                for (uint32_t h = 0; h < nv; h += 4 * 1024u) {
+                    const uint4 x0 = src4[h], x1 = src4[h + 1024u], x2 = src4[h + 2048u], x3 = src4[h + 3072u];
+                    dst4[h] = x0;
+                    dst4[h + 1024u] = x1;
+                    dst4[h + 2048u] = x2;
+                    dst4[h + 3072u] = x3;
+                }
             } else {
                 for (uint32_t v = threadIdx.x; v < nv; v += blockDim.x)
                     reinterpret_cast<uint4*>(tile)[v] = reinterpret_cast<const uint4*>(shard)[v];
@@ -209,6 +216,24 @@ __global__ __launch_bounds__(1024, 8) void k_tile_owner(TileArgs a) {
             if (ret == LMR_RET_RESULT) a.ok[r] = ok;
         }
     };
+    if constexpr (sizeof(T) <= 4) {
+        // packed records (the wide path): one 8-B load per record, kPk in flight per thread
+        if (a.packed) {
+            const uint2* rec = reinterpret_cast<const uint2*>(a.bin_val);
+            constexpr uint32_t kPk = 8;
+            for (uint32_t b0 = lo; b0 < hi; b0 += kPk * 1024u) {
+                uint2 x[kPk];
+#pragma unroll
+                for (uint32_t k = 0; k < kPk; k++) x[k] = rec[min(b0 + threadIdx.x + k * 1024u, hi - 1)];
+#pragma unroll
+                for (uint32_t k = 0; k < kPk; k++) {
+                    const uint32_t r = b0 + threadIdx.x + k * 1024u;
+                    if (r < hi) apply_one(r, x[k].x, from_bits<T>(U(x[k].y)));
+                }
+            }
+            continue;
+        }
+    }
     if constexpr (sizeof(T) == 4) {
         // 4-byte values: 4 consecutive records per thread and iteration, one 8-B load of their
         // offsets and one 16-B load of their values (fewer, wider memory instructions than a 2-B
@@ -330,8 +355,8 @@ __global__ __launch_bounds__(1024) void k_tile_delta(TileArgs a) {
     const int gop = fsub ? int(LMR_OP_FETCH_ADD) : delta_global_op(op);
     const int fop = fsub ? int(LMR_OP_FETCH_ADD) : op;
     // elements some record of the piece touched (fetch forms: only those need their base)
-    __shared__ uint32_t touched[16384 / 32];
-    static_assert(TB / int(sizeof(W)) <= 16384, "touched[] covers 16K elements");
+    constexpr int kTileWords = TB / int(sizeof(W));
+    __shared__ uint32_t touched[kTileWords / 32];
     for (uint32_t it = blockIdx.x; it < nitems; it += gridDim.x) {
         const TileItem w = a.delta[it];
         const uint64_t base = uint64_t(w.tile) << a.tile_shift;
@@ -348,6 +373,14 @@ __global__ __launch_bounds__(1024) void k_tile_delta(TileArgs a) {
 #pragma unroll
         for (int k = 0; k < int(kSplit / 1024); k++) {
             const uint32_t r = min(w.lo + threadIdx.x + uint32_t(k) * 1024u, w.hi - 1);
+            if constexpr (sizeof(T) <= 4) {
+                if (a.packed) {                                 // the wide path's packed records
+                    const uint2 x = reinterpret_cast<const uint2*>(a.bin_val)[r];
+                    lk[k] = uint16_t(x.x);
+                    vk[k] = from_bits<T>(U(x.y));
+                    continue;
+                }
+            }
             lk[k] = bin_lidx[r];
             vk[k] = a.scalar ? sv : bin_val[r];
         }
@@ -368,38 +401,45 @@ __global__ __launch_bounds__(1024) void k_tile_delta(TileArgs a) {
             if (in && ret != LMR_RET_NONE && U(to_bits(pre[k])) == U(ident_bits)) atomicOr(&touched[l >> 5], 1u << (l & 31));
         }
         __syncthreads();
-        // one device-scope atomic per changed element, a load per touched unchanged one;
-        // every element's operation is issued before any result is waited for
-        constexpr int kPer = TB / int(sizeof(W)) / 1024;   // elements per thread (a tile's words / 1024)
-        T b[kPer];
-        bool need[kPer];
+        // one device-scope atomic per changed element, a load per touched unchanged one; every
+        // element's operation of a group of up to 16 per thread is issued before any result is
+        // waited for (a 128 KiB tile of 32-bit words is two groups)
+        constexpr int kPer = kTileWords / 1024;           // elements per thread (a tile's words / 1024)
+        constexpr int kGrp = kPer < 16 ? kPer : (kPer > 16 ? 8 : 16);   // (16 of 32 spilled)
+        static_assert(kPer % kGrp == 0, "whole groups");
+        for (int k0 = 0; k0 < kPer; k0 += kGrp) {
+            T b[kGrp];
+            bool need[kGrp];
 #pragma unroll
-        for (int k = 0; k < kPer; k++) {
-            const uint32_t e = threadIdx.x + uint32_t(k) * 1024u;
-            need[k] = false;
-            if (e < len) {
-                T d;
-                if constexpr (sizeof(T) >= 4) d = tile[e];
-                else d = T(U(tile[e]));
-                uint8_t ok = 0;
-                if (U(to_bits(d)) != U(ident_bits)) {
-                    b[k] = rmw_global<T>(shard + e, gop, a.kind, d, cmp, eps, ok, a.err);
-                    need[k] = true;
-                } else if (ret != LMR_RET_NONE && ((touched[e >> 5] >> (e & 31)) & 1u)) {
-                    b[k] = rmw_global<T>(shard + e, LMR_OP_LOAD, a.kind, d, cmp, eps, ok, a.err);
-                    need[k] = true;
+            for (int k = 0; k < kGrp; k++) {
+                const uint32_t e = threadIdx.x + uint32_t(k0 + k) * 1024u;
+                need[k] = false;
+                if (e < len) {
+                    T d;
+                    if constexpr (sizeof(T) >= 4) d = tile[e];
+                    else d = T(U(tile[e]));
+                    uint8_t ok = 0;
+                    if (U(to_bits(d)) != U(ident_bits)) {
+                        b[k] = rmw_global<T>(shard + e, gop, a.kind, d, cmp, eps, ok, a.err);
+                        need[k] = true;
+                    } else if (ret != LMR_RET_NONE && ((touched[e >> 5] >> (e & 31)) & 1u)) {
+                        b[k] = rmw_global<T>(shard + e, LMR_OP_LOAD, a.kind, d, cmp, eps, ok, a.err);
+                        need[k] = true;
+                    }
+                }
+            }
+            if (ret != LMR_RET_NONE) {
+#pragma unroll
+                for (int k = 0; k < kGrp; k++) {
+                    const uint32_t e = threadIdx.x + uint32_t(k0 + k) * 1024u;
+                    if (need[k]) {
+                        if constexpr (sizeof(T) >= 4) tile[e] = b[k];
+                        else tile[e] = W(U(b[k]));
+                    }
                 }
             }
         }
         if (ret != LMR_RET_NONE) {
-#pragma unroll
-            for (int k = 0; k < kPer; k++) {
-                const uint32_t e = threadIdx.x + uint32_t(k) * 1024u;
-                if (need[k]) {
-                    if constexpr (sizeof(T) >= 4) tile[e] = b[k];
-                    else tile[e] = W(U(b[k]));
-                }
-            }
             __syncthreads();
 #pragma unroll
             for (int k = 0; k < int(kSplit / 1024); k++) {
@@ -499,14 +539,8 @@ hipError_t launch_tile_kernels(int dtype, int opt, const TileArgs& t, bool delta
             if (opt == LMR_OP_FETCH_ADD) return go(std::integral_constant<int, LMR_OP_FETCH_ADD>{}, tbc);
             return go(std::integral_constant<int, -1>{}, tbc);
         };
-        hipError_t el;
-        if constexpr (sizeof(Ty) == 8) {
-            if (tile_bytes == kWideBytes) el = by_op(std::integral_constant<int, int(kWideBytes)>{});
-            else el = by_op(std::integral_constant<int, kTileBytes>{});
-        } else {
-            if (tile_bytes != kTileBytes) return hipErrorInvalidValue;
-            el = by_op(std::integral_constant<int, kTileBytes>{});
-        }
+        const hipError_t el = tile_bytes == kWideBytes ? by_op(std::integral_constant<int, int(kWideBytes)>{})
+                                                       : by_op(std::integral_constant<int, kTileBytes>{});
         return el != hipSuccess ? el : hipGetLastError();
     });
     // the launch stream continues after both (joined even when a launch failed)

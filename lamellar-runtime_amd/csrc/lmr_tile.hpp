@@ -58,6 +58,9 @@ struct TileArgs {
     // region of the tile after the previous one (staging order per element)
     int mixed;
     RegionOp rop[kMaxRegions];
+    // the wide path's packed records (1/2/4-byte elements): bin_val holds one uint2 per record,
+    // {tile-local index, value bits}, and bin_lidx is unused
+    int packed = 0;
 };
 
 __host__ __device__ constexpr bool op_combines(int op) {
@@ -70,7 +73,7 @@ __host__ __device__ constexpr bool op_combines(int op) {
 // side lane when there is one: the two kernels touch disjoint tiles and records);
 // opt: LMR_OP_ADD / LMR_OP_FETCH_ADD select the specialised kernels, anything else the
 // generic op switch
-// tile_bytes: kTileBytes, or kWideBytes for 8-byte elements (the wide staged path's tiles)
+// tile_bytes: kTileBytes, or kWideBytes (the wide staged path's tiles of LDS words)
 hipError_t launch_tile_kernels(int dtype, int opt, const TileArgs& t, bool delta, unsigned dgrid, hipStream_t s,
                                const SideLane& side, uint32_t tile_bytes = kTileBytes);
 

@@ -29,6 +29,20 @@ def test_ctypes_binding_covers_header(lam):
     assert set(declared_symbols()) == set(_capi.SIGNATURES)
 
 
+def test_integration_extern_block_covers_header():
+    """INTEGRATION.md's Rust `extern "C"` block declares every function of the C ABI."""
+    text = open(os.path.join(ROOT, "INTEGRATION.md")).read()
+    blocks = re.findall(r"```rust\n(.*?)```", text, flags=re.S)
+    declared = set()
+    for b in blocks:
+        for ext in re.findall(r'extern "C" \{(.*?)\n\}', b, flags=re.S):
+            declared |= set(re.findall(r"\bpub fn (lmr_[a-z0-9_]+)\s*\(", ext))
+    missing = sorted(set(declared_symbols()) - declared)
+    assert not missing, missing
+    extra = sorted(declared - set(declared_symbols()))
+    assert not extra, extra
+
+
 def test_abi_version_and_status_strings(capi, lam):
     from lamellar_runtime_amd import _capi
     assert capi.lmr_abi_version() == 8

@@ -163,3 +163,65 @@ def test_dropped_array_keeps_its_session():
     p = subprocess.run([sys.executable, "-c", DROP_WORKER], env=env, timeout=170,
                        stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
     assert p.returncode == 0 and "drop ok" in p.stdout, p.stdout[-4000:]
+
+
+CABI_WORKER = r'''
+import ctypes, os, sys
+import numpy as np
+import torch
+sys.path.insert(0, os.environ["LMR_ROOT"])
+from _lamellar_bootstrap import load_package
+lam = load_package()
+from lamellar_runtime_amd import _capi
+world = lam.LamellarWorldBuilder().build()
+n_len = int(os.environ["LMR_LEN"])
+rng = np.random.default_rng(1234)
+k = world.team().kernels
+k.reserve(1 << 22)
+lib = _capi.lib()
+a = lam.AtomicArray(world.team(), n_len, lam.Distribution.Block, "u64")
+ai = rng.integers(0, n_len, 600000).astype(np.uint64)
+av = rng.integers(0, 2**63, ai.size, dtype=np.uint64)
+a.batch_add(ai, av).spawn()                 # exchange left open: a deferred session in the workspace
+assert k._xdeferred is not None
+# a Rust caller on the raw ABI, with no Python flush in between: a tiled apply on another shard ...
+m = 1 << 20
+b = torch.zeros(n_len, dtype=torch.int64, device=k.device)
+bi = rng.integers(0, n_len, m).astype(np.uint64)
+bv = rng.integers(0, 2**63, m, dtype=np.uint64)
+ti = torch.from_numpy(bi.view(np.int64)).to(k.device)
+tv = torch.from_numpy(bv.view(np.int64)).to(k.device)
+d = k._desc(b, n_len, 1, lam.dtype_of("u64"), int(lam.ArrayOpCmd.Add))
+st = lib.lmr_apply_soa(k.ctx, ctypes.byref(d), ti.data_ptr(), 8, tv.data_ptr(), None, m, None, None, k.stream())
+assert st == 0, st
+# ... and the staged-session calls are refused until the flush
+assert lib.lmr_stage_begin(k.ctx, ctypes.byref(d)) == 1
+k._xdeferred = None                         # (the apply above applied the open session already)
+assert lib.lmr_exchange_flush(k.ctx, k.stream()) == 0
+assert lib.lmr_stage_begin(k.ctx, ctypes.byref(d)) == 0
+assert lib.lmr_stage_finish(k.ctx, k.stream()) == 0
+torch.cuda.synchronize()
+assert k.errors() == 0
+ra = np.zeros(n_len, np.uint64)
+np.add.at(ra, ai.astype(np.int64), av)
+rb = np.zeros(n_len, np.uint64)
+np.add.at(rb, bi.astype(np.int64), bv)
+assert np.array_equal(a.to_numpy(), ra), "the deferred exchange batch"
+assert np.array_equal(b.cpu().numpy().view(np.uint64), rb), "the tiled apply on the other shard"
+print("cabi ok", flush=True)
+world.barrier()
+'''
+
+
+def test_deferred_session_protected_at_the_c_abi():
+    """A deferred exchange session lives in the context's workspace: a tiled lmr_apply_soa on
+    another shard, called through the raw C ABI with no flush in between (a Rust caller), applies
+    the open session first in its stream order instead of reusing the workspace under it, and
+    lmr_stage_begin is refused until lmr_exchange_flush. Both arrays equal numpy's replay.
+    1-rank RCCL, forced exchange."""
+    env = dict(os.environ, LMR_ROOT=ROOT, LMR_LEN=str(PER_PE), LAMELLAR_COMM_BACKEND="nccl",
+               LAMELLAR_FORCE_EXCHANGE="1", LAMELLAR_EXCHANGE_CHUNK=str(1 << 18), RANK="0", WORLD_SIZE="1",
+               LOCAL_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(29550 + (os.getpid() % 50)))
+    p = subprocess.run([sys.executable, "-c", CABI_WORKER], env=env, timeout=170,
+                       stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
+    assert p.returncode == 0 and "cabi ok" in p.stdout, p.stdout[-4000:]

@@ -223,3 +223,68 @@ def test_heap_buffers_dma_in_place(world, orc, lam):
         assert bits_equal(h_res.copy(), res_o)
         if op == CAS:
             assert np.array_equal(h_ok, ok_o)
+
+
+HEAP_SHUTDOWN_WORKER = r'''
+import mmap, os, sys
+import numpy as np
+import torch
+sys.path.insert(0, os.environ["LMR_ROOT"])
+from _lamellar_bootstrap import load_package
+lam = load_package()
+from lamellar_runtime_amd import _capi
+world = lam.LamellarWorldBuilder().build()
+k = world.team().kernels
+lib = _capi.lib()
+rng = np.random.default_rng(2026)
+shard_len, n = 1 << 20, 3 * 65536 + 77
+for rnd in range(3):
+    m = mmap.mmap(-1, 32 << 20)                       # the lamellae heap of one world's lifetime
+    heap = np.frombuffer(m, dtype=np.uint8)
+    k.host_register_heap(heap)
+    idx = rng.integers(0, shard_len, n).astype(np.uint32)
+    vals = rng.integers(0, 2**40, n, dtype=np.uint64)
+    rec = np.zeros(n, np.dtype([("i", "<u4"), ("pad", "<u4"), ("v", "<u8")]))
+    rec["i"], rec["v"] = idx, vals
+    buf = heap[4096 + 8 * rnd:4096 + 8 * rnd + rec.nbytes]
+    buf[:] = rec.view(np.uint8)
+    olds = heap[(8 << 20) + 16:(8 << 20) + 16 + 8 * n].view(np.uint64)
+    shard = torch.zeros(shard_len, dtype=torch.int64, device=k.device)
+    dt = lam.dtype_of("u64")
+    k.apply_mvmi_host(shard, shard_len, 1, dt, int(lam.ArrayOpCmd.FetchAdd), buf, 4, olds)
+    ref = np.zeros(shard_len, np.uint64)
+    np.add.at(ref, idx.astype(np.int64), vals)
+    assert np.array_equal(shard.cpu().numpy().view(np.uint64), ref)
+    got = olds.copy()
+    # shutdown: the heap unregistered (the library drains its host-stage copies first), dropped,
+    # unmapped; then pageable copies of fresh memory, some of it at the heap's old addresses
+    k.host_unregister_heap(heap)
+    del buf, olds, heap
+    m.close()
+    for _ in range(3):
+        x = rng.integers(0, 2**62, (4 << 20) // 8, dtype=np.int64)
+        assert np.array_equal(torch.from_numpy(x).cuda().cpu().numpy(), x)
+    torch.cuda.synchronize()
+    assert k.errors() == 0
+    # the olds per element chain from 0 (distinct partial sums)
+    order = np.lexsort((got, idx))
+    ii, gg = idx[order], got[order]
+    first = np.r_[True, ii[1:] != ii[:-1]]
+    assert np.all(gg[first] == 0)
+print("heap shutdown ok", flush=True)
+'''
+
+
+def test_heap_shutdown_path():
+    """The lamellae heap's whole life, three times in one process: lmr_host_register_heap over a
+    fresh mapping, a fetch_add whose records and olds live in it (DMA'd in place), then
+    lmr_host_unregister_heap (the library drains its host-stage copies first), unmap, and pageable
+    copies of fresh memory. Runs in a process of its own: the fault rounds 3-5 saw followed an
+    unlock of caller memory, and a repeat must not take the suite's process with it."""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, LMR_ROOT=root, RANK="0", WORLD_SIZE="1", LOCAL_RANK="0")
+    p = subprocess.run([sys.executable, "-c", HEAP_SHUTDOWN_WORKER], env=env, timeout=170,
+                       stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
+    assert p.returncode == 0 and "heap shutdown ok" in p.stdout, p.stdout[-4000:]

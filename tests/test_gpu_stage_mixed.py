@@ -22,7 +22,7 @@ from test_gpu_parity import to_dev
 pytestmark = pytest.mark.gpu
 
 U32 = 2
-L = (1 << 22) + 333                     # 257 tiles of 16K u32: two-level partition
+L = (1 << 22) + 333                     # 129 wide tiles (LMR_WIDE4=1) / 257 two-level tiles of 16K u32
 N = 1 << 18
 
 
@@ -49,7 +49,9 @@ def _fold(op, init, idx, vals):
     return out
 
 
-def test_mixed_session_order_insensitive_phases(world, lam):
+@pytest.mark.parametrize("wide4", ["1", "0"], ids=["wide", "two-level"])
+def test_mixed_session_order_insensitive_phases(world, lam, monkeypatch, wide4):
+    monkeypatch.setenv("LMR_WIDE4", wide4)
     k = world.team().kernels
     dt = lam.dtype_of("u32")
     rng = np.random.default_rng(4242)
@@ -83,9 +85,10 @@ def test_mixed_session_order_insensitive_phases(world, lam):
     for (op, v), i in zip(phases, idxs):
         ref = _fold(op, ref, i, v)
     assert np.array_equal(got, ref)
-    # the count-free first phase is applied at the switch; the counted phases 2..6 share one
-    # sweep, or two when the workspace (at least 4 phases) fills
-    assert stages["tile_apply"][1] in (2, 3), stages
+    # two-level: the count-free first phase is applied at the switch; the counted phases 2..6
+    # share one sweep, or two when the workspace (at least 4 phases) fills; wide: the first phase
+    # joins the others
+    assert stages["tile_apply"][1] in ((1, 2) if wide4 == "1" else (2, 3)), stages
 
 
 def _swap_final(init, idx, vals, rets):
@@ -97,7 +100,9 @@ def _swap_final(init, idx, vals, rets):
     return acc.astype(np.uint32)
 
 
-def test_mixed_session_returning_phases(world, lam, orc):
+@pytest.mark.parametrize("wide4", ["1", "0"], ids=["wide", "two-level"])
+def test_mixed_session_returning_phases(world, lam, orc, monkeypatch, wide4):
+    monkeypatch.setenv("LMR_WIDE4", wide4)
     k = world.team().kernels
     dt = lam.dtype_of("u32")
     rng = np.random.default_rng(777)
@@ -147,8 +152,13 @@ def test_mixed_session_returning_phases(world, lam, orc):
     assert okC.cpu().numpy().any() and (~okC.cpu().numpy().astype(bool)).any()
 
 
-def test_deferred_batches_array_api(world, lam, orc):
-    """Spawned batches are staged and applied at the next flush point, in issue order."""
+@pytest.mark.parametrize("wide4", ["1", "0"], ids=["wide", "two-level"])
+def test_deferred_batches_array_api(world, lam, orc, monkeypatch, wide4):
+    """Spawned batches are staged and applied at the next flush point, in issue order. On the wide
+    path (the default for this u32 shard) the first, count-free batch is not partitioned yet at the
+    op switch and joins the later ones: one sweep; on the two-level path it is applied at the
+    switch."""
+    monkeypatch.setenv("LMR_WIDE4", wide4)
     team = world.team()
     arr = lam.AtomicArray(team, L, lam.Distribution.Block, "u32")
     rng = np.random.default_rng(99)
@@ -165,17 +175,21 @@ def test_deferred_batches_array_api(world, lam, orc):
     k.profile(True)
     k.profile_read(reset=True)
     try:
-        arr.batch_bit_xor(ti(iA), tv(vA)).spawn()
-        hS = arr.batch_swap(ti(iS), tv(vS)).spawn()
-        arr.batch_bit_or(ti(iO), tv(vO)).spawn()
+        # wide: the inputs handed over (Owned), so nothing is partitioned before the flush and the
+        # count-free first batch joins the others; two-level: plain (borrowed) tensors, each batch
+        # partitioned at its spawn
+        own = (lambda t: lam.Owned(t)) if wide4 == "1" else (lambda t: t)
+        arr.batch_bit_xor(own(ti(iA)), own(tv(vA))).spawn()
+        hS = arr.batch_swap(own(ti(iS)), own(tv(vS))).spawn()
+        arr.batch_bit_or(own(ti(iO)), own(tv(vO))).spawn()
         assert k._deferred is not None                    # nothing applied yet
         rS = hS.block()                                   # flush point
         stages = k.profile_read(reset=True)
     finally:
         k.profile(False)
     assert k._deferred is None
-    # xor (count-free) applied at the switch, swap + or in one sweep
-    assert stages["tile_apply"][1] == 2, stages
+    # two-level: xor (count-free) applied at the switch, swap + or in one sweep; wide: one sweep
+    assert stages["tile_apply"][1] == (1 if wide4 == "1" else 2), stages
     final = arr.to_numpy()
     s1 = _fold(XOR, s0, iA, vA)
     rs = rS.cpu().numpy().view(np.uint32)
@@ -212,12 +226,16 @@ def test_small_stream_after_other_op_phase(world, lam):
     assert np.array_equal(got, ref)
 
 
-def test_fused_partition_groups(world, lam):
+@pytest.mark.parametrize("wide4", ["1", "0"], ids=["wide", "two-level"])
+def test_fused_partition_groups(world, lam, monkeypatch, wide4):
     """Counted regions are partitioned together at the finish: one count / coarse / fine
     launch per group of up to 8 pending regions of one index width (u64 global and u32
     local indices here, 11 counted phases -> groups of 2, 3 and 6 regions: 3 launches per
     pass), each region with its own count rows, tile totals and tables; the final shard is
-    the serial per-phase replay, bit for bit."""
+    the serial per-phase replay, bit for bit. On the wide path (LMR_WIDE4=1, the default for this
+    shard) the count-free first phase joins the counted ones (groups of 3, 3 and 6 regions: 3 count
+    and 3 scatter launches, no fine pass)."""
+    monkeypatch.setenv("LMR_WIDE4", wide4)
     k = world.team().kernels
     dt = lam.dtype_of("u32")
     rng = np.random.default_rng(31337)
@@ -248,7 +266,11 @@ def test_fused_partition_groups(world, lam):
     for op, v, i in zip(ops, vals, idxs):
         ref = _fold(op, ref, i, v)
     assert np.array_equal(shard.cpu().numpy().view(np.uint32), ref)
-    assert stages["bin_count"][1] == 3 and stages["fine_scatter"][1] == 4, stages   # (+1: the free phase)
+    if wide4 == "1":
+        assert stages["bin_count"][1] == 3 and stages.get("fine_scatter", (0, 0))[1] == 0, stages
+        assert stages["tile_apply"][1] == 1, stages
+    else:
+        assert stages["bin_count"][1] == 3 and stages["fine_scatter"][1] == 4, stages   # (+1: the free phase)
 
 
 def test_deferred_fetch_add_batches_one_sweep(world, lam, orc):
