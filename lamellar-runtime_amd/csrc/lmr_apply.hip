@@ -2569,7 +2569,10 @@ hipError_t launch_stage_finish(const TiledWs& w, StageSession& s, hipStream_t st
     const int vb = dtype_bytes(dtype);
     const uint32_t stride = uint32_t(kMaxTiles + 1);
     const bool has_res = a.ret != LMR_RET_NONE;
-    uint8_t* res_bin = w.tmp_val;                                 // temps are free after the fine passes
+    // temps are free after the fine passes (the wide path's packed 16-B records live in tmp_val:
+    // results then go to bin_val)
+    uint8_t* const recs = wide ? wide_records(w, s) : w.bin_val;
+    uint8_t* res_bin = recs == w.tmp_val ? w.bin_val : w.tmp_val;
     uint8_t* ok_bin = reinterpret_cast<uint8_t*>(w.tmp_idx);
     hipError_t e;
     {
@@ -2590,7 +2593,7 @@ hipError_t launch_stage_finish(const TiledWs& w, StageSession& s, hipStream_t st
         t.scalar = false;                                         // values are materialised in the bins
         t.items = items; t.delta = items + kMaxTiles; t.delta_count = w.item_count;
         t.num_tiles = T;
-        t.bin_lidx = w.bin_lidx; t.bin_val = w.bin_val;
+        t.bin_lidx = w.bin_lidx; t.bin_val = recs;
         t.results = res_bin; t.ok = ok_bin; t.err = a.err;
         t.rts = w.rts; t.nreg = uint32_t(s.nreg); t.rstride = stride;
         t.mixed = mixed ? 1 : 0;

@@ -178,19 +178,29 @@ static hipError_t xstate_wait_streams(XState* x) {
 
 // per-PE header rows of one chunk: [count, MVSI local index or -1, flags (LMR_XHDR_*), scalar
 // bits, chunk count, packed records of the batch, chunk size]
+// ovf (may be null): the sender's overflow count so far; > 0 sets LMR_XHDR_OVERFLOW in every row
 __global__ void k_xhdr(const uint64_t* counts, uint32_t npes, int64_t mvsi_pe, int64_t mvsi_off, int64_t mvsi_n,
-                       int64_t flags, uint64_t sbits, int64_t my_k, int64_t m, int64_t chunk, int64_t* hdr) {
+                       int64_t flags, uint64_t sbits, int64_t my_k, int64_t m, int64_t chunk, int64_t* hdr,
+                       const uint32_t* ovf) {
     const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
     if (p >= npes) return;
     int64_t* r = hdr + uint64_t(p) * LMR_XHDR_WORDS;
     const bool mv = mvsi_pe >= 0 && int64_t(p) == mvsi_pe;
     r[0] = mvsi_pe >= 0 ? (mv ? mvsi_n : 0) : (counts ? int64_t(counts[p]) : 0);
     r[1] = mv ? mvsi_off : -1;
-    r[2] = flags;
+    r[2] = flags | ((ovf && *ovf) ? int64_t(LMR_XHDR_OVERFLOW) : int64_t(0));
     r[3] = int64_t(sbits);
     r[4] = my_k;
     r[5] = m;
     r[6] = chunk;
+}
+
+// batch start: the count-free pack's fill counters and the overflow count (one launch instead of a
+// memset per chunk; the pack's counts kernel leaves the fill counters zero after each chunk)
+__global__ void k_xbegin(uint32_t* fill, uint32_t nfill, uint32_t* ovf) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < nfill) fill[i] = 0;
+    if (i < 2) ovf[i] = 0;
 }
 
 }  // namespace lmr
@@ -583,7 +593,11 @@ lmr_status_t lmr_batch_exchange(lmr_ctx_t* ctx, const lmr_transport_t* tp, const
         hipStreamWaitEvent(x->sx, x->ev_begin, 0) != hipSuccess || hipStreamWaitEvent(x->sa, x->ev_begin, 0) != hipSuccess ||
         hipStreamWaitEvent(x->sh, x->ev_begin, 0) != hipSuccess)
         return LMR_E_HIP;
-    if (free_pack && hipMemsetAsync(x->ovf_count.p, 0, 8, x->sp) != hipSuccess) return LMR_E_HIP;
+    if (free_pack) {
+        hipLaunchKernelGGL(k_xbegin, dim3((npes + 255) / 256), dim3(256), 0, x->sp, x->fill.as<uint32_t>(), npes,
+                           x->ovf_count.as<uint32_t>());
+        if (hipGetLastError() != hipSuccess) return LMR_E_HIP;
+    }
     // header rows on their own stream when the transport allows it (LMR_TRANSPORT_SPLIT_HEADERS;
     // host-buffer transports are host-ordered): chunk j+1's header exchange is posted before
     // chunk j's all-to-all-v and waits only for chunk j+1's pack, so the host's per-chunk read
@@ -682,6 +696,7 @@ lmr_status_t lmr_batch_exchange(lmr_ctx_t* ctx, const lmr_transport_t* tp, const
                 pa.ovf_vals = scalar ? nullptr : x->ovf_vals.as<uint8_t>();
                 pa.ovf_count = x->ovf_count.as<uint32_t>();
                 pa.ovf_cap = m;
+                pa.fill_zeroed = true;                  // (k_xbegin, then each chunk's counts kernel)
                 if (launch_pack_free(pa, x->fill.as<uint32_t>(), uint32_t(region_cap(cnt)), x->sp) != hipSuccess)
                     return LMR_E_HIP;
             } else {
@@ -691,7 +706,8 @@ lmr_status_t lmr_batch_exchange(lmr_ctx_t* ctx, const lmr_transport_t* tp, const
         }
         hipLaunchKernelGGL(k_xhdr, dim3((npes + 255) / 256), dim3(256), 0, x->sp, packed ? x->counts.as<uint64_t>() : nullptr,
                            npes, mvsi && j == 0 ? mvsi_pe : -1, mvsi_off, int64_t(n), my_flags, sbits, int64_t(my_k),
-                           int64_t(m), int64_t(chunk), x->hdr_send[b].as<int64_t>());
+                           int64_t(m), int64_t(chunk), x->hdr_send[b].as<int64_t>(),
+                           free_pack ? x->ovf_count.as<uint32_t>() : nullptr);
         if (hipGetLastError() != hipSuccess) return LMR_E_HIP;
         return hipEventRecord(x->ev_packed[b], x->sp) == hipSuccess ? LMR_OK : LMR_E_HIP;
     };
@@ -706,18 +722,20 @@ lmr_status_t lmr_batch_exchange(lmr_ctx_t* ctx, const lmr_transport_t* tp, const
     };
     // ---- the header all-to-all of chunk j (header stream) and its rows to the host. Receive
     // rows b are read on the device by chunk j-2's staging of fixed regions: that is done first.
-    auto post_header = [&](uint64_t j) -> lmr_status_t {
+    // `to_host`: the rows are copied to pinned host memory for the host to read (chunk 0, every
+    // chunk the host plans from, and the last chunk, whose flags decide the overflow round); with
+    // no host read they stay on the device (fixed-region mode: two copies per chunk saved)
+    auto post_header = [&](uint64_t j, bool to_host) -> lmr_status_t {
         const int b = int(j & 1);
         if (hipStreamWaitEvent(shd, x->ev_packed[b], 0) != hipSuccess) return LMR_E_HIP;
         if (x->recv_used[b] && hipStreamWaitEvent(shd, x->ev_recv_free[b], 0) != hipSuccess) return LMR_E_HIP;
         lmr_status_t e = tp_alltoall(tp, x, x->hdr_send[b].p, x->hdr_recv[b].p, LMR_XHDR_WORDS * 8, shd);
         if (e != LMR_OK) { guard.tp_failed = true; return e; }
         int64_t* hs_ = const_cast<int64_t*>(h_send_rows(b));
-        if (hipMemcpyAsync(hs_, x->hdr_send[b].p, rows * 8, hipMemcpyDeviceToHost, shd) != hipSuccess ||
-            hipMemcpyAsync(hs_ + rows, x->hdr_recv[b].p, rows * 8, hipMemcpyDeviceToHost, shd) != hipSuccess ||
-            hipEventRecord(x->ev_hdr[b], shd) != hipSuccess)
+        if (to_host && (hipMemcpyAsync(hs_, x->hdr_send[b].p, rows * 8, hipMemcpyDeviceToHost, shd) != hipSuccess ||
+                        hipMemcpyAsync(hs_ + rows, x->hdr_recv[b].p, rows * 8, hipMemcpyDeviceToHost, shd) != hipSuccess))
             return LMR_E_HIP;
-        return LMR_OK;
+        return hipEventRecord(x->ev_hdr[b], shd) == hipSuccess ? LMR_OK : LMR_E_HIP;
     };
     // ---- owner side with host counts (apply stream): stage every source's records of receive
     // buffer b (counts cnt[p]; own records from send buffer b at the given offsets when bypassed)
@@ -865,7 +883,7 @@ lmr_status_t lmr_batch_exchange(lmr_ctx_t* ctx, const lmr_transport_t* tp, const
     } else {
     // chunk 0: pack, header exchange; chunk 1's pack (local work) runs during the wait
     if ((st = pack_until(1)) != LMR_OK) return st;
-    if ((st = post_header(0)) != LMR_OK) return st;
+    if ((st = post_header(0, true)) != LMR_OK) return st;
     if ((st = pack_until(std::min<uint64_t>(my_k, 2))) != LMR_OK) return st;
     nchunks = 1;
     for (uint64_t j = 0; j < nchunks; j++) {
@@ -895,7 +913,7 @@ lmr_status_t lmr_batch_exchange(lmr_ctx_t* ctx, const lmr_transport_t* tp, const
         }
         if (split && j + 1 < nchunks) {                 // the next header before this chunk's records
             if ((st = pack_until(j + 2)) != LMR_OK) return st;
-            if ((st = post_header(j + 1)) != LMR_OK) return st;
+            if ((st = post_header(j + 1, !nowait || j + 2 == nchunks)) != LMR_OK) return st;
         }
         const uint64_t lo = chunk_lo(j), hi = chunk_hi(j);
         const uint64_t my_cap = free_pack ? cap_of(m, chunk, j) : 0;
@@ -1014,7 +1032,7 @@ lmr_status_t lmr_batch_exchange(lmr_ctx_t* ctx, const lmr_transport_t* tp, const
         if (j + 1 < nchunks) {
             if (!split) {
                 if ((st = pack_until(j + 2)) != LMR_OK) return st;
-                if ((st = post_header(j + 1)) != LMR_OK) return st;
+                if ((st = post_header(j + 1, !nowait || j + 2 == nchunks)) != LMR_OK) return st;
             }
             if ((st = pack_until(std::min<uint64_t>(j + 3, nchunks))) != LMR_OK) return st;
         }
@@ -1023,7 +1041,16 @@ lmr_status_t lmr_batch_exchange(lmr_ctx_t* ctx, const lmr_transport_t* tp, const
     // ---- overflow round (some PE packed fixed regions): the records that did not fit their
     // region, from every FIXED sender's overflow list, packed by the counted pack and exchanged
     // with exact counts (one more header exchange, read by the host once per batch)
-    if (any_fixed) {
+    // (skipped when no PE's last-chunk rows carry LMR_XHDR_OVERFLOW: every PE reads the same rows,
+    // so every PE skips it alike)
+    bool any_ovf = false;
+    if (any_fixed && !push) {
+        const int bl = int((nchunks - 1) & 1);
+        if (hipEventSynchronize(x->ev_hdr[bl]) != hipSuccess) return LMR_E_HIP;
+        const int64_t* h_last = h_recv_rows(bl);
+        for (uint32_t p = 0; p < npes; p++) any_ovf = any_ovf || (h_last[p * LMR_XHDR_WORDS + 2] & LMR_XHDR_OVERFLOW);
+    }
+    if (any_fixed && (push || any_ovf)) {
         const uint64_t J = nchunks;
         const int b = int(J & 1);
         uint64_t novf = 0;
@@ -1048,9 +1075,9 @@ lmr_status_t lmr_batch_exchange(lmr_ctx_t* ctx, const lmr_transport_t* tp, const
         hipLaunchKernelGGL(k_xhdr, dim3((npes + 255) / 256), dim3(256), 0, x->sp,
                            novf > 0 ? x->counts.as<uint64_t>() : nullptr, npes, int64_t(-1), int64_t(0), int64_t(0),
                            int64_t(scalar ? LMR_XHDR_SCALAR : 0), sbits, int64_t(1), int64_t(novf), int64_t(novf),
-                           x->hdr_send[b].as<int64_t>());
+                           x->hdr_send[b].as<int64_t>(), nullptr);
         if (hipGetLastError() != hipSuccess || hipEventRecord(x->ev_packed[b], x->sp) != hipSuccess) return LMR_E_HIP;
-        if ((st = post_header(J)) != LMR_OK) return st;
+        if ((st = post_header(J, true)) != LMR_OK) return st;
         if (hipEventSynchronize(x->ev_hdr[b]) != hipSuccess) return LMR_E_HIP;
         const int64_t* h_send = h_send_rows(b);
         const int64_t* h_recv = h_recv_rows(b);

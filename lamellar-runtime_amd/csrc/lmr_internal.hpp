@@ -237,7 +237,7 @@ struct StageSession {
     bool switched = false;  // the op changed with records staged (lmr_stage_op): later phases counted
     bool wide = false;      // counted regions partitioned one-level into 128 KiB tiles (wide_applies)
     bool wide_set = false;  //   decided at the session's first partition
-    bool wpack = false;     // wide, 1/2/4-byte elements: packed uint2 records (TileArgs::packed)
+    bool wpack = false;     // wide: packed records (TileArgs::packed: uint2 for 1/2/4-byte values, uint4 for 8-byte)
     uint64_t wcnt = 0;      // wide: count entries in use
     uint64_t wrh = 0;       // wide: round-count entries (u16) in use
     StageRegion reg[kMaxRegions];
@@ -267,6 +267,7 @@ hipError_t launch_stage_finish(const TiledWs& w, StageSession& s, hipStream_t st
 // returning regions' results from binned order back to arrival order after the tile sweep
 bool wide_applies(int dtype, uint64_t shard_len, uint64_t cap);
 hipError_t wide_partition(const TiledWs& w, StageSession& s, hipStream_t st);
+uint8_t* wide_records(const TiledWs& w, const StageSession& s);
 hipError_t wide_unpartition(const TiledWs& w, const StageSession& s, const uint8_t* res_bin, const uint8_t* ok_bin,
                             uint32_t num_tiles, hipStream_t st);
 
@@ -328,6 +329,9 @@ struct PackArgs {
     // the peer transport's IPC-mapped receive regions) instead of out_idx / out_vals + i * cap
     uint8_t* const* out_idx_tab = nullptr;
     uint8_t* const* out_vals_tab = nullptr;
+    // count-free pack only: `fill` is zero on entry (no memset) and is left zero (the counts kernel
+    // clears it after copying it to dest_counts): the exchange's per-chunk pack
+    bool fill_zeroed = false;
 };
 hipError_t launch_pack(const PackArgs& a, uint32_t* counts, uint32_t* partials, uint32_t* total,
                        hipStream_t s);

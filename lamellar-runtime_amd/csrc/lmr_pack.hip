@@ -389,9 +389,12 @@ __global__ __launch_bounds__(1024) void k_pack_stage(PackK p) {
     }
 }
 
-__global__ void k_fill_counts(const uint32_t* fill, uint32_t npes, uint64_t* dest_counts) {
+__global__ void k_fill_counts(uint32_t* fill, uint32_t npes, uint64_t* dest_counts, int clear) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < npes) dest_counts[i] = fill[i];
+    if (i < npes) {
+        dest_counts[i] = fill[i];
+        if (clear) fill[i] = 0;             // zero again for the next pack (PackArgs::fill_zeroed)
+    }
 }
 
 __global__ void k_dest_offsets(const uint32_t* counts, uint32_t npes, uint32_t G, const uint32_t* total,
@@ -513,8 +516,10 @@ hipError_t launch_pack_free(const PackArgs& a, uint32_t* fill, uint32_t cap, hip
     const bool pairs = pairs_on && a.vals && a.val_bytes == 8 &&
                        ((reinterpret_cast<uintptr_t>(a.gidx) | reinterpret_cast<uintptr_t>(a.vals)) & 15) == 0;
     ProfScope ps(a.prof, LMR_STAGE_PACK, s, a.n);
-    hipError_t e = hipMemsetAsync(fill, 0, size_t(npes) * 4, s);
-    if (e != hipSuccess) return e;
+    if (!a.fill_zeroed) {
+        const hipError_t e = hipMemsetAsync(fill, 0, size_t(npes) * 4, s);
+        if (e != hipSuccess) return e;
+    }
     if (a.n > 0) {
         const int mode = layout_map_mode(a.layout);
         const int vbk = a.vals ? int(a.val_bytes) : 1;
@@ -535,7 +540,8 @@ hipError_t launch_pack_free(const PackArgs& a, uint32_t* fill, uint32_t cap, hip
                                    p);
         });
     }
-    hipLaunchKernelGGL(k_fill_counts, dim3((npes + 255) / 256), dim3(256), 0, s, fill, npes, a.dest_counts);
+    hipLaunchKernelGGL(k_fill_counts, dim3((npes + 255) / 256), dim3(256), 0, s, fill, npes, a.dest_counts,
+                       a.fill_zeroed ? 1 : 0);
     return hipGetLastError();
 }
 

@@ -233,6 +233,23 @@ __global__ __launch_bounds__(1024, 8) void k_tile_owner(TileArgs a) {
             }
             continue;
         }
+    } else {
+        // packed 16-B records of 8-byte values {index, 0, value}: one 16-B load per record
+        if (a.packed) {
+            const uint4* rec = reinterpret_cast<const uint4*>(a.bin_val);
+            constexpr uint32_t kPk = 4;
+            for (uint32_t b0 = lo; b0 < hi; b0 += kPk * 1024u) {
+                uint4 x[kPk];
+#pragma unroll
+                for (uint32_t k = 0; k < kPk; k++) x[k] = rec[min(b0 + threadIdx.x + k * 1024u, hi - 1)];
+#pragma unroll
+                for (uint32_t k = 0; k < kPk; k++) {
+                    const uint32_t r = b0 + threadIdx.x + k * 1024u;
+                    if (r < hi) apply_one(r, x[k].x, from_bits<T>(U(uint64_t(x[k].z) | (uint64_t(x[k].w) << 32))));
+                }
+            }
+            continue;
+        }
     }
     if constexpr (sizeof(T) == 4) {
         // 4-byte values: 4 consecutive records per thread and iteration, one 8-B load of their
@@ -373,13 +390,17 @@ __global__ __launch_bounds__(1024) void k_tile_delta(TileArgs a) {
 #pragma unroll
         for (int k = 0; k < int(kSplit / 1024); k++) {
             const uint32_t r = min(w.lo + threadIdx.x + uint32_t(k) * 1024u, w.hi - 1);
-            if constexpr (sizeof(T) <= 4) {
-                if (a.packed) {                                 // the wide path's packed records
+            if (a.packed) {                                     // the wide path's packed records
+                if constexpr (sizeof(T) <= 4) {
                     const uint2 x = reinterpret_cast<const uint2*>(a.bin_val)[r];
                     lk[k] = uint16_t(x.x);
                     vk[k] = from_bits<T>(U(x.y));
-                    continue;
+                } else {
+                    const uint4 x = reinterpret_cast<const uint4*>(a.bin_val)[r];
+                    lk[k] = uint16_t(x.x);
+                    vk[k] = from_bits<T>(U(uint64_t(x.z) | (uint64_t(x.w) << 32)));
                 }
+                continue;
             }
             lk[k] = bin_lidx[r];
             vk[k] = a.scalar ? sv : bin_val[r];

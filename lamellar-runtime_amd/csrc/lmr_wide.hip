@@ -267,7 +267,10 @@ __global__ __launch_bounds__(1024) void k_wide_stage(WStageTable t) {
         for (uint32_t q = threadIdx.x; q < tot; q += kWT) {
             const uint32_t x = s_b[q];
             const uint32_t dst = cursor[x] + (q - base[x]);
-            if constexpr (PK) {
+            if constexpr (PK && VB == 8) {
+                const uint64_t v = uint64_t(s_v[q]);
+                reinterpret_cast<uint4*>(t.bin_val)[dst] = make_uint4(s_l[q], 0u, uint32_t(v), uint32_t(v >> 32));
+            } else if constexpr (PK) {
                 reinterpret_cast<uint2*>(t.bin_val)[dst] = make_uint2(s_l[q], uint32_t(s_v[q]));
             } else {
                 t.bin_lidx[dst] = s_l[q];
@@ -413,9 +416,11 @@ hipError_t wdispatch_vb(int vb, F&& f) {
 
 // LMR_WIDE=0: no wide sessions; LMR_WIDE4=0: none below 8-byte elements. Read per session, so a
 // process (a test) can switch them.
-// LMR_WIDE_PACK=0: the 1/2/4-byte wide path writes split offset / value arrays (A/B)
-bool wide_pack_env() {
+// packed records: 1/2/4-byte values by default (LMR_WIDE_PACK=0: split offset / value arrays), 8-byte
+// values on request (LMR_WIDE_PACK=8 or =1: 16-B records {index, 0, value} in the temp array)
+bool wide_pack_env(int vb) {
     const char* e = getenv("LMR_WIDE_PACK");
+    if (vb == 8) return e && *e && (atoi(e) == 8 || atoi(e) == 1) && e[0] != '4';
     return !(e && *e && atoi(e) == 0);
 }
 // LMR_WIDE4=0 / 1: no / wide sessions below 8-byte elements (default kWide4Default)
@@ -446,6 +451,12 @@ uint32_t wide_blocks(uint64_t n) {
 
 }  // namespace
 
+// the wide session's binned records: bin_val (split arrays, or packed 8-B records), or the temp
+// array for packed 16-B records of 8-byte values (cap x 16 B; the results then go to bin_val)
+uint8_t* wide_records(const TiledWs& w, const StageSession& s) {
+    return s.wpack && dtype_bytes(s.dtype) == 8 ? w.tmp_val : w.bin_val;
+}
+
 bool wide_applies(int dtype, uint64_t shard_len, uint64_t cap) {
     const int vb = dtype_bytes(dtype);
     if (vb == 0 || !wide_env(vb)) return false;
@@ -461,7 +472,7 @@ bool wide_applies(int dtype, uint64_t shard_len, uint64_t cap) {
 
 hipError_t wide_partition(const TiledWs& w, StageSession& s, hipStream_t st) {
     const int vb = dtype_bytes(s.dtype);
-    if (s.parted == 0) s.wpack = vb <= 4 && wide_pack_env();     // one record layout per session
+    if (s.parted == 0) s.wpack = wide_pack_env(vb);              // one record layout per session
     const int shift = wide_shift(vb);
     const uint32_t R = wide_round(vb);
     while (s.parted < s.nreg) {
@@ -518,7 +529,7 @@ hipError_t wide_partition(const TiledWs& w, StageSession& s, hipStream_t st) {
         ct.shard_len = sc.shard_len = a0.shard_len;
         ct.err = a0.err;
         sc.bin_lidx = w.bin_lidx;
-        sc.bin_val = w.bin_val;
+        sc.bin_val = wide_records(w, s);
         ws.gbase = gbase;
         ws.total = w.total;
         hipError_t e;
@@ -544,11 +555,9 @@ hipError_t wide_partition(const TiledWs& w, StageSession& s, hipStream_t st) {
             e = wdispatch_iw(iw, [&](auto iwt) {
                 return wdispatch_vb(vb, [&](auto vbt) {
                     constexpr int IW = decltype(iwt)::value, VB = decltype(vbt)::value;
-                    if constexpr (VB <= 4) {
-                        if (s.wpack) {
-                            hipLaunchKernelGGL((k_wide_stage<IW, VB, true>), dim3(blocks), dim3(kWT), 0, st, sc);
-                            return hipGetLastError();
-                        }
+                    if (s.wpack) {
+                        hipLaunchKernelGGL((k_wide_stage<IW, VB, true>), dim3(blocks), dim3(kWT), 0, st, sc);
+                        return hipGetLastError();
                     }
                     hipLaunchKernelGGL((k_wide_stage<IW, VB, false>), dim3(blocks), dim3(kWT), 0, st, sc);
                     return hipGetLastError();

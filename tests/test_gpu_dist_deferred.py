@@ -184,7 +184,8 @@ ai = rng.integers(0, n_len, 600000).astype(np.uint64)
 av = rng.integers(0, 2**63, ai.size, dtype=np.uint64)
 a.batch_add(ai, av).spawn()                 # exchange left open: a deferred session in the workspace
 assert k._xdeferred is not None
-# a Rust caller on the raw ABI, with no Python flush in between: a tiled apply on another shard ...
+# a Rust caller on the raw ABI, with no Python flush in between: the staged-session calls are refused
+# while the session is open ...
 m = 1 << 20
 b = torch.zeros(n_len, dtype=torch.int64, device=k.device)
 bi = rng.integers(0, n_len, m).astype(np.uint64)
@@ -192,12 +193,13 @@ bv = rng.integers(0, 2**63, m, dtype=np.uint64)
 ti = torch.from_numpy(bi.view(np.int64)).to(k.device)
 tv = torch.from_numpy(bv.view(np.int64)).to(k.device)
 d = k._desc(b, n_len, 1, lam.dtype_of("u64"), int(lam.ArrayOpCmd.Add))
+assert lib.lmr_stage_begin(k.ctx, ctypes.byref(d)) == 1
+assert lib.lmr_stage_finish(k.ctx, k.stream()) == 1
+# ... and a tiled apply on another shard applies the open session first (stream order)
 st = lib.lmr_apply_soa(k.ctx, ctypes.byref(d), ti.data_ptr(), 8, tv.data_ptr(), None, m, None, None, k.stream())
 assert st == 0, st
-# ... and the staged-session calls are refused until the flush
-assert lib.lmr_stage_begin(k.ctx, ctypes.byref(d)) == 1
-k._xdeferred = None                         # (the apply above applied the open session already)
-assert lib.lmr_exchange_flush(k.ctx, k.stream()) == 0
+k._xdeferred = None                         # (the apply above applied the open session)
+assert lib.lmr_exchange_flush(k.ctx, k.stream()) == 0          # nothing left open: a no-op
 assert lib.lmr_stage_begin(k.ctx, ctypes.byref(d)) == 0
 assert lib.lmr_stage_finish(k.ctx, k.stream()) == 0
 torch.cuda.synchronize()
