@@ -317,6 +317,7 @@ namespace lmr {
 
 bool stage_session_free(const lmr_ctx* ctx) { return ctx->stage && ctx->stage->open && ctx->stage->s.free; }
 bool stage_session_open(const lmr_ctx* ctx) { return ctx->stage && ctx->stage->open; }
+bool stage_session_empty(const lmr_ctx* ctx) { return !stage_session_open(ctx) || ctx->stage->s.nreg == 0; }
 bool stage_session_of(const lmr_ctx* ctx, const lmr_apply_desc_t& d) {
     if (!stage_session_open(ctx)) return false;
     const lmr_apply_desc_t& c = ctx->stage->desc;
@@ -420,6 +421,11 @@ lmr_status_t lmr_ctx_destroy(lmr_ctx_t* ctx) {
 lmr_status_t lmr_ctx_reserve(lmr_ctx_t* ctx, uint64_t max_records) {
     if (!ctx) return LMR_E_INVALID;
     if (max_records > max_rec_cap()) max_records = max_rec_cap();
+    // a deferred exchange session lives in the workspace: applied first (the free below waits for it)
+    if (ctx->xdefer_open) {
+        const lmr_status_t st = lmr_exchange_flush(ctx, nullptr);
+        if (st != LMR_OK) return st;
+    }
     if (ctx->stage && ctx->stage->s.nreg > 0) return LMR_E_INVALID;   // staged records live in the workspace
     (void)hipSetDevice(ctx->device);
     if (ctx->ws_alloc) (void)hipFree(ctx->ws_alloc);

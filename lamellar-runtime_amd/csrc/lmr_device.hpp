@@ -539,6 +539,16 @@ struct BufStream {
     }
 };
 
+// ---------------------------------------------------------------- global address space
+// A pointer read from memory (a device table, LDS) is a generic pointer: its loads and stores
+// become flat_* instructions, which count on the LDS counter too, so the next LDS access waits
+// for them (a write-out loop's stores, a prefetch's loads). For memory known to be global (device
+// allocations, IPC-mapped peer memory) the cast makes them global_* instructions.
+template <typename T>
+__device__ __forceinline__ __attribute__((address_space(1))) T* as_global(T* p) {
+    return (__attribute__((address_space(1))) T*)p;
+}
+
 // ---------------------------------------------------------------- index load
 template <int IW> struct idx_t;
 template <> struct idx_t<1> { using I = uint8_t; };

@@ -22,6 +22,7 @@
 //                 each chunk's results -> lmr_scatter_results into input order.
 // Chunk j's exchange overlaps chunk j-1's staging on the apply stream; receive
 // buffers are double-buffered between the two streams.
+#include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 #include <vector>
@@ -107,6 +108,11 @@ struct XState {
     DevBuf recv_idx[2], recv_vals[2];
     std::vector<DevBuf> pos, res, rok;   // per chunk (returning ops)
     DevBuf ovf_idx, ovf_vals, ovf_count;  // count-free pack: records past their region (global index, value)
+    // the peer push's bucketed mode (lmr_bucket.hip): the sender's (owner, bucket) fill counters and
+    // per-owner totals, the owner's session of fixed tile regions and its tile fills
+    DevBuf bfill, btot, tfill;
+    BucketSession bs;
+    bool tfill_zero = false;             // tfill is zero as the apply stream will see it
     DevBuf back, back_ok;
     HostBuf h_hdr;                       // per chunk parity: [send rows | recv rows] int64
     HostBuf h_send, h_recv;              // host-buffer transports
@@ -127,7 +133,7 @@ void xstate_free(XState* x) {
     for (DevBuf* b : {&x->hdr_send[0], &x->hdr_send[1], &x->hdr_recv[0], &x->hdr_recv[1], &x->counts, &x->offsets,
                       &x->one_idx, &x->fill, &x->send_idx[0], &x->send_idx[1], &x->send_vals[0], &x->send_vals[1],
                       &x->recv_idx[0], &x->recv_idx[1], &x->recv_vals[0], &x->recv_vals[1], &x->back, &x->back_ok,
-                      &x->ovf_idx, &x->ovf_vals, &x->ovf_count})
+                      &x->ovf_idx, &x->ovf_vals, &x->ovf_count, &x->bfill, &x->btot, &x->tfill})
         b->release();
     for (auto* v : {&x->pos, &x->res, &x->rok})
         for (DevBuf& b : *v) b.release();
@@ -195,12 +201,23 @@ __global__ void k_xhdr(const uint64_t* counts, uint32_t npes, int64_t mvsi_pe, i
     r[6] = chunk;
 }
 
-// batch start: the count-free pack's fill counters and the overflow count (one launch instead of a
-// memset per chunk; the pack's counts kernel leaves the fill counters zero after each chunk)
-__global__ void k_xbegin(uint32_t* fill, uint32_t nfill, uint32_t* ovf) {
+// batch start: the count-free pack's fill counters (and the bucketed pack's), and the overflow count
+// (one launch instead of a memset per chunk; the packs leave their fill counters zero after each chunk)
+__global__ void k_xbegin(uint32_t* fill, uint32_t nfill, uint32_t* bfill, uint32_t nbfill, uint32_t* ovf) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i < nfill) fill[i] = 0;
+    if (i < nbfill) bfill[i] = 0;
     if (i < 2) ovf[i] = 0;
+}
+
+// the bucketed session's one tile sweep (nothing when none is open)
+hipError_t bucket_sweep(lmr_ctx* ctx, XState* x, hipStream_t s) {
+    if (!x->bs.open) return hipSuccess;
+    TiledWs w = carve_tiled_ws(ctx->ws, ctx->rec_cap);
+    w.side = SideLane{ctx->side, ctx->side_fork, ctx->side_join};
+    const hipError_t e = launch_bucket_sweep(x->bs, w, s);   // (its plan kernel zeroes the tile fills)
+    x->tfill_zero = e == hipSuccess;
+    return e;
 }
 
 }  // namespace lmr
@@ -210,6 +227,14 @@ using namespace lmr;
 namespace {
 
 inline lmr_status_t hs(hipError_t e) { return e == hipSuccess ? LMR_OK : LMR_E_HIP; }
+
+// LMR_XDEBUG=1: the exchange names the line of a failing HIP step on stderr (diagnostics only)
+lmr_status_t xfail(int line) {
+    static const bool dbg = getenv("LMR_XDEBUG") != nullptr;
+    if (dbg) fprintf(stderr, "[lmr_exchange] HIP failure at lmr_exchange.hip:%d (%s)\n", line,
+                     hipGetErrorString(hipGetLastError()));
+    return LMR_E_HIP;
+}
 
 // Transport calls; host-buffer transports get pinned staging around the callback.
 lmr_status_t tp_alltoall(const lmr_transport_t* tp, XState* x, const void* send, void* recv, uint64_t bytes,
@@ -382,6 +407,13 @@ bool valid_layout(const lmr_layout_t* L) {
     return L && L->num_pes > 0 && L->my_pe < L->num_pes && L->distribution <= 1 && L->orig_elem_per_pe > 0;
 }
 
+// the peer push's bucketed mode (LAMELLAR_EXCHANGE_BUCKETS=1; every PE must set it alike, the
+// handshake falls back to the plain push otherwise)
+bool bucket_mode_enabled() {
+    const char* e = getenv("LAMELLAR_EXCHANGE_BUCKETS");
+    return e && e[0] == '1';
+}
+
 bool free_pack_enabled() {
     const char* e = getenv("LAMELLAR_FREE_PACK");
     return !(e && e[0] == '0');
@@ -536,7 +568,7 @@ lmr_status_t lmr_batch_exchange(lmr_ctx_t* ctx, const lmr_transport_t* tp, const
     (void)hipSetDevice(ctx->device);
     if (!ctx->xch) ctx->xch = new XState();
     XState* x = ctx->xch;
-    if (xstate_init(x) != hipSuccess) return LMR_E_HIP;
+    if (xstate_init(x) != hipSuccess) return xfail(__LINE__);
     hipStream_t s0 = reinterpret_cast<hipStream_t>(stream);
     // --- shape on the sender side
     int64_t mvsi_pe = -1, mvsi_off = 0;
@@ -548,8 +580,8 @@ lmr_status_t lmr_batch_exchange(lmr_ctx_t* ctx, const lmr_transport_t* tp, const
         mvsi_pe = int64_t(pe);
         mvsi_off = int64_t(off);
     } else if (n > 0 && i_len == 1) {                  // one index (1 x 1): a one-record batch
-        if (x->one_idx.need(8, x) != hipSuccess) return LMR_E_HIP;
-        if (hipMemcpyAsync(x->one_idx.p, &h_index, 8, hipMemcpyHostToDevice, s0) != hipSuccess) return LMR_E_HIP;
+        if (x->one_idx.need(8, x) != hipSuccess) return xfail(__LINE__);
+        if (hipMemcpyAsync(x->one_idx.p, &h_index, 8, hipMemcpyHostToDevice, s0) != hipSuccess) return xfail(__LINE__);
         gidx = x->one_idx.as<uint64_t>();
     }
     const uint64_t chunk = exchange_chunk();
@@ -558,10 +590,10 @@ lmr_status_t lmr_batch_exchange(lmr_ctx_t* ctx, const lmr_transport_t* tp, const
     const size_t rows = size_t(npes) * LMR_XHDR_WORDS;
     for (int b = 0; b < 2; b++)
         if (x->hdr_send[b].need(rows * 8, x) != hipSuccess || x->hdr_recv[b].need(rows * 8, x) != hipSuccess)
-            return LMR_E_HIP;
+            return xfail(__LINE__);
     if (x->counts.need(size_t(npes) * 8, x) != hipSuccess || x->offsets.need(size_t(npes + 1) * 8, x) != hipSuccess ||
         x->h_hdr.need(4 * rows * 8) != hipSuccess)
-        return LMR_E_HIP;
+        return xfail(__LINE__);
     const uint64_t cmax = std::min<uint64_t>(m, chunk);
     // nothing returned: the count-free pack (fixed per-destination regions, no count pass);
     // records past a destination's region go to an overflow list, exchanged after the last chunk
@@ -579,25 +611,20 @@ lmr_status_t lmr_batch_exchange(lmr_ctx_t* ctx, const lmr_transport_t* tp, const
     };
     const uint64_t send_recs = free_pack ? std::max<uint64_t>(cmax, uint64_t(npes) * region_cap(cmax)) : cmax;
     if (free_pack && (send_recs > 0xFFFFFFFFull || x->fill.need(size_t(npes) * 4 + 8, x) != hipSuccess))
-        return LMR_E_HIP;
+        return xfail(__LINE__);
     if (free_pack && (x->ovf_idx.need(m * 8 + 16, x) != hipSuccess ||
                       x->ovf_vals.need((scalar ? 0 : m * eb) + 16, x) != hipSuccess ||
                       x->ovf_count.need(16, x) != hipSuccess))
-        return LMR_E_HIP;
+        return xfail(__LINE__);
     for (int b = 0; b < 2; b++)
         if (x->send_idx[b].need(send_recs * iw + 8, x) != hipSuccess ||
             x->send_vals[b].need(send_recs * eb + 8, x) != hipSuccess)
-            return LMR_E_HIP;
+            return xfail(__LINE__);
     // --- the internal streams start after everything already on the caller's stream
     if (hipEventRecord(x->ev_begin, s0) != hipSuccess || hipStreamWaitEvent(x->sp, x->ev_begin, 0) != hipSuccess ||
         hipStreamWaitEvent(x->sx, x->ev_begin, 0) != hipSuccess || hipStreamWaitEvent(x->sa, x->ev_begin, 0) != hipSuccess ||
         hipStreamWaitEvent(x->sh, x->ev_begin, 0) != hipSuccess)
-        return LMR_E_HIP;
-    if (free_pack) {
-        hipLaunchKernelGGL(k_xbegin, dim3((npes + 255) / 256), dim3(256), 0, x->sp, x->fill.as<uint32_t>(), npes,
-                           x->ovf_count.as<uint32_t>());
-        if (hipGetLastError() != hipSuccess) return LMR_E_HIP;
-    }
+        return xfail(__LINE__);
     // header rows on their own stream when the transport allows it (LMR_TRANSPORT_SPLIT_HEADERS;
     // host-buffer transports are host-ordered): chunk j+1's header exchange is posted before
     // chunk j's all-to-all-v and waits only for chunk j+1's pack, so the host's per-chunk read
@@ -610,11 +637,15 @@ lmr_status_t lmr_batch_exchange(lmr_ctx_t* ctx, const lmr_transport_t* tp, const
     // the same op on the same shard and stages count-free; otherwise it is applied first
     lmr_status_t st = LMR_OK;
     bool cont = false;
-    const bool was_open = ctx->xdefer_open && stage_session_open(ctx);
+    const bool was_open = ctx->xdefer_open && (stage_session_open(ctx) || x->bs.open);
     ctx->xdefer_open = false;                   // (the staged-session calls refuse while it is set)
     if (was_open) {
         cont = !returning && !ordered && stage_session_free(ctx) && stage_session_of(ctx, *desc);
-        if (!cont && (st = lmr_stage_finish(ctx, reinterpret_cast<lmr_stream_t>(x->sa))) != LMR_OK) return st;
+        if (!cont) {
+            if (bucket_sweep(ctx, x, x->sa) != hipSuccess) return xfail(__LINE__);
+            if (stage_session_open(ctx) && (st = lmr_stage_finish(ctx, reinterpret_cast<lmr_stream_t>(x->sa))) != LMR_OK)
+                return st;
+        }
     }
     if (!cont && (st = lmr_stage_begin(ctx, desc)) != LMR_OK) return st;
     // fixed-region mode: a FIXED sender's regions go whole to DEVCOUNT receivers (their count-free
@@ -623,6 +654,34 @@ lmr_status_t lmr_batch_exchange(lmr_ctx_t* ctx, const lmr_transport_t* tp, const
     const bool devcount = fixed_mode_enabled() && !returning && !ordered && stage_session_free(ctx);
     const int64_t my_flags = (scalar ? LMR_XHDR_SCALAR : 0) | (ordered ? LMR_XHDR_ORDERED : 0) |
                              (free_pack ? LMR_XHDR_FIXED : 0) | (devcount ? LMR_XHDR_DEVCOUNT : 0);
+    // the peer push's bucketed mode, as far as this PE can take it: the layout's buckets fit the
+    // pack's keys, a bucket slice of the receive region holds this PE's chunk with headroom, and the
+    // workspace holds the owner's tile regions
+    PeerTransport* peer = peer_of(tp);
+    uint32_t bC = 0, bcap = 0;
+    int bshift = 0;
+    bool my_bucket = false;
+    if (peer && free_pack && devcount && bucket_mode_enabled() && ctx->ws && ctx->rec_cap > 0 && npes <= kBucketMaxSrc &&
+        desc->shard_len > 0 && bucket_geometry(*layout, int(desc->dtype), bC, bshift)) {
+        bcap = bucket_slice_cap(peer_region_records(peer), bC, eb);
+        const uint64_t per = (cmax + uint64_t(npes) * bC - 1) / (uint64_t(npes) * bC);
+        const int ts = tile_shift(int(desc->dtype));
+        const uint64_t my_tiles = (desc->shard_len + (uint64_t(1) << ts) - 1) >> ts;
+        my_bucket = bcap > 0 && uint64_t(bcap) >= per + per / 16 + 256 && my_tiles <= uint64_t(bC) * 128;
+    }
+    if (my_bucket && (x->bfill.need(size_t(npes) * bC * 4 + 8, x) != hipSuccess ||
+                      x->btot.need(size_t(npes) * 4 + 8, x) != hipSuccess))
+        return xfail(__LINE__);
+    if (my_bucket && !x->tfill.p) {
+        if (x->tfill.need(size_t(kMaxTiles) * 4 + 8, x) != hipSuccess) return xfail(__LINE__);
+        x->tfill_zero = false;
+    }
+    if (free_pack) {
+        const uint32_t nb = my_bucket ? npes * bC : 0u, nt = std::max(npes, nb);
+        hipLaunchKernelGGL(k_xbegin, dim3((nt + 255) / 256), dim3(256), 0, x->sp, x->fill.as<uint32_t>(), npes,
+                           x->bfill.as<uint32_t>(), nb, x->ovf_count.as<uint32_t>());
+        if (hipGetLastError() != hipSuccess) return xfail(__LINE__);
+    }
     // a failed exchange closes the session (its staged records are dropped) so the context
     // stays usable; the work already enqueued on the internal streams drains first (after a
     // transport failure the transport is aborted first: peers may never post their halves)
@@ -636,6 +695,9 @@ lmr_status_t lmr_batch_exchange(lmr_ctx_t* ctx, const lmr_transport_t* tp, const
             if (tp_failed) transport_abort(t);
             (void)c->xch->drain();
             stage_abort(c->stage);
+            c->xch->bs.open = false;               // (its tile fills are zeroed before the next session)
+            c->xch->bs.staged = 0;
+            c->xch->tfill_zero = false;
         }
     } guard{ctx, tp};
     struct ChunkRec {
@@ -663,8 +725,8 @@ lmr_status_t lmr_batch_exchange(lmr_ctx_t* ctx, const lmr_transport_t* tp, const
     // send buffer b and its header rows: chunk j-2's all-to-all-v (and, for own records staged
     // from the send buffer or counted from the header rows, chunk j-2's staging) are done with them
     auto wait_send_slot = [&](int b) -> lmr_status_t {
-        if (x->send_used[b] && hipStreamWaitEvent(x->sp, x->ev_send_free[b], 0) != hipSuccess) return LMR_E_HIP;
-        if (x->recv_used[b] && hipStreamWaitEvent(x->sp, x->ev_recv_free[b], 0) != hipSuccess) return LMR_E_HIP;
+        if (x->send_used[b] && hipStreamWaitEvent(x->sp, x->ev_send_free[b], 0) != hipSuccess) return xfail(__LINE__);
+        if (x->recv_used[b] && hipStreamWaitEvent(x->sp, x->ev_recv_free[b], 0) != hipSuccess) return xfail(__LINE__);
         return LMR_OK;
     };
     auto pack_chunk = [&](uint64_t j) -> lmr_status_t {
@@ -675,7 +737,7 @@ lmr_status_t lmr_batch_exchange(lmr_ctx_t* ctx, const lmr_transport_t* tp, const
         if (e != LMR_OK) return e;
         if (returning && x->pos.size() <= j) x->pos.resize(j + 1);
         if (packed) {
-            if (returning && x->pos[j].need(cnt * 4 + 8, x) != hipSuccess) return LMR_E_HIP;
+            if (returning && x->pos[j].need(cnt * 4 + 8, x) != hipSuccess) return xfail(__LINE__);
             if (free_pack) {
                 PackArgs pa;
                 pa.layout = *layout;
@@ -698,7 +760,7 @@ lmr_status_t lmr_batch_exchange(lmr_ctx_t* ctx, const lmr_transport_t* tp, const
                 pa.ovf_cap = m;
                 pa.fill_zeroed = true;                  // (k_xbegin, then each chunk's counts kernel)
                 if (launch_pack_free(pa, x->fill.as<uint32_t>(), uint32_t(region_cap(cnt)), x->sp) != hipSuccess)
-                    return LMR_E_HIP;
+                    return xfail(__LINE__);
             } else {
                 e = counted_pack(j);
                 if (e != LMR_OK) return e;
@@ -708,7 +770,7 @@ lmr_status_t lmr_batch_exchange(lmr_ctx_t* ctx, const lmr_transport_t* tp, const
                            npes, mvsi && j == 0 ? mvsi_pe : -1, mvsi_off, int64_t(n), my_flags, sbits, int64_t(my_k),
                            int64_t(m), int64_t(chunk), x->hdr_send[b].as<int64_t>(),
                            free_pack ? x->ovf_count.as<uint32_t>() : nullptr);
-        if (hipGetLastError() != hipSuccess) return LMR_E_HIP;
+        if (hipGetLastError() != hipSuccess) return xfail(__LINE__);
         return hipEventRecord(x->ev_packed[b], x->sp) == hipSuccess ? LMR_OK : LMR_E_HIP;
     };
     uint64_t packed_upto = 0;                          // chunks [0, packed_upto) are enqueued on sp
@@ -727,18 +789,19 @@ lmr_status_t lmr_batch_exchange(lmr_ctx_t* ctx, const lmr_transport_t* tp, const
     // no host read they stay on the device (fixed-region mode: two copies per chunk saved)
     auto post_header = [&](uint64_t j, bool to_host) -> lmr_status_t {
         const int b = int(j & 1);
-        if (hipStreamWaitEvent(shd, x->ev_packed[b], 0) != hipSuccess) return LMR_E_HIP;
-        if (x->recv_used[b] && hipStreamWaitEvent(shd, x->ev_recv_free[b], 0) != hipSuccess) return LMR_E_HIP;
+        if (hipStreamWaitEvent(shd, x->ev_packed[b], 0) != hipSuccess) return xfail(__LINE__);
+        if (x->recv_used[b] && hipStreamWaitEvent(shd, x->ev_recv_free[b], 0) != hipSuccess) return xfail(__LINE__);
         lmr_status_t e = tp_alltoall(tp, x, x->hdr_send[b].p, x->hdr_recv[b].p, LMR_XHDR_WORDS * 8, shd);
         if (e != LMR_OK) { guard.tp_failed = true; return e; }
         int64_t* hs_ = const_cast<int64_t*>(h_send_rows(b));
         if (to_host && (hipMemcpyAsync(hs_, x->hdr_send[b].p, rows * 8, hipMemcpyDeviceToHost, shd) != hipSuccess ||
                         hipMemcpyAsync(hs_ + rows, x->hdr_recv[b].p, rows * 8, hipMemcpyDeviceToHost, shd) != hipSuccess))
-            return LMR_E_HIP;
+            return xfail(__LINE__);
         return hipEventRecord(x->ev_hdr[b], shd) == hipSuccess ? LMR_OK : LMR_E_HIP;
     };
     // ---- owner side with host counts (apply stream): stage every source's records of receive
     // buffer b (counts cnt[p]; own records from send buffer b at the given offsets when bypassed)
+    bool bucketed = false;                       // (the peer push's bucketed mode, agreed at the handshake)
     auto stage_host = [&](int b, const int64_t* h_recv, const std::vector<uint64_t>& cnt, uint64_t self_io,
                           uint64_t self_vo, const uint8_t* send_vals, uint64_t j) -> lmr_status_t {
         uint64_t io = 0, vo = 0, ro = 0;
@@ -779,9 +842,12 @@ lmr_status_t lmr_batch_exchange(lmr_ctx_t* ctx, const lmr_transport_t* tp, const
                 if (own) break;
             }
             const uint64_t ubits = uint64_t(bits);
-            if (ord) {                                  // applied now, each element's records in stream order
+            if (ord || bucketed) {
+                // applied now: an ordered stream each element's records in stream order; in the
+                // bucketed mode (the overflow round: order-insensitive records, whose workspace
+                // holds the session's tile regions) with device atomics
                 lmr_apply_desc_t d = *desc;
-                d.strategy = LMR_STRATEGY_ORDERED;
+                d.strategy = ord ? LMR_STRATEGY_ORDERED : LMR_STRATEGY_DIRECT;
                 e = lmr_apply_soa(ctx, &d, src_i, iw, sc ? nullptr : src_v, sc ? &ubits : nullptr, tot, res, okp, sa);
             } else {
                 e = lmr_stage_soa(ctx, src_i, iw, sc ? nullptr : src_v, sc ? &ubits : nullptr, tot, res, okp, sa);
@@ -799,13 +865,13 @@ lmr_status_t lmr_batch_exchange(lmr_ctx_t* ctx, const lmr_transport_t* tp, const
     // ---- the peer transport's push: one host handshake per batch; if every PE packs and stages
     // fixed regions that fit the receive regions, every sender's pack writes straight into the
     // owners' regions (lmr_peer.hip) and nothing else crosses between the PEs but the mailbox
-    PeerTransport* peer = peer_of(tp);
     bool push = false;
+    const int64_t my_binfo = my_bucket ? int64_t((uint64_t(bC) << 32) | bcap) : 0;
     if (peer) {
         std::vector<int64_t> pi;
         const int64_t fits = (!free_pack || region_cap(cmax) <= peer_region_records(peer)) ? 1 : 0;
-        const int64_t info[8] = {my_flags, int64_t(m), int64_t(chunk), int64_t(my_k), int64_t(sbits), fits, 0, 0};
-        if ((st = peer_handshake(peer, info, pi)) != LMR_OK) return st;
+        const int64_t info[8] = {my_flags, int64_t(m), int64_t(chunk), int64_t(my_k), int64_t(sbits), fits, my_binfo, 0};
+        if ((st = peer_handshake(peer, info, pi)) != LMR_OK) return st == LMR_E_HIP ? xfail(__LINE__) : st;
         push = iw <= 8 && eb <= 8;
         for (uint32_t p = 0; p < npes; p++) {
             const int64_t* r = pi.data() + size_t(p) * 8;
@@ -816,9 +882,36 @@ lmr_status_t lmr_batch_exchange(lmr_ctx_t* ctx, const lmr_transport_t* tp, const
             src_bits[p] = r[4];
             nchunks = std::max<uint64_t>(nchunks, uint64_t(std::max<int64_t>(r[3], 1)));
         }
+        bucketed = push && my_binfo != 0;
+        for (uint32_t p = 0; p < npes; p++) bucketed = bucketed && pi[size_t(p) * 8 + 6] == my_binfo;
     }
+    // the bucketed session and the staged one both keep records in the workspace's temp arrays:
+    // whichever this batch does not use is applied first
+    if (!bucketed && bucket_sweep(ctx, x, x->sa) != hipSuccess) return xfail(__LINE__);
+    if (bucketed && !stage_session_empty(ctx)) {
+        if ((st = lmr_stage_finish(ctx, reinterpret_cast<lmr_stream_t>(x->sa))) != LMR_OK) return st;
+        if ((st = lmr_stage_begin(ctx, desc)) != LMR_OK) return st;
+    }
+    auto bucket_open = [&]() -> bool {
+        BucketSession& bs = x->bs;
+        if (bs.open) return true;
+        const int ts = tile_shift(int(desc->dtype));
+        const TiledWs w = carve_tiled_ws(ctx->ws, ctx->rec_cap);
+        bs.desc = *desc;
+        bs.C = bC;
+        bs.T = uint32_t((desc->shard_len + (uint64_t(1) << ts) - 1) >> ts);
+        bs.cap_t = std::min<uint64_t>(w.tmp_cap, 0xFFFFFFFFull) / bs.T;
+        bs.staged = 0;
+        bs.tfill = x->tfill.as<uint32_t>();
+        bs.err = ctx->d_err;
+        bs.prof = ctx->prof;
+        if (!x->tfill_zero && hipMemsetAsync(bs.tfill, 0, size_t(bs.T) * 4, x->sa) != hipSuccess) return false;
+        x->tfill_zero = true;
+        bs.open = true;
+        return true;
+    };
     if (push) {
-        if (xstate_wait_streams(x) != hipSuccess) return LMR_E_HIP;
+        if (xstate_wait_streams(x) != hipSuccess) return xfail(__LINE__);
         any_fixed = true;
         uint32_t* fill = x->fill.as<uint32_t>();
         for (uint64_t j = 0; j < nchunks; j++) {
@@ -830,7 +923,7 @@ lmr_status_t lmr_batch_exchange(lmr_ctx_t* ctx, const lmr_transport_t* tp, const
                 peer_wait_freed(peer, b, ctx->d_err, x->sw_free) != hipSuccess ||
                 hipEventRecord(x->ev_free_ok[b], x->sw_free) != hipSuccess ||
                 hipStreamWaitEvent(x->sp, x->ev_free_ok[b], 0) != hipSuccess)
-                return LMR_E_HIP;
+                return xfail(__LINE__);
             const uint64_t lo = chunk_lo(j), cnt = chunk_hi(j) - lo;
             if (j < my_k && cnt > 0) {
                 PackArgs pa;
@@ -854,17 +947,52 @@ lmr_status_t lmr_batch_exchange(lmr_ctx_t* ctx, const lmr_transport_t* tp, const
                 pa.ovf_cap = m;
                 pa.out_idx_tab = peer_idx_table(peer, b);
                 pa.out_vals_tab = scalar ? nullptr : peer_vals_table(peer, b);
-                if (launch_pack_free(pa, fill, uint32_t(region_cap(cnt)), x->sp) != hipSuccess) return LMR_E_HIP;
-            } else if (hipMemsetAsync(fill, 0, size_t(npes) * 4, x->sp) != hipSuccess) {
-                return LMR_E_HIP;
+                if (bucketed) {
+                    if (launch_pack_bucket(pa, bC, bshift, bcap, x->bfill.as<uint32_t>(), x->btot.as<uint32_t>(), x->sp) !=
+                        hipSuccess)
+                        return xfail(__LINE__);
+                } else if (launch_pack_free(pa, fill, uint32_t(region_cap(cnt)), x->sp) != hipSuccess) {
+                    return xfail(__LINE__);
+                }
+                if (peer_publish(peer, b, bucketed ? x->btot.as<uint32_t>() : fill, seq, x->sp) != hipSuccess)
+                    return xfail(__LINE__);
+            } else if (peer_publish(peer, b, nullptr, seq, x->sp) != hipSuccess) {   // (nothing this chunk)
+                return xfail(__LINE__);
             }
-            if (peer_publish(peer, b, fill, seq, x->sp) != hipSuccess) return LMR_E_HIP;
             // owner (apply stream): every source has published, each region staged with its count
             if (hipStreamWaitEvent(x->sw_pub, x->ev_begin, 0) != hipSuccess ||
                 peer_wait_published(peer, b, seq, ctx->d_err, x->sw_pub) != hipSuccess ||
                 hipEventRecord(x->ev_pub_ok[b], x->sw_pub) != hipSuccess ||
                 hipStreamWaitEvent(x->sa, x->ev_pub_ok[b], 0) != hipSuccess)
-                return LMR_E_HIP;
+                return xfail(__LINE__);
+            if (bucketed) {
+                // every source's bucket slices binned into the session's tile regions in one launch
+                BucketChunk c;
+                c.S = npes;
+                c.cap_b = bcap;
+                for (uint32_t p = 0; p < npes; p++) {
+                    const uint64_t cap = cap_of(uint64_t(std::max<int64_t>(src_m[p], 0)),
+                                                uint64_t(std::max<int64_t>(src_ch[p], 0)), j);
+                    if (cap == 0) continue;
+                    const bool sc = (src_fl[p] & LMR_XHDR_SCALAR) != 0;
+                    const uint64_t ch = uint64_t(std::max<int64_t>(src_ch[p], 1));
+                    c.idx[p] = peer_recv_idx(peer, p, b);
+                    c.val[p] = sc ? nullptr : peer_recv_vals(peer, p, b);
+                    c.sbits[p] = uint64_t(src_bits[p]);
+                    c.expect += (std::min(ch, uint64_t(std::max<int64_t>(src_m[p], 0))) + npes - 1) / npes;
+                }
+                if (c.expect > 0) {
+                    if (x->bs.open && x->bs.staged + c.expect > bucket_session_limit(x->bs) &&
+                        bucket_sweep(ctx, x, x->sa) != hipSuccess)
+                        return xfail(__LINE__);
+                    if (!bucket_open()) return xfail(__LINE__);
+                    TiledWs w = carve_tiled_ws(ctx->ws, ctx->rec_cap);
+                    if (launch_fine_bucket(c, x->bs, w, x->sa) != hipSuccess) return xfail(__LINE__);
+                    x->bs.staged += c.expect;
+                }
+                if (peer_mark_free(peer, b, seq, x->sa) != hipSuccess) return xfail(__LINE__);
+                continue;
+            }
             for (uint32_t p = 0; p < npes; p++) {
                 const uint64_t cap = cap_of(uint64_t(std::max<int64_t>(src_m[p], 0)),
                                             uint64_t(std::max<int64_t>(src_ch[p], 0)), j);
@@ -878,7 +1006,7 @@ lmr_status_t lmr_batch_exchange(lmr_ctx_t* ctx, const lmr_transport_t* tp, const
                 if (st != LMR_OK) return st;
             }
             if ((st = lmr_stage_flush(ctx, reinterpret_cast<lmr_stream_t>(x->sa))) != LMR_OK) return st;
-            if (peer_mark_free(peer, b, seq, x->sa) != hipSuccess) return LMR_E_HIP;
+            if (peer_mark_free(peer, b, seq, x->sa) != hipSuccess) return xfail(__LINE__);
         }
     } else {
     // chunk 0: pack, header exchange; chunk 1's pack (local work) runs during the wait
@@ -894,7 +1022,7 @@ lmr_status_t lmr_batch_exchange(lmr_ctx_t* ctx, const lmr_transport_t* tp, const
             // ---- the host reads chunk j's header rows (RCCL's send / recv counts are host
             // arguments); meanwhile the pack stream runs chunk j+1's pack and the apply stream
             // chunk j-1's staging
-            if (hipEventSynchronize(x->ev_hdr[b]) != hipSuccess) return LMR_E_HIP;
+            if (hipEventSynchronize(x->ev_hdr[b]) != hipSuccess) return xfail(__LINE__);
             const uint64_t k = lmr_exchange_plan(npes, iw, eb, h_send, h_recv, isb.data(), iso.data(), irb.data(),
                                                  iro.data(), vsb.data(), vso.data(), vrb.data(), vro.data());
             if (j == 0) {
@@ -976,29 +1104,29 @@ lmr_status_t lmr_batch_exchange(lmr_ctx_t* ctx, const lmr_transport_t* tp, const
                 cr.total += cr.recv_cnt[p];
             }
         // ---- receive buffers of this chunk (double-buffered against the apply stream)
-        if (x->recv_used[b] && hipStreamWaitEvent(x->sx, x->ev_recv_free[b], 0) != hipSuccess) return LMR_E_HIP;
+        if (x->recv_used[b] && hipStreamWaitEvent(x->sx, x->ev_recv_free[b], 0) != hipSuccess) return xfail(__LINE__);
         const uint64_t ib = iro[npes - 1] + irb[npes - 1], vb = vro[npes - 1] + vrb[npes - 1];
         if (x->recv_idx[b].need(ib + 8, x) != hipSuccess || x->recv_vals[b].need(vb + 8, x) != hipSuccess)
-            return LMR_E_HIP;
+            return xfail(__LINE__);
         const uint8_t* send_vals = mvsi ? static_cast<const uint8_t*>(d_vals) : x->send_vals[b].as<uint8_t>();
         // the records after the chunk's header rows (and so after its pack): with no host read of
         // the rows in between, only this orders them (and the owner's staging, which reads the rows)
-        if (nowait && hipStreamWaitEvent(x->sx, x->ev_hdr[b], 0) != hipSuccess) return LMR_E_HIP;
+        if (nowait && hipStreamWaitEvent(x->sx, x->ev_hdr[b], 0) != hipSuccess) return xfail(__LINE__);
         st = tp_alltoallv(tp, x, x->send_idx[b].p, isb.data(), iso.data(), x->recv_idx[b].p, irb.data(), iro.data(),
                           unit_for(iw), x->sx);
         if (st == LMR_OK)
             st = tp_alltoallv(tp, x, send_vals, vsb.data(), vso.data(), x->recv_vals[b].p, vrb.data(), vro.data(),
                               unit_for(eb), x->sx);
         if (st != LMR_OK) { guard.tp_failed = true; return st; }
-        if (hipEventRecord(x->ev_send_free[b], x->sx) != hipSuccess) return LMR_E_HIP;
+        if (hipEventRecord(x->ev_send_free[b], x->sx) != hipSuccess) return xfail(__LINE__);
         x->send_used[b] = true;
         if (hipEventRecord(x->ev_x[b], x->sx) != hipSuccess || hipStreamWaitEvent(x->sa, x->ev_x[b], 0) != hipSuccess)
-            return LMR_E_HIP;
+            return xfail(__LINE__);
         // ---- owner side: stage every source's records (apply stream)
         if (returning) {
             if (x->res.size() <= j) { x->res.resize(j + 1); x->rok.resize(j + 1); }
-            if (x->res[j].need(cr.total * eb + 8, x) != hipSuccess) return LMR_E_HIP;
-            if (want_ok && x->rok[j].need(cr.total + 8, x) != hipSuccess) return LMR_E_HIP;
+            if (x->res[j].need(cr.total * eb + 8, x) != hipSuccess) return xfail(__LINE__);
+            if (want_ok && x->rok[j].need(cr.total + 8, x) != hipSuccess) return xfail(__LINE__);
         }
         if (nowait) {
             // fixed regions with their counts in the header rows (device), each its own stream
@@ -1023,7 +1151,7 @@ lmr_status_t lmr_batch_exchange(lmr_ctx_t* ctx, const lmr_transport_t* tp, const
         }
         // this chunk's streams partitioned now (fused), before its receive buffers are reused
         if ((st = lmr_stage_flush(ctx, reinterpret_cast<lmr_stream_t>(x->sa))) != LMR_OK) return st;
-        if (hipEventRecord(x->ev_recv_free[b], x->sa) != hipSuccess) return LMR_E_HIP;
+        if (hipEventRecord(x->ev_recv_free[b], x->sa) != hipSuccess) return xfail(__LINE__);
         x->recv_used[b] = true;
         chunks.push_back(std::move(cr));
         // ---- the next chunk's header exchange (after this chunk's all-to-all-v on the
@@ -1046,7 +1174,7 @@ lmr_status_t lmr_batch_exchange(lmr_ctx_t* ctx, const lmr_transport_t* tp, const
     bool any_ovf = false;
     if (any_fixed && !push) {
         const int bl = int((nchunks - 1) & 1);
-        if (hipEventSynchronize(x->ev_hdr[bl]) != hipSuccess) return LMR_E_HIP;
+        if (hipEventSynchronize(x->ev_hdr[bl]) != hipSuccess) return xfail(__LINE__);
         const int64_t* h_last = h_recv_rows(bl);
         for (uint32_t p = 0; p < npes; p++) any_ovf = any_ovf || (h_last[p * LMR_XHDR_WORDS + 2] & LMR_XHDR_OVERFLOW);
     }
@@ -1058,14 +1186,14 @@ lmr_status_t lmr_batch_exchange(lmr_ctx_t* ctx, const lmr_transport_t* tp, const
             uint32_t c32 = 0;
             if (hipMemcpyAsync(&c32, x->ovf_count.p, 4, hipMemcpyDeviceToHost, x->sp) != hipSuccess ||
                 hipStreamSynchronize(x->sp) != hipSuccess)
-                return LMR_E_HIP;
+                return xfail(__LINE__);
             novf = std::min<uint64_t>(c32, m);
         }
         if ((st = wait_send_slot(b)) != LMR_OK) return st;
         if (novf > 0) {
             if (x->send_idx[b].need(novf * iw + 8, x) != hipSuccess ||
                 x->send_vals[b].need(novf * eb + 8, x) != hipSuccess)
-                return LMR_E_HIP;
+                return xfail(__LINE__);
             st = lmr_pack_unordered(ctx, layout, x->ovf_idx.as<uint64_t>(), novf, scalar ? nullptr : x->ovf_vals.p,
                                     desc->dtype, iw, x->send_idx[b].p, scalar ? nullptr : x->send_vals[b].p, nullptr,
                                     x->counts.as<uint64_t>(), x->offsets.as<uint64_t>(),
@@ -1076,9 +1204,9 @@ lmr_status_t lmr_batch_exchange(lmr_ctx_t* ctx, const lmr_transport_t* tp, const
                            novf > 0 ? x->counts.as<uint64_t>() : nullptr, npes, int64_t(-1), int64_t(0), int64_t(0),
                            int64_t(scalar ? LMR_XHDR_SCALAR : 0), sbits, int64_t(1), int64_t(novf), int64_t(novf),
                            x->hdr_send[b].as<int64_t>(), nullptr);
-        if (hipGetLastError() != hipSuccess || hipEventRecord(x->ev_packed[b], x->sp) != hipSuccess) return LMR_E_HIP;
+        if (hipGetLastError() != hipSuccess || hipEventRecord(x->ev_packed[b], x->sp) != hipSuccess) return xfail(__LINE__);
         if ((st = post_header(J, true)) != LMR_OK) return st;
-        if (hipEventSynchronize(x->ev_hdr[b]) != hipSuccess) return LMR_E_HIP;
+        if (hipEventSynchronize(x->ev_hdr[b]) != hipSuccess) return xfail(__LINE__);
         const int64_t* h_send = h_send_rows(b);
         const int64_t* h_recv = h_recv_rows(b);
         (void)lmr_exchange_plan(npes, iw, eb, h_send, h_recv, isb.data(), iso.data(), irb.data(), iro.data(),
@@ -1089,10 +1217,10 @@ lmr_status_t lmr_batch_exchange(lmr_ctx_t* ctx, const lmr_transport_t* tp, const
             // may be a collective (the host transports' are)
             const uint64_t self_io = iso[me], self_vo = vso[me];
             if (bypass) isb[me] = irb[me] = vsb[me] = vrb[me] = 0;
-            if (x->recv_used[b] && hipStreamWaitEvent(x->sx, x->ev_recv_free[b], 0) != hipSuccess) return LMR_E_HIP;
+            if (x->recv_used[b] && hipStreamWaitEvent(x->sx, x->ev_recv_free[b], 0) != hipSuccess) return xfail(__LINE__);
             const uint64_t ib = iro[npes - 1] + irb[npes - 1], vb = vro[npes - 1] + vrb[npes - 1];
             if (x->recv_idx[b].need(ib + 8, x) != hipSuccess || x->recv_vals[b].need(vb + 8, x) != hipSuccess)
-                return LMR_E_HIP;
+                return xfail(__LINE__);
             const uint8_t* send_vals = x->send_vals[b].as<uint8_t>();
             st = tp_alltoallv(tp, x, x->send_idx[b].p, isb.data(), iso.data(), x->recv_idx[b].p, irb.data(),
                               iro.data(), unit_for(iw), x->sx);
@@ -1100,13 +1228,13 @@ lmr_status_t lmr_batch_exchange(lmr_ctx_t* ctx, const lmr_transport_t* tp, const
                 st = tp_alltoallv(tp, x, send_vals, vsb.data(), vso.data(), x->recv_vals[b].p, vrb.data(), vro.data(),
                                   unit_for(eb), x->sx);
             if (st != LMR_OK) { guard.tp_failed = true; return st; }
-            if (hipEventRecord(x->ev_send_free[b], x->sx) != hipSuccess) return LMR_E_HIP;
+            if (hipEventRecord(x->ev_send_free[b], x->sx) != hipSuccess) return xfail(__LINE__);
             x->send_used[b] = true;
             if (hipEventRecord(x->ev_x[b], x->sx) != hipSuccess || hipStreamWaitEvent(x->sa, x->ev_x[b], 0) != hipSuccess)
-                return LMR_E_HIP;
+                return xfail(__LINE__);
             if ((st = stage_host(b, h_recv, cnt, self_io, self_vo, send_vals, J)) != LMR_OK) return st;
             if ((st = lmr_stage_flush(ctx, reinterpret_cast<lmr_stream_t>(x->sa))) != LMR_OK) return st;
-            if (hipEventRecord(x->ev_recv_free[b], x->sa) != hipSuccess) return LMR_E_HIP;
+            if (hipEventRecord(x->ev_recv_free[b], x->sa) != hipSuccess) return xfail(__LINE__);
             x->recv_used[b] = true;
         }
     }
@@ -1117,6 +1245,7 @@ lmr_status_t lmr_batch_exchange(lmr_ctx_t* ctx, const lmr_transport_t* tp, const
     } else {
         st = lmr_stage_finish(ctx, reinterpret_cast<lmr_stream_t>(x->sa));
         if (st != LMR_OK) return st;
+        if (bucket_sweep(ctx, x, x->sa) != hipSuccess) return xfail(__LINE__);
     }
     guard.armed = false;
     if (returning) {
@@ -1132,13 +1261,13 @@ lmr_status_t lmr_batch_exchange(lmr_ctx_t* ctx, const lmr_transport_t* tp, const
                 nsent += cr.send_cnt[p];
             }
             if (x->back.need(nsent * eb + 8, x) != hipSuccess || (want_ok && x->back_ok.need(nsent + 8, x) != hipSuccess))
-                return LMR_E_HIP;
+                return xfail(__LINE__);
             if (bypass && cr.recv_cnt[me]) {           // own results: a device copy, not the transport
                 if (hipMemcpyAsync(static_cast<uint8_t*>(x->back.p) + ro[me], x->res[j].as<uint8_t>() + so[me], sb[me],
                                    hipMemcpyDeviceToDevice, x->sa) != hipSuccess ||
                     (want_ok && hipMemcpyAsync(x->back_ok.as<uint8_t>() + oro[me], x->rok[j].as<uint8_t>() + oso[me],
                                                osb[me], hipMemcpyDeviceToDevice, x->sa) != hipSuccess))
-                    return LMR_E_HIP;
+                    return xfail(__LINE__);
             }
             if (bypass) sb[me] = rb[me] = osb[me] = orb[me] = 0;
             st = tp_alltoallv(tp, x, x->res[j].p, sb.data(), so.data(), x->back.p, rb.data(), ro.data(), unit_for(eb),
@@ -1155,7 +1284,7 @@ lmr_status_t lmr_batch_exchange(lmr_ctx_t* ctx, const lmr_transport_t* tp, const
             if (mvsi) {                                 // results come back in value order
                 if (hipMemcpyAsync(d_results, x->back.p, nsent * eb, hipMemcpyDeviceToDevice, x->sa) != hipSuccess ||
                     (want_ok && hipMemcpyAsync(d_ok, x->back_ok.p, nsent, hipMemcpyDeviceToDevice, x->sa) != hipSuccess))
-                    return LMR_E_HIP;
+                    return xfail(__LINE__);
             } else {
                 st = lmr_scatter_results(x->back.p, x->pos[j].as<uint32_t>(), nsent, eb,
                                          static_cast<uint8_t*>(d_results) + cr.lo * eb, want_ok ? x->back_ok.as<uint8_t>() : nullptr,
@@ -1169,12 +1298,12 @@ lmr_status_t lmr_batch_exchange(lmr_ctx_t* ctx, const lmr_transport_t* tp, const
         hipEventRecord(x->ev_apply_done, x->sa) != hipSuccess || hipEventRecord(x->ev_h_done, x->sh) != hipSuccess ||
         hipStreamWaitEvent(s0, x->ev_pack_done, 0) != hipSuccess || hipStreamWaitEvent(s0, x->ev_x_done, 0) != hipSuccess ||
         hipStreamWaitEvent(s0, x->ev_apply_done, 0) != hipSuccess || hipStreamWaitEvent(s0, x->ev_h_done, 0) != hipSuccess)
-        return LMR_E_HIP;
+        return xfail(__LINE__);
     if (push && (hipEventRecord(x->ev_marked[0], x->sw_free) != hipSuccess ||
                  hipEventRecord(x->ev_marked[1], x->sw_pub) != hipSuccess ||
                  hipStreamWaitEvent(s0, x->ev_marked[0], 0) != hipSuccess ||
                  hipStreamWaitEvent(s0, x->ev_marked[1], 0) != hipSuccess))
-        return LMR_E_HIP;
+        return xfail(__LINE__);
     return LMR_OK;
 }
 
@@ -1188,14 +1317,18 @@ lmr_status_t lmr_exchange_flush(lmr_ctx_t* ctx, lmr_stream_t stream) {
     if (!ctx) return LMR_E_INVALID;
     if (!ctx->xdefer_open) return LMR_OK;
     ctx->xdefer_open = false;
-    if (!stage_session_open(ctx)) return LMR_OK;
+    XState* x = ctx->xch;
+    const bool bopen = x && x->bs.open;
+    if (!stage_session_open(ctx) && !bopen) return LMR_OK;
     // the session was staged on the exchange's apply stream: `stream` (any stream, per the
     // header) waits for that staging before the sweep
-    if (XState* x = ctx->xch) {
+    if (x) {
         if (hipEventRecord(x->ev_apply_done, x->sa) != hipSuccess ||
             hipStreamWaitEvent(reinterpret_cast<hipStream_t>(stream), x->ev_apply_done, 0) != hipSuccess)
             return LMR_E_HIP;
     }
+    if (bopen && bucket_sweep(ctx, x, reinterpret_cast<hipStream_t>(stream)) != hipSuccess) return LMR_E_HIP;
+    if (!stage_session_open(ctx)) return LMR_OK;
     return lmr_stage_finish(ctx, stream);
 }
 

@@ -278,6 +278,8 @@ bool stage_session_free(const lmr_ctx* ctx);
 // a session is open / open for this descriptor (shard, element type, kind, op and operands)
 bool stage_session_open(const lmr_ctx* ctx);
 bool stage_session_of(const lmr_ctx* ctx, const lmr_apply_desc_t& d);
+// no session open, or one with no region staged
+bool stage_session_empty(const lmr_ctx* ctx);
 lmr_status_t stage_soa_dev(lmr_ctx* ctx, const void* d_indices, uint32_t index_size, const void* d_vals,
                            const void* val, uint64_t cap, uint64_t expect, const int64_t* d_n, hipStream_t s);
 
@@ -340,6 +342,42 @@ hipError_t launch_pack(const PackArgs& a, uint32_t* counts, uint32_t* partials, 
 // incomplete (pack again with launch_pack); with one, region i holds its first cap records and the
 // rest are in the list)
 hipError_t launch_pack_free(const PackArgs& a, uint32_t* fill, uint32_t cap, hipStream_t s);
+
+// the peer push's bucketed mode (lmr_bucket.hip): the sender packs by (owner, owner coarse bucket
+// of 128 tiles) into bucket slices of the owner's receive region, the owner bins each chunk
+// straight into fixed per-tile regions of a session swept once
+constexpr uint32_t kBucketHdr = 512;        // bytes of slice counts at the head of a bucketed index region
+constexpr uint32_t kBucketMaxKeys = 1024;   // (owner, bucket) keys of the sender's pack
+constexpr uint32_t kBucketMaxSrc = 16;      // PEs
+struct BucketSession {
+    bool open = false;
+    lmr_apply_desc_t desc{};
+    uint32_t T = 0, C = 0;   // the owner's tiles, buckets
+    uint64_t cap_t = 0;      // records per fixed tile region (workspace temp arrays)
+    uint64_t staged = 0;     // records expected in the session so far
+    uint32_t* tfill = nullptr;   // device [kMaxTiles] tile fills (zero between sessions)
+    uint32_t* err = nullptr;
+    Prof* prof = nullptr;
+};
+struct BucketChunk {
+    uint32_t S = 0, cap_b = 0;
+    const uint8_t* idx[kBucketMaxSrc] = {};   // source s's index area this chunk (null: nothing from s)
+    const uint8_t* val[kBucketMaxSrc] = {};   // null: the scalar sbits[s]
+    uint64_t sbits[kBucketMaxSrc] = {};
+    uint64_t expect = 0;
+};
+// buckets of the layout's largest shard (false: the layout / element type cannot take the mode)
+bool bucket_geometry(const lmr_layout_t& L, int dtype, uint32_t& C, int& cshift);
+// records per bucket slice of a receive region of R records (8 bytes each, index and value areas)
+uint32_t bucket_slice_cap(uint64_t R, uint32_t C, uint32_t eb);
+// the sender's pack of one chunk (a.out_idx_tab / out_vals_tab: the owners' regions) and the slice
+// counts into the owners' region headers; tot[q]: records written for owner q
+hipError_t launch_pack_bucket(const PackArgs& a, uint32_t C, int cshift, uint32_t cap_b, uint32_t* fill,
+                              uint32_t* tot, hipStream_t s);
+// largest session (records) the fixed tile regions take with headroom
+uint64_t bucket_session_limit(const BucketSession& bs);
+hipError_t launch_fine_bucket(const BucketChunk& c, const BucketSession& bs, const TiledWs& w, hipStream_t st);
+hipError_t launch_bucket_sweep(BucketSession& bs, const TiledWs& w, hipStream_t st);
 constexpr int kReduceBlocks = 1024;
 hipError_t launch_reduce(int dtype, int op, const void* x, uint64_t n, uint64_t* out, uint8_t* has,
                          void* part, uint8_t* part_has, hipStream_t s);

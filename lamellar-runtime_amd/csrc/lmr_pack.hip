@@ -364,8 +364,8 @@ __global__ __launch_bounds__(1024) void k_pack_stage(PackK p) {
                 I* oi = reinterpret_cast<I*>(p.out_idx_tab[c]);
                 V* ov = vals ? reinterpret_cast<V*>(p.out_vals_tab[c]) : nullptr;
                 for (uint32_t i = (wave % wpb) * 64 + lane; i < len; i += wpb * 64) {
-                    oi[d + i] = s_off[b + i];
-                    if (ov) ov[d + i] = s_val[b + i];
+                    as_global(oi)[d + i] = s_off[b + i];
+                    if (ov) as_global(ov)[d + i] = s_val[b + i];
                 }
             }
         } else if (!FREE || !s_over) {

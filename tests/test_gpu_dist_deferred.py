@@ -47,6 +47,7 @@ for j in range(4):
 world.wait_all()
 st = k.profile_read(reset=True)
 out["sweeps"] = np.array([st.get("tile_apply", (0, 0))[1]])
+out["coarse"] = np.array([st.get("bin_scatter", (0, 0))[1]])
 out["after_add"] = arr.to_numpy()
 fi = rng.integers(0, n_len, 300000).astype(np.uint64)
 fv = rng.integers(1, 1000, fi.size, dtype=np.uint64)
@@ -85,10 +86,19 @@ def _run(ws, env_extra, outdir):
     return [dict(np.load(os.path.join(outdir, f"pe{r}.npz"))) for r in range(ws)]
 
 
-@pytest.mark.parametrize("ws,backend,defer", [(1, "nccl", "1"), (2, "gloo", "1"), (3, "gloo", "1"), (2, "gloo", "0")],
-                         ids=["rccl-1rank", "gloo-2pe", "gloo-3pe", "gloo-2pe-nodefer"])
-def test_deferred_exchange_sessions(ws, backend, defer):
+@pytest.mark.parametrize("ws,backend,defer,mode",
+                         [(1, "nccl", "1", ""), (2, "gloo", "1", ""), (3, "gloo", "1", ""), (2, "gloo", "0", ""),
+                          (1, "nccl", "1", "buckets"), (2, "gloo", "1", "buckets"), (3, "gloo", "1", "buckets"),
+                          (2, "gloo", "0", "buckets")],
+                         ids=["rccl-1rank", "gloo-2pe", "gloo-3pe", "gloo-2pe-nodefer", "buckets-1rank", "buckets-2pe",
+                              "buckets-3pe", "buckets-2pe-nodefer"])
+def test_deferred_exchange_sessions(ws, backend, defer, mode):
+    """mode=buckets: the peer transport's bucketed push (LAMELLAR_EXCHANGE_BUCKETS=1): the owner's
+    session is the bucketed one (fixed tile regions, no owner coarse pass: no bin_scatter launch
+    in the add batches), left open across deferred batches the same way."""
     env = {"LAMELLAR_COMM_BACKEND": backend, "LAMELLAR_EXCHANGE_DEFER": defer}
+    if mode == "buckets":
+        env.update(LAMELLAR_TRANSPORT="peer", LAMELLAR_EXCHANGE_BUCKETS="1", LAMELLAR_PEER_TIMEOUT="60")
     if ws == 1:
         env["LAMELLAR_FORCE_EXCHANGE"] = "1"
     with tempfile.TemporaryDirectory() as d:
@@ -117,6 +127,8 @@ def test_deferred_exchange_sessions(ws, backend, defer):
     for r in range(ws):
         assert np.array_equal(pe[r]["after_xor"], a), r
     sweeps = [int(pe[r]["sweeps"][0]) for r in range(ws)]
+    if mode == "buckets":
+        assert all(int(pe[r]["coarse"][0]) == 0 for r in range(ws)), [int(pe[r]["coarse"][0]) for r in range(ws)]
     if defer == "1":
         assert all(s < 4 for s in sweeps), sweeps          # four batches, fewer sweeps
     else:
