@@ -34,7 +34,7 @@ namespace {
 constexpr uint32_t kBT = 1024;
 constexpr int kBRpt = 8;
 constexpr uint32_t kBRound = kBRpt * kBT;             // 8K records per LDS round
-constexpr uint32_t kBTilesPerBucket = 128;            // a coarse bucket: 128 tiles (the staged path's)
+constexpr uint32_t kBTilesPerBucket = 512;            // tiles per bucket at most (LMR_BUCKET_TPB)
 
 // ---------------------------------------------------------------- sender
 struct BPackK {
@@ -55,14 +55,20 @@ struct BPackK {
     uint32_t* err;
 };
 
-template <int VB, int MODE>
+// RPT records per thread and round: 8 (8K-record rounds, 132 KB of LDS, one block per CU) or 4
+// (4K, 76 KB, two blocks per CU: one block's round-trip latencies overlap the other's)
+// PAIRS: two consecutive records per 16-B load of indices and of values (8-byte values, both arrays
+// 16-B aligned, even block ranges); record j of a round is then 2 * ((j / 2) * 1024 + thread) + j % 2
+template <int VB, int MODE, int RPT, bool PAIRS>
 __global__ __launch_bounds__(1024) void k_pack_bucket(BPackK p) {
     using V = typename idx_t<VB>::I;
+    constexpr uint32_t kPRound = RPT * kBT;
     __shared__ uint32_t hist[kBucketMaxKeys], base[kBucketMaxKeys], cur[kBucketMaxKeys], room[kBucketMaxKeys],
         obase[kBucketMaxKeys], s_tot;
-    __shared__ uint16_t s_k[kBRound];
-    __shared__ uint32_t s_i[kBRound];
-    __shared__ V s_v[kBRound];
+    __shared__ uint16_t s_k[kPRound];
+    __shared__ uint32_t s_i[kPRound];
+    __shared__ V s_v[kPRound];
+    __shared__ uint8_t s_dq[kBucketMaxKeys];
     __shared__ uint8_t* s_itab[kBucketMaxSrc];
     __shared__ uint8_t* s_vtab[kBucketMaxSrc];
     const uint32_t nkeys = p.npes * p.C;
@@ -76,25 +82,45 @@ __global__ __launch_bounds__(1024) void k_pack_bucket(BPackK p) {
     const uint64_t bmask = (uint64_t(1) << p.cshift) - 1;
     const V* vals = reinterpret_cast<const V*>(p.vals);
     bool oob = false;
-    uint64_t g[kBRpt];
-    V v[kBRpt];
+    uint64_t g[RPT];
+    V v[RPT];
+    auto kof = [&](uint64_t r0, int j) -> uint64_t {
+        return PAIRS ? r0 + 2 * (uint64_t(j >> 1) * kBT + threadIdx.x) + (j & 1) : r0 + uint64_t(j) * kBT + threadIdx.x;
+    };
+    // (pairs: every pair is loaded from an even offset <= kl, the block range's last pair, and the
+    // records past hi are masked by the round)
+    const uint64_t kl = lo < hi ? lo + ((hi - 1 - lo) & ~uint64_t(1)) : lo;
     auto load_round = [&](uint64_t r0) {
+        if constexpr (PAIRS) {
 #pragma unroll
-        for (int j = 0; j < kBRpt; j++) {
-            const uint64_t k = r0 + uint64_t(j) * kBT + threadIdx.x;
-            g[j] = k < hi ? p.gidx[k] : ~uint64_t(0);
-            v[j] = k < hi ? (vals ? vals[k] : V(p.val_bits)) : V(0);
+            for (int j = 0; j < RPT; j += 2) {
+                const uint64_t k = kof(r0, j);
+                const uint64_t kc = k <= kl ? k : kl;
+                const ulonglong2 x = *reinterpret_cast<const ulonglong2*>(p.gidx + kc);
+                const ulonglong2 y = *reinterpret_cast<const ulonglong2*>(vals + kc);
+                g[j] = k < hi ? x.x : ~uint64_t(0);
+                g[j + 1] = k + 1 < hi ? x.y : ~uint64_t(0);
+                v[j] = V(y.x);
+                v[j + 1] = V(y.y);
+            }
+        } else {
+#pragma unroll
+            for (int j = 0; j < RPT; j++) {
+                const uint64_t k = kof(r0, j);
+                g[j] = k < hi ? p.gidx[k] : ~uint64_t(0);
+                v[j] = k < hi ? (vals ? vals[k] : V(p.val_bits)) : V(0);
+            }
         }
     };
     if (lo < hi) load_round(lo);
-    for (uint64_t r0 = lo; r0 < hi; r0 += kBRound) {
+    for (uint64_t r0 = lo; r0 < hi; r0 += kPRound) {
         for (uint32_t x = threadIdx.x; x < nkeys; x += kBT) hist[x] = 0;
         __syncthreads();
-        uint32_t key[kBRpt];                          // (key << 16) | rank, all ones: no record
-        uint32_t lof[kBRpt];                          // offset in the bucket
+        uint32_t key[RPT];                          // (key << 16) | rank, all ones: no record
+        uint32_t lof[RPT];                          // offset in the bucket
 #pragma unroll
-        for (int j = 0; j < kBRpt; j++) {
-            const uint64_t k = r0 + uint64_t(j) * kBT + threadIdx.x;
+        for (int j = 0; j < RPT; j++) {
+            const uint64_t k = kof(r0, j);
             uint64_t pe = 0, off = 0;
             const bool ok = k < hi && pe_and_offset_mode<MODE>(p.F, g[j], pe, off);
             oob |= k < hi && !ok;
@@ -112,14 +138,16 @@ __global__ __launch_bounds__(1024) void k_pack_bucket(BPackK p) {
                 // overflow list
                 const uint32_t r = h ? atomicAdd(&p.fill[threadIdx.x], h) : 0u;
                 const uint32_t rm = r >= p.cap_b ? 0u : min(h, p.cap_b - r);
-                cur[threadIdx.x] = r;
+                const uint32_t dq = threadIdx.x / p.C;
+                cur[threadIdx.x] = (threadIdx.x - dq * p.C) * p.cap_b + r;   // the run's first slot in the region
+                s_dq[threadIdx.x] = uint8_t(dq);
                 room[threadIdx.x] = rm;
                 obase[threadIdx.x] = h > rm ? atomicAdd(p.ovf_count, h - rm) : 0u;
             }
         }
         __syncthreads();
 #pragma unroll
-        for (int j = 0; j < kBRpt; j++) {
+        for (int j = 0; j < RPT; j++) {
             if (key[j] == ~0u) continue;
             const uint32_t kk = key[j] >> 16, rk = key[j] & 0xFFFFu;
             const uint32_t q = base[kk] + rk;
@@ -135,15 +163,20 @@ __global__ __launch_bounds__(1024) void k_pack_bucket(BPackK p) {
             s_i[q] = lof[j];
             s_v[q] = v[j];
         }
-        if (r0 + kBRound < hi) load_round(r0 + kBRound);   // the next round's loads under the write-out
+        if (r0 + kPRound < hi) load_round(r0 + kPRound);   // the next round's loads under the write-out
         __syncthreads();
         const uint32_t tot = s_tot;
-        for (uint32_t q = threadIdx.x; q < tot; q += kBT) {
+        // (a static trip count: the compiler can then wait for the prefetched loads alone, not for
+        // the write-out's stores after them, at the next round's first use)
+#pragma unroll
+        for (int it = 0; it < RPT; it++) {
+            const uint32_t q = uint32_t(it) * kBT + threadIdx.x;
+            if (q >= tot) continue;
             const uint32_t kk = s_k[q];
             const uint32_t jj = q - base[kk];
             if (jj >= room[kk]) continue;             // (a hole: its record went to the overflow list)
-            const uint32_t dq = kk / p.C, b = kk - dq * p.C;
-            const uint64_t slot = uint64_t(b) * p.cap_b + cur[kk] + jj;
+            const uint32_t dq = s_dq[kk];
+            const uint32_t slot = cur[kk] + jj;
             as_global(reinterpret_cast<uint32_t*>(s_itab[dq]))[slot] = s_i[q];
             if (p.val_tab) as_global(reinterpret_cast<V*>(s_vtab[dq]))[slot] = s_v[q];
         }
@@ -185,6 +218,7 @@ struct BFineK {
     const uint8_t* val[kBucketMaxSrc];   // null: the source's scalar sbits[s]
     uint64_t sbits[kBucketMaxSrc];
     uint32_t S, C, cap_b, T;
+    uint32_t tpb;                        // tiles per bucket (a power of two, <= kBTilesPerBucket)
     int tile_shift;
     uint64_t cap_t;                      // records per fixed tile region
     uint16_t* bin_lidx;                  // [T * cap_t]
@@ -203,7 +237,7 @@ __global__ __launch_bounds__(1024) void k_fine_bucket(BFineK p) {
     __shared__ uint32_t hist[kBTilesPerBucket], base[kBTilesPerBucket], cur[kBTilesPerBucket],
         room[kBTilesPerBucket], s_tot, s_part[16], s_spill;
     __shared__ uint16_t s_l[kBRound];
-    __shared__ uint8_t s_f[kBRound];
+    __shared__ uint16_t s_f[kBRound];
     __shared__ V s_v[kBRound];
     __shared__ const uint8_t* s_ib[kBucketMaxSrc];
     __shared__ const uint8_t* s_vb[kBucketMaxSrc];
@@ -285,10 +319,10 @@ __global__ __launch_bounds__(1024) void k_fine_bucket(BFineK p) {
         const uint32_t a = max(v_lo, bstart(b)), e = min(v_hi, bstart(b + 1));
         const uint32_t bn = next_bucket(b + 1);
         const bool has_next = bn < C && bstart(bn) < v_hi;
-        const uint32_t t0 = b * kBTilesPerBucket;
-        const uint32_t nf = t0 < p.T ? min(kBTilesPerBucket, p.T - t0) : 0u;
+        const uint32_t t0 = b * p.tpb;
+        const uint32_t nf = t0 < p.T ? min(p.tpb, p.T - t0) : 0u;
         for (uint32_t v0 = a; v0 < e; v0 += kBRound) {
-            for (uint32_t f = threadIdx.x; f < kBTilesPerBucket; f += kBT) hist[f] = 0;
+            for (uint32_t f = threadIdx.x; f < p.tpb; f += kBT) hist[f] = 0;
             if (threadIdx.x == 0) s_spill = 0;
             __syncthreads();
             uint32_t key[kBRpt];                     // (tile in bucket << 16) | rank, all ones: none
@@ -302,7 +336,7 @@ __global__ __launch_bounds__(1024) void k_fine_bucket(BFineK p) {
             }
             __syncthreads();
             {
-                const uint32_t h = threadIdx.x < kBTilesPerBucket ? hist[threadIdx.x] : 0u;
+                const uint32_t h = threadIdx.x < p.tpb ? hist[threadIdx.x] : 0u;
                 const uint32_t ex = block_excl_scan(h, &s_tot);
                 if (threadIdx.x < nf) {
                     base[threadIdx.x] = ex;
@@ -320,7 +354,7 @@ __global__ __launch_bounds__(1024) void k_fine_bucket(BFineK p) {
                 const uint32_t f = key[j] >> 16;
                 const uint32_t q = base[f] + (key[j] & 0xFFFFu);
                 s_l[q] = uint16_t(li[j] & lmask);
-                s_f[q] = uint8_t(f);
+                s_f[q] = uint16_t(f);
                 s_v[q] = vv[j];
             }
             {   // one prefetch site: this bucket's next round, else the next bucket's first
@@ -379,6 +413,19 @@ hipError_t bdispatch_vb(int vb, F&& f) {
 
 }  // namespace
 
+// LMR_BUCKET_TPB: log2 of the tiles per bucket (default 8: 256 tiles of 64 KiB). The sender's keys
+// are PEs x buckets: at 8 PEs x 2^26-element u64 shards, 256 keys. Measured on one GPU at that
+// geometry (tools/bucket_bench, per 2^26-record chunk, pack + owner fine pass on two streams):
+// 128 tiles (512 keys) 1.13-1.17 ms, 256 tiles 1.02-1.06, 512 tiles 1.04; 64 tiles (1024 keys) 1.22
+int bucket_tpb_log2() {
+    static const int v = [] {
+        const char* e = getenv("LMR_BUCKET_TPB");
+        const int x = (e && *e) ? atoi(e) : 8;
+        return x < 0 ? 0 : (x > 9 ? 9 : x);
+    }();
+    return v;
+}
+
 bool bucket_geometry(const lmr_layout_t& L, int dtype, uint32_t& C, int& cshift) {
     const int vb = dtype_bytes(dtype);
     if (vb == 0 || L.num_pes == 0 || L.num_pes > kBucketMaxSrc) return false;
@@ -387,8 +434,9 @@ bool bucket_geometry(const lmr_layout_t& L, int dtype, uint32_t& C, int& cshift)
     const int ts = tile_shift(dtype);
     const uint64_t tiles = (maxlen + (uint64_t(1) << ts) - 1) >> ts;
     if (tiles == 0 || tiles > uint64_t(kMaxTiles)) return false;
-    C = uint32_t((tiles + kBTilesPerBucket - 1) / kBTilesPerBucket);
-    cshift = ts + 7;
+    const int tl = bucket_tpb_log2();
+    C = uint32_t((tiles + (uint64_t(1) << tl) - 1) >> tl);
+    cshift = ts + tl;
     return uint64_t(C) * L.num_pes <= kBucketMaxKeys && uint64_t(C) * 4 <= kBucketHdr;
 }
 
@@ -426,16 +474,33 @@ hipError_t launch_pack_bucket(const PackArgs& a, uint32_t C, int cshift, uint32_
     p.ovf_cap = a.ovf_cap;
     p.err = a.err;
     ProfScope ps(a.prof, LMR_STAGE_PACK, s, a.n);
+    static const int rpt = [] { const char* e = getenv("LMR_BUCKET_RPT"); return (e && e[0] == '4') ? 4 : 8; }();
+    static const bool pairs_on = [] { const char* e = getenv("LMR_PACK_PAIRS"); return !(e && e[0] == '0'); }();
+    // (an even record count too: a block's last pair is loaded whole, so no load passes the arrays)
+    const bool pairs = pairs_on && a.vals && a.val_bytes == 8 && (a.n & 1) == 0 &&
+                       ((reinterpret_cast<uintptr_t>(a.gidx) | reinterpret_cast<uintptr_t>(a.vals)) & 15) == 0;
+    if (pairs && (p.chunk & 1)) p.chunk += 1;
     if (a.n > 0) {
         const int mode = layout_map_mode(a.layout);
         const hipError_t e = bdispatch_vb(a.vals ? int(a.val_bytes) : 8, [&](auto vbt) {
             constexpr int VB = decltype(vbt)::value;
-            if (mode == LMR_MAP_BLOCK)
-                hipLaunchKernelGGL((k_pack_bucket<VB, LMR_MAP_BLOCK>), dim3(unsigned(G)), dim3(kBT), 0, s, p);
-            else if (mode == LMR_MAP_CYCLIC)
-                hipLaunchKernelGGL((k_pack_bucket<VB, LMR_MAP_CYCLIC>), dim3(unsigned(G)), dim3(kBT), 0, s, p);
-            else
-                hipLaunchKernelGGL((k_pack_bucket<VB, LMR_MAP_GENERIC>), dim3(unsigned(G)), dim3(kBT), 0, s, p);
+            auto go = [&](auto rt) {
+                constexpr int R = decltype(rt)::value;
+                constexpr bool kP = VB == 8;
+                if (kP && pairs && mode == LMR_MAP_BLOCK)
+                    hipLaunchKernelGGL((k_pack_bucket<VB, LMR_MAP_BLOCK, R, kP>), dim3(unsigned(G)), dim3(kBT), 0, s, p);
+                else if (kP && pairs && mode == LMR_MAP_CYCLIC)
+                    hipLaunchKernelGGL((k_pack_bucket<VB, LMR_MAP_CYCLIC, R, kP>), dim3(unsigned(G)), dim3(kBT), 0, s, p);
+                else if (mode == LMR_MAP_BLOCK)
+                    hipLaunchKernelGGL((k_pack_bucket<VB, LMR_MAP_BLOCK, R, false>), dim3(unsigned(G)), dim3(kBT), 0, s, p);
+                else if (mode == LMR_MAP_CYCLIC)
+                    hipLaunchKernelGGL((k_pack_bucket<VB, LMR_MAP_CYCLIC, R, false>), dim3(unsigned(G)), dim3(kBT), 0, s, p);
+                else
+                    hipLaunchKernelGGL((k_pack_bucket<VB, LMR_MAP_GENERIC, R, false>), dim3(unsigned(G)), dim3(kBT), 0, s,
+                                       p);
+            };
+            if (rpt == 4) go(std::integral_constant<int, 4>{});
+            else go(std::integral_constant<int, 8>{});
             return hipGetLastError();
         });
         if (e != hipSuccess) return e;
@@ -462,6 +527,7 @@ hipError_t launch_fine_bucket(const BucketChunk& c, const BucketSession& bs, con
     p.C = bs.C;
     p.cap_b = c.cap_b;
     p.T = bs.T;
+    p.tpb = 1u << bs.tpb_log2;
     p.tile_shift = tile_shift(int(bs.desc.dtype));
     p.cap_t = bs.cap_t;
     p.bin_lidx = reinterpret_cast<uint16_t*>(w.tmp_idx);

@@ -346,13 +346,14 @@ hipError_t launch_pack_free(const PackArgs& a, uint32_t* fill, uint32_t cap, hip
 // the peer push's bucketed mode (lmr_bucket.hip): the sender packs by (owner, owner coarse bucket
 // of 128 tiles) into bucket slices of the owner's receive region, the owner bins each chunk
 // straight into fixed per-tile regions of a session swept once
-constexpr uint32_t kBucketHdr = 512;        // bytes of slice counts at the head of a bucketed index region
+constexpr uint32_t kBucketHdr = 4096;       // bytes of slice counts at the head of a bucketed index region (kBucketMaxKeys u32)
 constexpr uint32_t kBucketMaxKeys = 1024;   // (owner, bucket) keys of the sender's pack
 constexpr uint32_t kBucketMaxSrc = 16;      // PEs
 struct BucketSession {
     bool open = false;
     lmr_apply_desc_t desc{};
     uint32_t T = 0, C = 0;   // the owner's tiles, buckets
+    int tpb_log2 = 8;        // log2 of the tiles per bucket (bucket_tpb_log2)
     uint64_t cap_t = 0;      // records per fixed tile region (workspace temp arrays)
     uint64_t staged = 0;     // records expected in the session so far
     uint32_t* tfill = nullptr;   // device [kMaxTiles] tile fills (zero between sessions)
@@ -367,6 +368,7 @@ struct BucketChunk {
     uint64_t expect = 0;
 };
 // buckets of the layout's largest shard (false: the layout / element type cannot take the mode)
+int bucket_tpb_log2();
 bool bucket_geometry(const lmr_layout_t& L, int dtype, uint32_t& C, int& cshift);
 // records per bucket slice of a receive region of R records (8 bytes each, index and value areas)
 uint32_t bucket_slice_cap(uint64_t R, uint32_t C, uint32_t eb);
