@@ -32,8 +32,6 @@ namespace lmr {
 namespace {
 
 constexpr uint32_t kBT = 1024;
-constexpr int kBRpt = 8;
-constexpr uint32_t kBRound = kBRpt * kBT;             // 8K records per LDS round
 constexpr uint32_t kBTilesPerBucket = 512;            // tiles per bucket at most (LMR_BUCKET_TPB)
 
 // ---------------------------------------------------------------- sender
@@ -229,16 +227,19 @@ struct BFineK {
     uint32_t* err;
 };
 
-template <int VB>
+// RPT records per thread and round: 8 (8K-record rounds, one block per CU) or 4 (4K, ~64 KB of LDS:
+// two blocks per CU, or one beside a pack block)
+template <int VB, int RPT>
 __global__ __launch_bounds__(1024) void k_fine_bucket(BFineK p) {
     using V = typename idx_t<VB>::I;
+    constexpr uint32_t kFRound = RPT * kBT;
     constexpr uint32_t kSegMax = kBucketMaxKeys * 2;   // (bucket, source) segments: C x S
     __shared__ uint32_t s_vs[kSegMax + 1];
     __shared__ uint32_t hist[kBTilesPerBucket], base[kBTilesPerBucket], cur[kBTilesPerBucket],
         room[kBTilesPerBucket], s_tot, s_part[16], s_spill;
-    __shared__ uint16_t s_l[kBRound];
-    __shared__ uint16_t s_f[kBRound];
-    __shared__ V s_v[kBRound];
+    __shared__ uint16_t s_l[kFRound];
+    __shared__ uint16_t s_f[kFRound];
+    __shared__ V s_v[kFRound];
     __shared__ const uint8_t* s_ib[kBucketMaxSrc];
     __shared__ const uint8_t* s_vb[kBucketMaxSrc];
     __shared__ uint64_t s_sb[kBucketMaxSrc];
@@ -284,13 +285,13 @@ __global__ __launch_bounds__(1024) void k_fine_bucket(BFineK p) {
     const uint32_t lmask = (1u << p.tile_shift) - 1u;
     const uint64_t tile_elems = uint64_t(1) << p.tile_shift;
     auto bstart = [&](uint32_t b) { return s_vs[b * S]; };   // bucket b = virtual [bstart(b), bstart(b + 1))
-    uint32_t li[kBRpt];
-    V vv[kBRpt];
-    // round [v0, min(v0 + kBRound, e)) of bucket b's virtual records (its sources' slices in order)
+    uint32_t li[RPT];
+    V vv[RPT];
+    // round [v0, min(v0 + kFRound, e)) of bucket b's virtual records (its sources' slices in order)
     auto load_round = [&](uint32_t b, uint32_t v0, uint32_t e) {
         uint32_t k = b * S;
 #pragma unroll
-        for (int j = 0; j < kBRpt; j++) {
+        for (int j = 0; j < RPT; j++) {
             const uint32_t v = v0 + uint32_t(j) * kBT + threadIdx.x;
             li[j] = 0;
             vv[j] = V(0);
@@ -321,13 +322,13 @@ __global__ __launch_bounds__(1024) void k_fine_bucket(BFineK p) {
         const bool has_next = bn < C && bstart(bn) < v_hi;
         const uint32_t t0 = b * p.tpb;
         const uint32_t nf = t0 < p.T ? min(p.tpb, p.T - t0) : 0u;
-        for (uint32_t v0 = a; v0 < e; v0 += kBRound) {
+        for (uint32_t v0 = a; v0 < e; v0 += kFRound) {
             for (uint32_t f = threadIdx.x; f < p.tpb; f += kBT) hist[f] = 0;
             if (threadIdx.x == 0) s_spill = 0;
             __syncthreads();
-            uint32_t key[kBRpt];                     // (tile in bucket << 16) | rank, all ones: none
+            uint32_t key[RPT];                     // (tile in bucket << 16) | rank, all ones: none
 #pragma unroll
-            for (int j = 0; j < kBRpt; j++) {
+            for (int j = 0; j < RPT; j++) {
                 const uint32_t v = v0 + uint32_t(j) * kBT + threadIdx.x;
                 const uint32_t f = li[j] >> p.tile_shift;
                 const bool ok = v < e && f < nf;
@@ -349,7 +350,7 @@ __global__ __launch_bounds__(1024) void k_fine_bucket(BFineK p) {
             }
             __syncthreads();
 #pragma unroll
-            for (int j = 0; j < kBRpt; j++) {
+            for (int j = 0; j < RPT; j++) {
                 if (key[j] == ~0u) continue;
                 const uint32_t f = key[j] >> 16;
                 const uint32_t q = base[f] + (key[j] & 0xFFFFu);
@@ -358,16 +359,19 @@ __global__ __launch_bounds__(1024) void k_fine_bucket(BFineK p) {
                 s_v[q] = vv[j];
             }
             {   // one prefetch site: this bucket's next round, else the next bucket's first
-                const bool more = v0 + kBRound < e;
+                const bool more = v0 + kFRound < e;
                 const uint32_t nbk = more ? b : (has_next ? bn : b);
-                load_round(nbk, more ? v0 + kBRound : (has_next ? max(v_lo, bstart(bn)) : e),
+                load_round(nbk, more ? v0 + kFRound : (has_next ? max(v_lo, bstart(bn)) : e),
                            more ? e : (has_next ? min(v_hi, bstart(bn + 1)) : e));
             }
             __syncthreads();
             const uint32_t tot = s_tot;
             // the write-out holds no device atomic (a returned value would make the compiler wait for
             // the prefetch); the records past their tile's region go in the loop after it
-            for (uint32_t q = threadIdx.x; q < tot; q += kBT) {
+#pragma unroll
+            for (int it = 0; it < RPT; it++) {       // (a static trip count, as in the pack)
+                const uint32_t q = uint32_t(it) * kBT + threadIdx.x;
+                if (q >= tot) continue;
                 const uint32_t f = s_f[q], jj = q - base[f];
                 if (jj < room[f]) {
                     const uint64_t dst = uint64_t(t0 + f) * p.cap_t + cur[f] + jj;
@@ -537,9 +541,11 @@ hipError_t launch_fine_bucket(const BucketChunk& c, const BucketSession& bs, con
     p.op = int(bs.desc.op);
     p.err = bs.err;
     ProfScope ps(bs.prof, LMR_STAGE_FINE_SCATTER, st, c.expect);
+    static const int rpt = [] { const char* e = getenv("LMR_BUCKET_FRPT"); return (e && e[0] == '4') ? 4 : 8; }();
     return bdispatch_vb(dtype_bytes(int(bs.desc.dtype)), [&](auto vbt) {
         constexpr int VB = decltype(vbt)::value;
-        hipLaunchKernelGGL((k_fine_bucket<VB>), dim3(1024), dim3(kBT), 0, st, p);
+        if (rpt == 4) hipLaunchKernelGGL((k_fine_bucket<VB, 4>), dim3(1024), dim3(kBT), 0, st, p);
+        else hipLaunchKernelGGL((k_fine_bucket<VB, 8>), dim3(1024), dim3(kBT), 0, st, p);
         return hipGetLastError();
     });
 }

@@ -3,7 +3,7 @@
 // on the per-GPU work of one N = 8 step.
 //
 //   pack  : one PE's 2^26-record chunk of u64 add records, uniform over a Block array of 8 x 2^26
-//           elements, packed by (owner, owner bucket of 128 tiles) = 512 keys into eight owners'
+//           elements, packed by (owner, owner bucket: 256 tiles by default, LMR_BUCKET_TPB) = 256 keys into eight owners'
 //           receive regions (uncached device memory, as the peer transport allocates them; on one
 //           GPU all eight are local, so no xGMI time is in these numbers)
 //   fine  : one owner's chunk: the eight regions read back as its eight sources' bucket slices
@@ -12,7 +12,7 @@
 //   both  : pack and fine at once on two streams (the exchange overlaps chunk j's fine pass with
 //           chunk j + 1's pack), on separate region sets
 //   sweep : the tile sweep of a session of four chunks (2^28 records) over the 2^26-element shard
-// usage: tools/bucket_bench [reps]
+// usage: tools/bucket_bench [reps]      (BB_CACHED=1: plain cached regions, a probe only)
 // build: see tools/bucket_bench.sh
 #include <hip/hip_runtime.h>
 #include <cstdio>
@@ -45,9 +45,17 @@ static Regions make_regions(uint32_t npes, uint64_t R) {
     Regions r;
     r.idx.resize(npes);
     r.val.resize(npes);
+    // BB_CACHED=1: plain (coarse-grained, cached) device memory instead of the peer transport's
+    // uncached regions (a probe of what the uncached write path costs; not a valid peer region)
+    static const bool cached = getenv("BB_CACHED") && getenv("BB_CACHED")[0] == '1';
     for (uint32_t q = 0; q < npes; q++) {
-        CK(hipExtMallocWithFlags(reinterpret_cast<void**>(&r.idx[q]), R * 8, hipDeviceMallocUncached));
-        CK(hipExtMallocWithFlags(reinterpret_cast<void**>(&r.val[q]), R * 8, hipDeviceMallocUncached));
+        if (cached) {
+            CK(hipMalloc(reinterpret_cast<void**>(&r.idx[q]), R * 8));
+            CK(hipMalloc(reinterpret_cast<void**>(&r.val[q]), R * 8));
+        } else {
+            CK(hipExtMallocWithFlags(reinterpret_cast<void**>(&r.idx[q]), R * 8, hipDeviceMallocUncached));
+            CK(hipExtMallocWithFlags(reinterpret_cast<void**>(&r.val[q]), R * 8, hipDeviceMallocUncached));
+        }
     }
     CK(hipMalloc(&r.d_idx, npes * sizeof(void*)));
     CK(hipMalloc(&r.d_val, npes * sizeof(void*)));
