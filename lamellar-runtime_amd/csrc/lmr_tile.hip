@@ -141,7 +141,9 @@ constexpr bool kOwnCombine = LMR_OWN_COMBINE != 0;   // wave-combined add in the
 // Owner mode: one block per tile — load the tile into LDS, apply the tile's
 // records with LDS atomics, write it back. Kept free of the delta path's
 // register arrays so two 1024-thread blocks (2 x 64 KiB LDS) fit per CU.
-template <typename T, int OPT>
+// PK: the wide path's packed records (a template parameter: a run-time test in the non-packed
+// kernels cost C3's tile sweep 6-10 %, round 6)
+template <typename T, int OPT, bool PK = false>
 __global__ __launch_bounds__(1024, 8) void k_tile_owner(TileArgs a) {
     using U = typename bits_of<T>::U;
     using W = typename word_of<T>::W;
@@ -218,7 +220,7 @@ __global__ __launch_bounds__(1024, 8) void k_tile_owner(TileArgs a) {
     };
     if constexpr (sizeof(T) <= 4) {
         // packed records (the wide path): one 8-B load per record, kPk in flight per thread
-        if (a.packed) {
+        if constexpr (PK) {
             const uint2* rec = reinterpret_cast<const uint2*>(a.bin_val);
             constexpr uint32_t kPk = 8;
             for (uint32_t b0 = lo; b0 < hi; b0 += kPk * 1024u) {
@@ -235,7 +237,7 @@ __global__ __launch_bounds__(1024, 8) void k_tile_owner(TileArgs a) {
         }
     } else {
         // packed 16-B records of 8-byte values {index, 0, value}: one 16-B load per record
-        if (a.packed) {
+        if constexpr (PK) {
             const uint4* rec = reinterpret_cast<const uint4*>(a.bin_val);
             constexpr uint32_t kPk = 4;
             for (uint32_t b0 = lo; b0 < hi; b0 += kPk * 1024u) {
@@ -344,7 +346,7 @@ __global__ __launch_bounds__(1024, 8) void k_tile_owner(TileArgs a) {
 // over the delta list: combine kSplit records in an identity-initialised LDS
 // tile, push one device-scope atomic per touched element, rebuild fetch
 // results as base (+) the record's LDS prefix.
-template <typename T, int OPT, int TB = kTileBytes>
+template <typename T, int OPT, int TB = kTileBytes, bool PK = false>
 __global__ __launch_bounds__(1024) void k_tile_delta(TileArgs a) {
     using U = typename bits_of<T>::U;
     using W = typename word_of<T>::W;
@@ -387,10 +389,10 @@ __global__ __launch_bounds__(1024) void k_tile_delta(TileArgs a) {
         // the piece's records loaded first (clamped, branch-free: all in flight), then combined
         uint16_t lk[kSplit / 1024];
         T vk[kSplit / 1024];
+        if constexpr (PK) {                                     // the wide path's packed records
 #pragma unroll
-        for (int k = 0; k < int(kSplit / 1024); k++) {
-            const uint32_t r = min(w.lo + threadIdx.x + uint32_t(k) * 1024u, w.hi - 1);
-            if (a.packed) {                                     // the wide path's packed records
+            for (int k = 0; k < int(kSplit / 1024); k++) {
+                const uint32_t r = min(w.lo + threadIdx.x + uint32_t(k) * 1024u, w.hi - 1);
                 if constexpr (sizeof(T) <= 4) {
                     const uint2 x = reinterpret_cast<const uint2*>(a.bin_val)[r];
                     lk[k] = uint16_t(x.x);
@@ -400,10 +402,14 @@ __global__ __launch_bounds__(1024) void k_tile_delta(TileArgs a) {
                     lk[k] = uint16_t(x.x);
                     vk[k] = from_bits<T>(U(uint64_t(x.z) | (uint64_t(x.w) << 32)));
                 }
-                continue;
             }
-            lk[k] = bin_lidx[r];
-            vk[k] = a.scalar ? sv : bin_val[r];
+        } else {
+#pragma unroll
+            for (int k = 0; k < int(kSplit / 1024); k++) {
+                const uint32_t r = min(w.lo + threadIdx.x + uint32_t(k) * 1024u, w.hi - 1);
+                lk[k] = bin_lidx[r];
+                vk[k] = a.scalar ? sv : bin_val[r];
+            }
         }
 #pragma unroll
         for (int k = 0; k < int(kSplit / 1024); k++) {
@@ -541,10 +547,11 @@ hipError_t launch_tile_kernels(int dtype, int opt, const TileArgs& t, bool delta
         return hipErrorUnknown;
     const hipError_t e = dispatch_dtype_t(dtype, [&](auto tag) {
         using Ty = decltype(tag);
-        auto go = [&](auto optc, auto tbc) {
+        auto go = [&](auto optc, auto tbc, auto pkc) {
             constexpr int OPT = decltype(optc)::value, TB = decltype(tbc)::value;
-            auto* kd = k_tile_delta<Ty, OPT, TB>;
-            auto* ko = k_tile_owner<Ty, OPT>;
+            constexpr bool PK = decltype(pkc)::value;
+            auto* kd = k_tile_delta<Ty, OPT, TB, PK>;
+            auto* ko = k_tile_owner<Ty, OPT, PK>;
             hipError_t ea = allow_lds(kd, TB);
             if (ea == hipSuccess) ea = allow_lds(ko, TB);
             if (ea != hipSuccess) return ea;
@@ -555,13 +562,16 @@ hipError_t launch_tile_kernels(int dtype, int opt, const TileArgs& t, bool delta
                 hipLaunchKernelGGL(kd, dim3(dgrid), dim3(1024), size_t(TB), s, t);
             return hipSuccess;
         };
-        auto by_op = [&](auto tbc) {
-            if (opt == LMR_OP_ADD) return go(std::integral_constant<int, LMR_OP_ADD>{}, tbc);
-            if (opt == LMR_OP_FETCH_ADD) return go(std::integral_constant<int, LMR_OP_FETCH_ADD>{}, tbc);
-            return go(std::integral_constant<int, -1>{}, tbc);
+        auto by_op = [&](auto tbc, auto pkc) {
+            if (opt == LMR_OP_ADD) return go(std::integral_constant<int, LMR_OP_ADD>{}, tbc, pkc);
+            if (opt == LMR_OP_FETCH_ADD) return go(std::integral_constant<int, LMR_OP_FETCH_ADD>{}, tbc, pkc);
+            return go(std::integral_constant<int, -1>{}, tbc, pkc);
         };
-        const hipError_t el = tile_bytes == kWideBytes ? by_op(std::integral_constant<int, int(kWideBytes)>{})
-                                                       : by_op(std::integral_constant<int, kTileBytes>{});
+        using W = std::integral_constant<int, int(kWideBytes)>;
+        // (packed records only on the wide path)
+        const hipError_t el = tile_bytes != kWideBytes ? by_op(std::integral_constant<int, kTileBytes>{}, std::false_type{})
+                              : t.packed ? by_op(W{}, std::true_type{})
+                                         : by_op(W{}, std::false_type{});
         return el != hipSuccess ? el : hipGetLastError();
     });
     // the launch stream continues after both (joined even when a launch failed)
