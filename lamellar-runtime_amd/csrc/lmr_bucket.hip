@@ -45,6 +45,11 @@ struct BPackK {
     int cshift;                  // bucket of a local offset = off >> cshift
     uint8_t* const* idx_tab;     // device: owner q's index area (header + C x cap_b u32 offsets in bucket)
     uint8_t* const* val_tab;     // device: owner q's value area (C x cap_b values)
+    // idx_tab null: owner q's areas at idx_base + q * idx_stride / val_base + q * val_stride (a send
+    // buffer of the collective exchange; val_base null: scalar value)
+    uint8_t* idx_base;
+    uint8_t* val_base;
+    uint64_t idx_stride, val_stride;
     uint32_t* fill;              // [npes * C] records reserved in each slice this chunk
     uint64_t* ovf_gidx;
     uint8_t* ovf_vals;
@@ -73,9 +78,11 @@ __global__ __launch_bounds__(1024) void k_pack_bucket(BPackK p) {
     // the owners' region pointers in LDS (a per-record load from the device table would put a
     // dependent global load in front of every store of the write-out)
     if (threadIdx.x < p.npes) {
-        s_itab[threadIdx.x] = p.idx_tab[threadIdx.x] + kBucketHdr;
-        s_vtab[threadIdx.x] = p.val_tab ? p.val_tab[threadIdx.x] : nullptr;
+        const uint64_t q = threadIdx.x;
+        s_itab[q] = (p.idx_tab ? p.idx_tab[q] : p.idx_base + q * p.idx_stride) + kBucketHdr;
+        s_vtab[q] = p.idx_tab ? (p.val_tab ? p.val_tab[q] : nullptr) : (p.val_base ? p.val_base + q * p.val_stride : nullptr);
     }
+    const bool has_vals = p.idx_tab ? p.val_tab != nullptr : p.val_base != nullptr;
     const uint64_t lo = uint64_t(blockIdx.x) * p.chunk, hi = min(lo + p.chunk, p.n);
     const uint64_t bmask = (uint64_t(1) << p.cshift) - 1;
     const V* vals = reinterpret_cast<const V*>(p.vals);
@@ -176,7 +183,7 @@ __global__ __launch_bounds__(1024) void k_pack_bucket(BPackK p) {
             const uint32_t dq = s_dq[kk];
             const uint32_t slot = cur[kk] + jj;
             as_global(reinterpret_cast<uint32_t*>(s_itab[dq]))[slot] = s_i[q];
-            if (p.val_tab) as_global(reinterpret_cast<V*>(s_vtab[dq]))[slot] = s_v[q];
+            if (has_vals) as_global(reinterpret_cast<V*>(s_vtab[dq]))[slot] = s_v[q];
         }
         __syncthreads();
     }
@@ -191,12 +198,13 @@ __global__ __launch_bounds__(1024) void k_pack_bucket(BPackK p) {
 // one block per owner q: the slices' counts into q's region header, their sum into tot[q] (the
 // mailbox count), the fill counters cleared for the next chunk, then a system-scope release
 __global__ __launch_bounds__(256) void k_bucket_hdr(uint32_t* fill, uint32_t C, uint32_t cap_b,
-                                                    uint8_t* const* idx_tab, uint32_t* tot) {
+                                                    uint8_t* const* idx_tab, uint8_t* idx_base, uint64_t idx_stride,
+                                                    uint32_t* tot) {
     const uint32_t q = blockIdx.x;
     __shared__ uint32_t s;
     if (threadIdx.x == 0) s = 0;
     __syncthreads();
-    uint32_t* hdr = reinterpret_cast<uint32_t*>(idx_tab[q]);
+    uint32_t* hdr = reinterpret_cast<uint32_t*>(idx_tab ? idx_tab[q] : idx_base + uint64_t(q) * idx_stride);
     for (uint32_t b = threadIdx.x; b < C; b += blockDim.x) {
         const uint32_t c = min(fill[q * C + b], cap_b);
         __hip_atomic_store(hdr + b, c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -215,7 +223,10 @@ struct BFineK {
     const uint8_t* idx[kBucketMaxSrc];   // source s's index area (header + slices), this chunk's parity
     const uint8_t* val[kBucketMaxSrc];   // null: the source's scalar sbits[s]
     uint64_t sbits[kBucketMaxSrc];
-    uint32_t S, C, cap_b, T;
+    uint32_t cap_b[kBucketMaxSrc];       // source s's slice capacity (records)
+    uint32_t S, C, T;
+    int cshift;                          // bucket b's elements start at b << cshift (k_bucket_direct)
+    uint64_t shard_len;
     uint32_t tpb;                        // tiles per bucket (a power of two, <= kBTilesPerBucket)
     int tile_shift;
     uint64_t cap_t;                      // records per fixed tile region
@@ -243,6 +254,7 @@ __global__ __launch_bounds__(1024) void k_fine_bucket(BFineK p) {
     __shared__ const uint8_t* s_ib[kBucketMaxSrc];
     __shared__ const uint8_t* s_vb[kBucketMaxSrc];
     __shared__ uint64_t s_sb[kBucketMaxSrc];
+    __shared__ uint32_t s_cb[kBucketMaxSrc];
     const uint32_t S = p.S, C = p.C, nseg = C * S;
     // the sources' areas in LDS: indexing the kernel-argument arrays by a per-lane source put two
     // dependent global loads (the pointers) in front of every record's loads
@@ -250,11 +262,13 @@ __global__ __launch_bounds__(1024) void k_fine_bucket(BFineK p) {
         s_ib[threadIdx.x] = p.idx[threadIdx.x] ? p.idx[threadIdx.x] + kBucketHdr : nullptr;
         s_vb[threadIdx.x] = p.val[threadIdx.x];
         s_sb[threadIdx.x] = p.sbits[threadIdx.x];
+        s_cb[threadIdx.x] = p.cap_b[threadIdx.x];
     }
+    __syncthreads();
     // segment (b, s) = virtual records [s_vs[b * S + s], s_vs[b * S + s + 1])
     for (uint32_t x = threadIdx.x; x < nseg; x += kBT) {
         const uint32_t b = x / S, s = x - b * S;
-        s_vs[x] = p.idx[s] ? min(reinterpret_cast<const uint32_t*>(p.idx[s])[b], p.cap_b) : 0u;
+        s_vs[x] = p.idx[s] ? min(reinterpret_cast<const uint32_t*>(p.idx[s])[b], s_cb[s]) : 0u;
     }
     __syncthreads();
     {   // in-place exclusive scan (one thread per up-to-two entries)
@@ -298,7 +312,7 @@ __global__ __launch_bounds__(1024) void k_fine_bucket(BFineK p) {
             if (v < e) {
                 while (v >= s_vs[k + 1]) k++;
                 const uint32_t s = k - b * S;
-                const uint64_t slot = uint64_t(b) * p.cap_b + (v - s_vs[k]);
+                const uint64_t slot = uint64_t(b) * s_cb[s] + (v - s_vs[k]);
                 li[j] = as_global(reinterpret_cast<const uint32_t*>(s_ib[s]))[slot];
                 const V* vb = reinterpret_cast<const V*>(s_vb[s]);
                 vv[j] = vb ? as_global(vb)[slot] : V(s_sb[s]);
@@ -395,6 +409,29 @@ __global__ __launch_bounds__(1024) void k_fine_bucket(BFineK p) {
     if (oob) raise_err(p.err, LMR_ERRBIT_OOB);
 }
 
+// an owner without a session workspace: every source's slices applied with device atomics (the
+// mode's ops are order-insensitive); one (source, bucket) slice per block iteration
+template <int VB>
+__global__ __launch_bounds__(256) void k_bucket_direct(BFineK p) {
+    using V = typename idx_t<VB>::I;
+    bool oob = false;
+    for (uint32_t sb = blockIdx.x; sb < p.S * p.C; sb += gridDim.x) {
+        const uint32_t s = sb % p.S, b = sb / p.S;
+        if (!p.idx[s]) continue;
+        const uint32_t cnt = min(reinterpret_cast<const uint32_t*>(p.idx[s])[b], p.cap_b[s]);
+        const uint32_t* off = reinterpret_cast<const uint32_t*>(p.idx[s] + kBucketHdr) + uint64_t(b) * p.cap_b[s];
+        const V* val = p.val[s] ? reinterpret_cast<const V*>(p.val[s]) + uint64_t(b) * p.cap_b[s] : nullptr;
+        for (uint32_t i = threadIdx.x; i < cnt; i += blockDim.x) {
+            const uint64_t e = (uint64_t(b) << p.cshift) + off[i];
+            if (e >= p.shard_len) { oob = true; continue; }
+            uint8_t okf;
+            rmw_global<V>(reinterpret_cast<V*>(p.shard) + e, p.op, LMR_KIND_NATIVE_ATOMIC, val ? val[i] : V(p.sbits[s]),
+                          V(0), V(0), okf, p.err);
+        }
+    }
+    if (oob) raise_err(p.err, LMR_ERRBIT_OOB);
+}
+
 __global__ void k_bucket_plan(uint32_t* tfill, uint32_t T, uint64_t cap_t, TileItem* items) {
     const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= T) return;
@@ -444,6 +481,12 @@ bool bucket_geometry(const lmr_layout_t& L, int dtype, uint32_t& C, int& cshift)
     return uint64_t(C) * L.num_pes <= kBucketMaxKeys && uint64_t(C) * 4 <= kBucketHdr;
 }
 
+bool bucket_op_ok(int dtype, int op) {
+    return dtype_bytes(dtype) > 0 && dtype <= LMR_I64 &&
+           (op == LMR_OP_ADD || op == LMR_OP_SUB || op == LMR_OP_MUL || op == LMR_OP_AND || op == LMR_OP_OR ||
+            op == LMR_OP_XOR);
+}
+
 uint32_t bucket_slice_cap(uint64_t R, uint32_t C, uint32_t eb) {
     if (C == 0 || R * 8 <= kBucketHdr) return 0;
     const uint64_t a = (R * 8 - kBucketHdr) / (uint64_t(C) * 4);
@@ -454,7 +497,7 @@ uint32_t bucket_slice_cap(uint64_t R, uint32_t C, uint32_t eb) {
 hipError_t launch_pack_bucket(const PackArgs& a, uint32_t C, int cshift, uint32_t cap_b, uint32_t* fill,
                               uint32_t* tot, hipStream_t s) {
     const uint32_t npes = a.layout.num_pes;
-    if (!a.out_idx_tab || npes == 0 || npes > kBucketMaxSrc || uint64_t(C) * npes > kBucketMaxKeys)
+    if ((!a.out_idx_tab && !a.out_idx) || npes == 0 || npes > kBucketMaxSrc || uint64_t(C) * npes > kBucketMaxKeys)
         return hipErrorInvalidValue;
     uint64_t G = (a.n + 65535) / 65536;
     G = std::max<uint64_t>(1, std::min<uint64_t>(G, kMaxBinBlocks));
@@ -471,6 +514,10 @@ hipError_t launch_pack_bucket(const PackArgs& a, uint32_t C, int cshift, uint32_
     p.cshift = cshift;
     p.idx_tab = a.out_idx_tab;
     p.val_tab = a.vals ? a.out_vals_tab : nullptr;
+    p.idx_base = a.out_idx;
+    p.val_base = a.vals ? a.out_vals : nullptr;
+    p.idx_stride = kBucketHdr + uint64_t(C) * cap_b * 4;           // (send-buffer layout, bucket_region_bytes)
+    p.val_stride = uint64_t(C) * cap_b * (a.vals ? a.val_bytes : 0);
     p.fill = fill;
     p.ovf_gidx = a.ovf_gidx;
     p.ovf_vals = a.ovf_vals;
@@ -509,7 +556,8 @@ hipError_t launch_pack_bucket(const PackArgs& a, uint32_t C, int cshift, uint32_
         });
         if (e != hipSuccess) return e;
     }
-    hipLaunchKernelGGL(k_bucket_hdr, dim3(npes), dim3(256), 0, s, fill, C, cap_b, a.out_idx_tab, tot);
+    hipLaunchKernelGGL(k_bucket_hdr, dim3(npes), dim3(256), 0, s, fill, C, cap_b, a.out_idx_tab, a.out_idx, p.idx_stride,
+                       tot);
     return hipGetLastError();
 }
 
@@ -526,10 +574,10 @@ hipError_t launch_fine_bucket(const BucketChunk& c, const BucketSession& bs, con
         p.idx[s] = c.idx[s];
         p.val[s] = c.val[s];
         p.sbits[s] = c.sbits[s];
+        p.cap_b[s] = c.cap_b[s];
     }
     p.S = c.S;
     p.C = bs.C;
-    p.cap_b = c.cap_b;
     p.T = bs.T;
     p.tpb = 1u << bs.tpb_log2;
     p.tile_shift = tile_shift(int(bs.desc.dtype));
@@ -549,6 +597,32 @@ hipError_t launch_fine_bucket(const BucketChunk& c, const BucketSession& bs, con
         return hipGetLastError();
     });
 }
+
+hipError_t launch_bucket_direct(const BucketChunk& c, const lmr_apply_desc_t& d, uint32_t C, int cshift, uint32_t* err,
+                                hipStream_t st) {
+    if (c.S == 0 || c.S > kBucketMaxSrc) return hipErrorInvalidValue;
+    BFineK p{};
+    for (uint32_t s = 0; s < c.S; s++) {
+        p.idx[s] = c.idx[s];
+        p.val[s] = c.val[s];
+        p.sbits[s] = c.sbits[s];
+        p.cap_b[s] = c.cap_b[s];
+    }
+    p.S = c.S;
+    p.C = C;
+    p.cshift = cshift;
+    p.shard = d.shard;
+    p.shard_len = d.shard_len;
+    p.op = int(d.op);
+    p.err = err;
+    return bdispatch_vb(dtype_bytes(int(d.dtype)), [&](auto vbt) {
+        constexpr int VB = decltype(vbt)::value;
+        hipLaunchKernelGGL((k_bucket_direct<VB>), dim3(2048), dim3(256), 0, st, p);
+        return hipGetLastError();
+    });
+}
+
+uint64_t bucket_region_idx_bytes(uint32_t C, uint32_t cap_b) { return kBucketHdr + uint64_t(C) * cap_b * 4; }
 
 hipError_t launch_bucket_sweep(BucketSession& bs, const TiledWs& w, hipStream_t st) {
     hipError_t e = hipSuccess;

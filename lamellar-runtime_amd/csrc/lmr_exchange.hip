@@ -678,12 +678,6 @@ lmr_status_t lmr_batch_exchange(lmr_ctx_t* ctx, const lmr_transport_t* tp, const
         if (x->tfill.need(size_t(kMaxTiles) * 4 + 8, x) != hipSuccess) return xfail(__LINE__);
         x->tfill_zero = false;
     }
-    if (free_pack) {
-        const uint32_t nb = my_bucket ? npes * bC : 0u, nt = std::max(npes, nb);
-        hipLaunchKernelGGL(k_xbegin, dim3((nt + 255) / 256), dim3(256), 0, x->sp, x->fill.as<uint32_t>(), npes,
-                           x->bfill.as<uint32_t>(), nb, x->ovf_count.as<uint32_t>());
-        if (hipGetLastError() != hipSuccess) return xfail(__LINE__);
-    }
     // a failed exchange closes the session (its staged records are dropped) so the context
     // stays usable; the work already enqueued on the internal streams drains first (after a
     // transport failure the transport is aborted first: peers may never post their halves)
@@ -731,6 +725,20 @@ lmr_status_t lmr_batch_exchange(lmr_ctx_t* ctx, const lmr_transport_t* tp, const
         if (x->recv_used[b] && hipStreamWaitEvent(x->sp, x->ev_recv_free[b], 0) != hipSuccess) return xfail(__LINE__);
         return LMR_OK;
     };
+    // the collective exchange's bucketed regions (rb): the push's layout -- per owner a header of
+    // slice counts, then C slices of bucket offsets -- in the send buffer, sent whole by the
+    // transport, binned by the owner without a coarse pass. Decided from inputs every PE has alike
+    // (the environment, the layout, the op), so every FIXED sender packs them or none does.
+    bool rb = false;
+    uint32_t rC = 0;
+    int rshift = 0;
+    // slice capacity of a sender's chunk j (records m, chunk size ch): 0 past its last chunk
+    auto rcb_of = [&](uint64_t mm, uint64_t ch, uint64_t j) -> uint32_t {
+        if (ch == 0 || j * ch >= mm || rC == 0) return 0;
+        const uint64_t c = std::min(ch, mm - j * ch);
+        const uint64_t per = (c + uint64_t(npes) * rC - 1) / (uint64_t(npes) * rC);
+        return uint32_t(per + per / 8 + 256);
+    };
     auto pack_chunk = [&](uint64_t j) -> lmr_status_t {
         const uint64_t lo = chunk_lo(j), cnt = chunk_hi(j) - lo;
         const int b = int(j & 1);
@@ -740,7 +748,31 @@ lmr_status_t lmr_batch_exchange(lmr_ctx_t* ctx, const lmr_transport_t* tp, const
         if (returning && x->pos.size() <= j) x->pos.resize(j + 1);
         if (packed) {
             if (returning && x->pos[j].need(cnt * 4 + 8, x) != hipSuccess) return xfail(__LINE__);
-            if (free_pack) {
+            if (rb) {
+                // fixed regions laid out by owner bucket, back to back in send buffer b (sent whole)
+                PackArgs pa;
+                pa.layout = *layout;
+                pa.gidx = gidx + lo;
+                pa.vals = scalar ? nullptr : static_cast<const uint8_t*>(d_vals) + lo * eb;
+                pa.val_bytes = eb;
+                pa.n = cnt;
+                pa.index_size = iw;
+                pa.out_idx = x->send_idx[b].as<uint8_t>();
+                pa.out_vals = scalar ? nullptr : x->send_vals[b].as<uint8_t>();
+                pa.out_pos = nullptr;
+                pa.dest_counts = nullptr;
+                pa.dest_offsets = nullptr;
+                pa.err = ctx->d_err;
+                pa.prof = ctx->prof;
+                pa.stable = false;
+                pa.ovf_gidx = x->ovf_idx.as<uint64_t>();
+                pa.ovf_vals = scalar ? nullptr : x->ovf_vals.as<uint8_t>();
+                pa.ovf_count = x->ovf_count.as<uint32_t>();
+                pa.ovf_cap = m;
+                if (launch_pack_bucket(pa, rC, rshift, rcb_of(m, chunk, j), x->bfill.as<uint32_t>(),
+                                       x->btot.as<uint32_t>(), x->sp) != hipSuccess)
+                    return xfail(__LINE__);
+            } else if (free_pack) {
                 PackArgs pa;
                 pa.layout = *layout;
                 pa.gidx = gidx + lo;
@@ -768,8 +800,10 @@ lmr_status_t lmr_batch_exchange(lmr_ctx_t* ctx, const lmr_transport_t* tp, const
                 if (e != LMR_OK) return e;
             }
         }
-        hipLaunchKernelGGL(k_xhdr, dim3((npes + 255) / 256), dim3(256), 0, x->sp, packed ? x->counts.as<uint64_t>() : nullptr,
-                           npes, mvsi && j == 0 ? mvsi_pe : -1, mvsi_off, int64_t(n), my_flags, sbits, int64_t(my_k),
+        // (bucketed regions: no counts in the rows, the slice counts travel in each region's header)
+        hipLaunchKernelGGL(k_xhdr, dim3((npes + 255) / 256), dim3(256), 0, x->sp,
+                           packed && !rb ? x->counts.as<uint64_t>() : nullptr, npes, mvsi && j == 0 ? mvsi_pe : -1,
+                           mvsi_off, int64_t(n), my_flags | (rb ? int64_t(LMR_XHDR_BUCKETS) : 0), sbits, int64_t(my_k),
                            int64_t(m), int64_t(chunk), x->hdr_send[b].as<int64_t>(),
                            free_pack ? x->ovf_count.as<uint32_t>() : nullptr);
         if (hipGetLastError() != hipSuccess) return xfail(__LINE__);
@@ -804,6 +838,7 @@ lmr_status_t lmr_batch_exchange(lmr_ctx_t* ctx, const lmr_transport_t* tp, const
     // ---- owner side with host counts (apply stream): stage every source's records of receive
     // buffer b (counts cnt[p]; own records from send buffer b at the given offsets when bypassed)
     bool bucketed = false;                       // (the peer push's bucketed mode, agreed at the handshake)
+    bool bsess = false;                          // (this batch's owner records go to the bucketed session)
     auto stage_host = [&](int b, const int64_t* h_recv, const std::vector<uint64_t>& cnt, uint64_t self_io,
                           uint64_t self_vo, const uint8_t* send_vals, uint64_t j) -> lmr_status_t {
         uint64_t io = 0, vo = 0, ro = 0;
@@ -844,10 +879,10 @@ lmr_status_t lmr_batch_exchange(lmr_ctx_t* ctx, const lmr_transport_t* tp, const
                 if (own) break;
             }
             const uint64_t ubits = uint64_t(bits);
-            if (ord || bucketed) {
+            if (ord || bsess || rb) {
                 // applied now: an ordered stream each element's records in stream order; in the
-                // bucketed mode (the overflow round: order-insensitive records, whose workspace
-                // holds the session's tile regions) with device atomics
+                // bucketed modes (the overflow round: order-insensitive records, whose workspace
+                // holds the session's tile regions, or an owner without one) with device atomics
                 lmr_apply_desc_t d = *desc;
                 d.strategy = ord ? LMR_STRATEGY_ORDERED : LMR_STRATEGY_DIRECT;
                 e = lmr_apply_soa(ctx, &d, src_i, iw, sc ? nullptr : src_v, sc ? &ubits : nullptr, tot, res, okp, sa);
@@ -889,10 +924,41 @@ lmr_status_t lmr_batch_exchange(lmr_ctx_t* ctx, const lmr_transport_t* tp, const
         for (uint32_t p = 0; p < npes; p++)
             bucketed = bucketed && pi[size_t(p) * 8 + 6] == my_binfo && pi[size_t(p) * 8 + 7] == int64_t(bshift);
     }
+    rb = !push && free_pack && fixed_mode_enabled() && bucket_mode_enabled() &&
+         bucket_op_ok(int(desc->dtype), int(desc->op)) && npes <= kBucketMaxSrc &&
+         bucket_geometry(*layout, int(desc->dtype), rC, rshift);
+    if (!rb) rC = 0;
+    // this PE binds bucketed regions into a session when it has the workspace for one (else each
+    // chunk's slices are applied with device atomics, launch_bucket_direct)
+    const int ts_ = tile_shift(int(desc->dtype));
+    const uint64_t my_tiles_ = (desc->shard_len + (uint64_t(1) << ts_) - 1) >> ts_;
+    const bool owner_ok = rb && ctx->ws && ctx->rec_cap > 0 && my_tiles_ > 0 &&
+                          my_tiles_ <= (uint64_t(rC) << bucket_tpb_log2());
+    bsess = bucketed || owner_ok;
+    const uint32_t uC = bucketed ? bC : rC;
+    if (rb) {
+        const uint32_t cb0 = rcb_of(m, chunk, 0);
+        for (int b = 0; b < 2; b++)
+            if (x->send_idx[b].need(size_t(npes) * bucket_region_idx_bytes(rC, cb0) + 8, x) != hipSuccess ||
+                x->send_vals[b].need(size_t(npes) * rC * cb0 * eb + 8, x) != hipSuccess)
+                return xfail(__LINE__);
+        if (x->bfill.need(size_t(npes) * rC * 4 + 8, x) != hipSuccess || x->btot.need(size_t(npes) * 4 + 8, x) != hipSuccess)
+            return xfail(__LINE__);
+    }
+    if (owner_ok && !x->tfill.p) {
+        if (x->tfill.need(size_t(kMaxTiles) * 4 + 8, x) != hipSuccess) return xfail(__LINE__);
+        x->tfill_zero = false;
+    }
+    if (free_pack) {   // (the pack's fill counters and the overflow count: zero at batch start)
+        const uint32_t nb = bucketed ? npes * bC : (rb ? npes * rC : 0u), nt = std::max(npes, nb);
+        hipLaunchKernelGGL(k_xbegin, dim3((nt + 255) / 256), dim3(256), 0, x->sp, x->fill.as<uint32_t>(), npes,
+                           x->bfill.as<uint32_t>(), nb, x->ovf_count.as<uint32_t>());
+        if (hipGetLastError() != hipSuccess) return xfail(__LINE__);
+    }
     // the bucketed session and the staged one both keep records in the workspace's temp arrays:
     // whichever this batch does not use is applied first
-    if (!bucketed && bucket_sweep(ctx, x, x->sa) != hipSuccess) return xfail(__LINE__);
-    if (bucketed && !stage_session_empty(ctx)) {
+    if (!bsess && bucket_sweep(ctx, x, x->sa) != hipSuccess) return xfail(__LINE__);
+    if (bsess && !stage_session_empty(ctx)) {
         if ((st = lmr_stage_finish(ctx, reinterpret_cast<lmr_stream_t>(x->sa))) != LMR_OK) return st;
         if ((st = lmr_stage_begin(ctx, desc)) != LMR_OK) return st;
     }
@@ -902,7 +968,7 @@ lmr_status_t lmr_batch_exchange(lmr_ctx_t* ctx, const lmr_transport_t* tp, const
         const int ts = tile_shift(int(desc->dtype));
         const TiledWs w = carve_tiled_ws(ctx->ws, ctx->rec_cap);
         bs.desc = *desc;
-        bs.C = bC;
+        bs.C = uC;
         bs.tpb_log2 = bucket_tpb_log2();
         bs.T = uint32_t((desc->shard_len + (uint64_t(1) << ts) - 1) >> ts);
         bs.cap_t = std::min<uint64_t>(w.tmp_cap, 0xFFFFFFFFull) / bs.T;
@@ -974,7 +1040,6 @@ lmr_status_t lmr_batch_exchange(lmr_ctx_t* ctx, const lmr_transport_t* tp, const
                 // every source's bucket slices binned into the session's tile regions in one launch
                 BucketChunk c;
                 c.S = npes;
-                c.cap_b = bcap;
                 for (uint32_t p = 0; p < npes; p++) {
                     const uint64_t cap = cap_of(uint64_t(std::max<int64_t>(src_m[p], 0)),
                                                 uint64_t(std::max<int64_t>(src_ch[p], 0)), j);
@@ -984,6 +1049,7 @@ lmr_status_t lmr_batch_exchange(lmr_ctx_t* ctx, const lmr_transport_t* tp, const
                     c.idx[p] = peer_recv_idx(peer, p, b);
                     c.val[p] = sc ? nullptr : peer_recv_vals(peer, p, b);
                     c.sbits[p] = uint64_t(src_bits[p]);
+                    c.cap_b[p] = bcap;
                     c.expect += (std::min(ch, uint64_t(std::max<int64_t>(src_m[p], 0))) + npes - 1) / npes;
                 }
                 if (c.expect > 0) {
@@ -1040,7 +1106,11 @@ lmr_status_t lmr_batch_exchange(lmr_ctx_t* ctx, const lmr_transport_t* tp, const
                     src_m[p] = r[5];
                     src_ch[p] = r[6];
                     any_fixed = any_fixed || (r[2] & LMR_XHDR_FIXED);
-                    nowait = nowait && (r[2] & LMR_XHDR_FIXED) && (r[2] & LMR_XHDR_DEVCOUNT);
+                    // (bucketed regions need no device counts: every PE takes them, session or not)
+                    nowait = nowait && (r[2] & LMR_XHDR_FIXED) && (r[2] & (LMR_XHDR_DEVCOUNT | LMR_XHDR_BUCKETS));
+                    // every FIXED sender packs bucketed regions or none does (the same inputs on every
+                    // PE, LAMELLAR_EXCHANGE_BUCKETS included): anything else is a configuration error
+                    if ((r[2] & LMR_XHDR_FIXED) && bool(r[2] & LMR_XHDR_BUCKETS) != rb) return LMR_E_INVALID;
                 }
             }
         }
@@ -1054,6 +1124,23 @@ lmr_status_t lmr_batch_exchange(lmr_ctx_t* ctx, const lmr_transport_t* tp, const
         for (uint32_t p = 0; p < npes; p++)
             if (src_fl[p] & LMR_XHDR_FIXED) capr[p] = cap_of(uint64_t(std::max<int64_t>(src_m[p], 0)),
                                                           uint64_t(std::max<int64_t>(src_ch[p], 0)), j);
+        // bucketed regions: whole, index area header + C slices of u32, values C slices
+        const uint32_t my_cb = rb ? rcb_of(m, chunk, j) : 0;
+        std::vector<uint32_t> rcb(npes, 0);
+        for (uint32_t p = 0; p < npes; p++)
+            if (src_fl[p] & LMR_XHDR_BUCKETS)
+                rcb[p] = rcb_of(uint64_t(std::max<int64_t>(src_m[p], 0)), uint64_t(std::max<int64_t>(src_ch[p], 0)), j);
+        const uint64_t my_rib = my_cb ? bucket_region_idx_bytes(rC, my_cb) : 0, my_rvb = uint64_t(rC) * my_cb * eb;
+        auto send_bucketed = [&](uint32_t p) {          // this PE's whole region for PE p
+            isb[p] = my_rib;
+            iso[p] = uint64_t(p) * my_rib;
+            vsb[p] = scalar ? 0 : my_rvb;
+            vso[p] = scalar ? 0 : uint64_t(p) * my_rvb;
+        };
+        auto recv_bucketed = [&](uint32_t p) {          // PE p's whole region for this PE
+            irb[p] = rcb[p] ? bucket_region_idx_bytes(rC, rcb[p]) : 0;
+            vrb[p] = (src_fl[p] & LMR_XHDR_SCALAR) ? 0 : uint64_t(rC) * rcb[p] * eb;
+        };
         if (nowait) {
             // whole fixed regions both ways: every size follows from chunk 0's rows
             uint64_t a = 0, c = 0;
@@ -1063,8 +1150,10 @@ lmr_status_t lmr_batch_exchange(lmr_ctx_t* ctx, const lmr_transport_t* tp, const
                 vsb[p] = scalar ? 0 : my_cap * eb;
                 vso[p] = scalar ? 0 : uint64_t(p) * my_cap * eb;
                 irb[p] = capr[p] * iw;
-                iro[p] = a; a += irb[p];
                 vrb[p] = (src_fl[p] & LMR_XHDR_SCALAR) ? 0 : capr[p] * eb;
+                if (rb) send_bucketed(p);
+                if (src_fl[p] & LMR_XHDR_BUCKETS) recv_bucketed(p);
+                iro[p] = a; a += irb[p];
                 vro[p] = c; c += vrb[p];
             }
         } else {
@@ -1086,6 +1175,11 @@ lmr_status_t lmr_batch_exchange(lmr_ctx_t* ctx, const lmr_transport_t* tp, const
                     vrb[p] = (h_recv[p * LMR_XHDR_WORDS + 2] & LMR_XHDR_SCALAR) ? 0 : r1 * eb;
                 }
                 cnt[p] = (h_recv[p * LMR_XHDR_WORDS + 2] & LMR_XHDR_FIXED) ? std::min(rc_, capr[p]) : rc_;
+                if (rb && j < my_k && hi > lo) send_bucketed(p);
+                if (src_fl[p] & LMR_XHDR_BUCKETS) {
+                    recv_bucketed(p);
+                    cnt[p] = 0;                          // (the owner reads the region's header)
+                }
             }
             uint64_t a = 0, c = 0;
             for (uint32_t p = 0; p < npes; p++) {
@@ -1117,8 +1211,9 @@ lmr_status_t lmr_batch_exchange(lmr_ctx_t* ctx, const lmr_transport_t* tp, const
         // the records after the chunk's header rows (and so after its pack): with no host read of
         // the rows in between, only this orders them (and the owner's staging, which reads the rows)
         if (nowait && hipStreamWaitEvent(x->sx, x->ev_hdr[b], 0) != hipSuccess) return xfail(__LINE__);
+        // (bucketed regions are u32 areas: the index unit divides both them and iw-wide segments)
         st = tp_alltoallv(tp, x, x->send_idx[b].p, isb.data(), iso.data(), x->recv_idx[b].p, irb.data(), iro.data(),
-                          unit_for(iw), x->sx);
+                          rb ? std::min<uint32_t>(4, unit_for(iw)) : unit_for(iw), x->sx);
         if (st == LMR_OK)
             st = tp_alltoallv(tp, x, send_vals, vsb.data(), vso.data(), x->recv_vals[b].p, vrb.data(), vro.data(),
                               unit_for(eb), x->sx);
@@ -1133,12 +1228,41 @@ lmr_status_t lmr_batch_exchange(lmr_ctx_t* ctx, const lmr_transport_t* tp, const
             if (x->res[j].need(cr.total * eb + 8, x) != hipSuccess) return xfail(__LINE__);
             if (want_ok && x->rok[j].need(cr.total + 8, x) != hipSuccess) return xfail(__LINE__);
         }
+        // bucketed regions: every source's slices binned in one launch (or applied directly)
+        {
+            BucketChunk c;
+            c.S = npes;
+            bool any = false;
+            for (uint32_t p = 0; p < npes; p++) {
+                if (!(src_fl[p] & LMR_XHDR_BUCKETS) || rcb[p] == 0) continue;
+                const bool own = bypass && p == me;
+                const bool sc = (src_fl[p] & LMR_XHDR_SCALAR) != 0;
+                c.idx[p] = own ? x->send_idx[b].as<uint8_t>() + self_io : x->recv_idx[b].as<uint8_t>() + iro[p];
+                c.val[p] = sc ? nullptr : own ? send_vals + self_vo : x->recv_vals[b].as<uint8_t>() + vro[p];
+                c.sbits[p] = uint64_t(src_bits[p]);
+                c.cap_b[p] = rcb[p];
+                const uint64_t ch = uint64_t(std::max<int64_t>(src_ch[p], 1));
+                c.expect += (std::min(ch, uint64_t(std::max<int64_t>(src_m[p], 0))) + npes - 1) / npes;
+                any = true;
+            }
+            if (any && bsess) {
+                if (x->bs.open && x->bs.staged + c.expect > bucket_session_limit(x->bs) &&
+                    bucket_sweep(ctx, x, x->sa) != hipSuccess)
+                    return xfail(__LINE__);
+                if (!bucket_open()) return xfail(__LINE__);
+                TiledWs w = carve_tiled_ws(ctx->ws, ctx->rec_cap);
+                if (launch_fine_bucket(c, x->bs, w, x->sa) != hipSuccess) return xfail(__LINE__);
+                x->bs.staged += c.expect;
+            } else if (any && launch_bucket_direct(c, *desc, rC, rshift, ctx->d_err, x->sa) != hipSuccess) {
+                return xfail(__LINE__);
+            }
+        }
         if (nowait) {
             // fixed regions with their counts in the header rows (device), each its own stream
             for (uint32_t p = 0; p < npes; p++) {
                 const bool own = bypass && p == me;
                 const uint64_t cap = own ? my_cap : capr[p];
-                if (cap == 0) continue;
+                if (cap == 0 || (src_fl[p] & LMR_XHDR_BUCKETS)) continue;
                 const uint8_t* src_i = own ? x->send_idx[b].as<uint8_t>() + self_io : x->recv_idx[b].as<uint8_t>() + iro[p];
                 const bool sc = (src_fl[p] & LMR_XHDR_SCALAR) != 0;
                 const uint8_t* src_v = sc ? nullptr : own ? send_vals + self_vo : x->recv_vals[b].as<uint8_t>() + vro[p];

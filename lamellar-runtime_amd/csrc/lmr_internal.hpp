@@ -361,7 +361,8 @@ struct BucketSession {
     Prof* prof = nullptr;
 };
 struct BucketChunk {
-    uint32_t S = 0, cap_b = 0;
+    uint32_t S = 0;
+    uint32_t cap_b[kBucketMaxSrc] = {};        // source s's slice capacity (records)
     const uint8_t* idx[kBucketMaxSrc] = {};   // source s's index area this chunk (null: nothing from s)
     const uint8_t* val[kBucketMaxSrc] = {};   // null: the scalar sbits[s]
     uint64_t sbits[kBucketMaxSrc] = {};
@@ -369,16 +370,26 @@ struct BucketChunk {
 };
 // buckets of the layout's largest shard (false: the layout / element type cannot take the mode)
 int bucket_tpb_log2();
+// integer ops whose records commute (any split and order gives the same shard): the mode's ops
+bool bucket_op_ok(int dtype, int op);
 bool bucket_geometry(const lmr_layout_t& L, int dtype, uint32_t& C, int& cshift);
 // records per bucket slice of a receive region of R records (8 bytes each, index and value areas)
 uint32_t bucket_slice_cap(uint64_t R, uint32_t C, uint32_t eb);
-// the sender's pack of one chunk (a.out_idx_tab / out_vals_tab: the owners' regions) and the slice
+// the sender's pack of one chunk (a.out_idx_tab / out_vals_tab: the owners' regions; or, with no
+// table, a.out_idx / a.out_vals holding the owners' areas back to back, bucket_region_idx_bytes and
+// C * cap_b * value bytes apart) and the slice
 // counts into the owners' region headers; tot[q]: records written for owner q
 hipError_t launch_pack_bucket(const PackArgs& a, uint32_t C, int cshift, uint32_t cap_b, uint32_t* fill,
                               uint32_t* tot, hipStream_t s);
 // largest session (records) the fixed tile regions take with headroom
 uint64_t bucket_session_limit(const BucketSession& bs);
 hipError_t launch_fine_bucket(const BucketChunk& c, const BucketSession& bs, const TiledWs& w, hipStream_t st);
+// an owner without a session workspace: the chunk's slices applied with device atomics
+hipError_t launch_bucket_direct(const BucketChunk& c, const lmr_apply_desc_t& d, uint32_t C, int cshift, uint32_t* err,
+                                hipStream_t st);
+// bytes of a bucketed index area: the slice-count header and C slices of cap_b u32 offsets (values:
+// C * cap_b * value bytes)
+uint64_t bucket_region_idx_bytes(uint32_t C, uint32_t cap_b);
 hipError_t launch_bucket_sweep(BucketSession& bs, const TiledWs& w, hipStream_t st);
 constexpr int kReduceBlocks = 1024;
 hipError_t launch_reduce(int dtype, int op, const void* x, uint64_t n, uint64_t* out, uint8_t* has,

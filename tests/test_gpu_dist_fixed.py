@@ -98,9 +98,11 @@ def _expected(pe, n_len):
                          [(1, "nccl", "1", ""), (2, "gloo", "1", ""), (3, "gloo", "1", ""), (2, "gloo", "0", ""),
                           (1, "nccl", "1", "peer"), (2, "gloo", "1", "peer"), (3, "gloo", "1", "peer"),
                           (1, "nccl", "1", "peer-buckets"), (2, "gloo", "1", "peer-buckets"),
-                          (3, "gloo", "1", "peer-buckets")],
+                          (3, "gloo", "1", "peer-buckets"), (1, "nccl", "1", "rb"), (2, "gloo", "1", "rb"),
+                          (3, "gloo", "1", "rb")],
                          ids=["rccl-1rank", "gloo-2pe", "gloo-3pe", "gloo-2pe-hostcounts",
-                              "peer-1rank", "peer-2pe", "peer-3pe", "buckets-1rank", "buckets-2pe", "buckets-3pe"])
+                              "peer-1rank", "peer-2pe", "peer-3pe", "buckets-1rank", "buckets-2pe", "buckets-3pe",
+                              "rb-rccl-1rank", "rb-gloo-2pe", "rb-gloo-3pe"])
 def test_fixed_region_exchange(ws, backend, fixed, transport):
     """transport=peer: lmr_transport_peer_create over the base transport -- every batch here is
     pushed (the sender's pack writes into the owners' IPC-mapped regions; counts and sequence
@@ -108,10 +110,13 @@ def test_fixed_region_exchange(ws, backend, fixed, transport):
     peer-buckets: the push's bucketed mode (LAMELLAR_EXCHANGE_BUCKETS=1: the sender packs by
     (owner, owner bucket of 128 tiles) into bucket slices, the owner bins them straight into its
     session's tile regions); the skewed batch overflows its slices (overflow round, applied with
-    device atomics)."""
-    buckets = transport == "peer-buckets"
-    if buckets:
+    device atomics). rb: the same bucketed regions over the collective transport (RCCL / gloo):
+    sent whole by the all-to-all-v, binned by the owner without a coarse pass."""
+    buckets = transport in ("peer-buckets", "rb")
+    if transport == "peer-buckets":
         transport = "peer"
+    elif transport == "rb":
+        transport = ""
     env = {"LAMELLAR_COMM_BACKEND": backend, "LAMELLAR_EXCHANGE_FIXED": fixed, "LAMELLAR_TRANSPORT": transport,
            "LAMELLAR_PEER_TIMEOUT": "60", "LAMELLAR_EXCHANGE_BUCKETS": "1" if buckets else "0"}
     if ws == 1:

@@ -148,10 +148,10 @@ int main(int argc, char** argv) {
     auto fine = [&](Regions& r, hipStream_t s) {
         BucketChunk c;
         c.S = npes;
-        c.cap_b = cap_b;
         for (uint32_t p = 0; p < npes; p++) {
             c.idx[p] = r.idx[p];
             c.val[p] = r.val[p];
+            c.cap_b[p] = cap_b;
         }
         c.expect = n;
         CK(launch_fine_bucket(c, bs, w, s));
