@@ -28,20 +28,22 @@ STAGES = {
                      "k_wide_stage"),
                     ("k_coarse_free", "k_coarse_scatter", "k_coarse_offsets", "k_bin_scatter", "k_coarse_stage",
                      "k_coarse_free_stage", "k_wide_stage")),
-    "fine_scatter": (("k_fine_free", "k_fine_scatter", "k_fine_piece", "k_fine_stage"),
+    "fine_scatter": (("k_fine_free", "k_fine_scatter", "k_fine_piece", "k_fine_stage", "k_fine_bucket"),
                      ("k_fine_free", "k_fine_scatter", "k_fine_piece", "k_piece_count", "k_free_tile_totals",
-                      "k_fine_stage")),
-    "tile_apply": (("k_tile_owner",), ("k_tile_owner", "k_tile_delta", "k_tile_plan", "k_stage_plan")),
+                      "k_fine_stage", "k_fine_bucket")),
+    "tile_apply": (("k_tile_owner",), ("k_tile_owner", "k_tile_delta", "k_tile_plan", "k_stage_plan", "k_bucket_plan")),
     "unpartition": (("k_tile_owner",), ("k_unpartition", "k_unpartition_multi", "k_unpart_rounds",
                                         "k_unpart_crounds", "k_unpart_wide")),
     "direct": (("k_apply_direct",), ("k_apply_direct",)),
-    "pack": (("k_pack_count", "k_pack_stage"), ("k_pack_count", "k_pack_scatter", "k_pack_stage", "k_dest_offsets",
-                                                 "k_fill_counts")),
+    "pack": (("k_pack_count", "k_pack_stage", "k_pack_bucket"),
+             ("k_pack_count", "k_pack_scatter", "k_pack_stage", "k_dest_offsets", "k_fill_counts", "k_pack_bucket",
+              "k_bucket_hdr")),
     "scatter_results": (("k_scatter_results",), ("k_scatter_results",)),
 }
 
 
 def base_name(k):
+    k = k.replace("(anonymous namespace)::", "")
     k = k.split("(")[0].split("<")[0]
     return k.replace("void ", "").replace("lmr::", "").strip()
 
@@ -98,6 +100,12 @@ def main():
                 out["_per_record"][st] = out[st] * inv / (steps * rps[st])
         for st, v in out["_per_record"].items():
             print(f"stage {st:16s} {v:10.2f} B per record")
+        if "_transport_per_pack" in out and rps.get("pack"):
+            inv = sum(cnt.get(a, 0) for a in STAGES["pack"][0])
+            if cnt.get("k_pack_count") and cnt.get("k_pack_stage"):
+                inv = cnt["k_pack_count"]
+            out["_transport_per_record"] = out["_transport_per_pack"] * inv / (steps * rps["pack"])
+            print(f"transport (RCCL kernels)  {out['_transport_per_record']:10.2f} B per record packed")
     elif len(sys.argv) > 3:
         recs = float(sys.argv[3])
         out["_per_record"] = {st: v / recs for st, v in out.items() if not st.startswith("_")}
