@@ -737,7 +737,10 @@ lmr_status_t lmr_batch_exchange(lmr_ctx_t* ctx, const lmr_transport_t* tp, const
         if (ch == 0 || j * ch >= mm || rC == 0) return 0;
         const uint64_t c = std::min(ch, mm - j * ch);
         const uint64_t per = (c + uint64_t(npes) * rC - 1) / (uint64_t(npes) * rC);
-        return uint32_t(per + per / 8 + 256);
+        // 1/16 + 256 records of headroom (the regions travel whole: headroom is wire bytes); a
+        // uniform stream's slices hold ~2^17-2^20 records, whose spread is far below that, and
+        // what a skewed one puts past a slice takes the overflow round
+        return uint32_t(per + per / 16 + 256);
     };
     auto pack_chunk = [&](uint64_t j) -> lmr_status_t {
         const uint64_t lo = chunk_lo(j), cnt = chunk_hi(j) - lo;
