@@ -1,17 +1,21 @@
-// lmr_bucket.hip — the peer push's bucketed mode: the sender's pack
-// groups a chunk's records by (owner PE, owner coarse bucket) and writes them straight into the
-// owner's receive region laid out by bucket, so the owner skips its coarse pass.
+// lmr_bucket.hip — the exchange's bucketed regions: the sender's pack
+// groups a chunk's records by (owner PE, owner bucket of 256 tiles) into a region per owner laid
+// out by bucket -- a header of slice counts, then the slices -- so the owner skips its coarse pass.
+// Over the peer transport the pack writes straight into the owners' IPC-mapped receive regions;
+// over a collective transport (RCCL, host callbacks) into the send buffer, whose regions the
+// all-to-all-v moves whole.
 //
-// Today's push (lmr_exchange.hip): sender pack by owner (8 keys) -> owner stages every source's
-// region -> owner coarse pass (24 B per record) -> fine pass (22 B) -> tile sweep. Here:
+// The plain exchange: sender pack by owner (8 keys) -> owner stages every source's region -> owner
+// coarse pass (24 B per record) -> fine pass (22 B) -> tile sweep. Here:
 //   k_pack_bucket   sender, LDS rounds of 8K records ranked by (owner, bucket) -- up to
-//                   kBucketMaxKeys keys: 8 PEs x 64 buckets of 128 tiles -- each round's run of
-//                   every key reserved with one atomicAdd on the key's fill counter and written
-//                   into the owner's region at bucket b's slice [b * cap_b, (b + 1) * cap_b);
-//                   records past a slice go to the overflow list (the exchange's overflow round)
+//                   kBucketMaxKeys keys: 8 PEs x 32 buckets of 256 tiles at 2^26-element u64 shards --
+//                   each round's run of every key reserved with one atomicAdd on the key's fill
+//                   counter and written into the owner's region at bucket b's slice
+//                   [b * cap_b, (b + 1) * cap_b); records past a slice go to the overflow list (the
+//                   exchange's overflow round)
 //   k_bucket_hdr    sender, per owner: the slices' record counts into the region's header (the
 //                   first kBucketHdr bytes of the index area), the fill counters cleared, one
-//                   system-scope release (the owner reads the header after the chunk's publish)
+//                   system-scope release (a peer owner reads the header after the chunk's publish)
 //   k_fine_bucket   owner, per chunk: every source's slices of a bucket are one virtual record
 //                   stream (record-balanced block ranges, as the count-free fine pass reads its
 //                   bucket segments), ranked by tile in LDS and appended to fixed tile regions of
@@ -21,8 +25,10 @@
 //                   order-insensitive: any split is exact)
 //   k_bucket_plan   owner, at the session's sweep: one tile item per tile from the fills (and the
 //                   fills cleared), then k_tile_owner over the items
-// Only count-free ops take it (add / sub / and / or / xor and the like, nothing returned). The
-// session stays open across deferred batches like the staged one (lmr_exchange_flush sweeps it).
+//   k_bucket_direct an owner without a session workspace: the slices applied with device atomics
+// Only ops whose records commute take it (add / sub / mul / and / or / xor on integers, nothing
+// returned). The session stays open across deferred batches like the staged one
+// (lmr_exchange_flush sweeps it).
 #include "lmr_tile.hpp"
 #include "lmr_device.hpp"
 #include <algorithm>

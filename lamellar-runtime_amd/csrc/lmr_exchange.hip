@@ -22,6 +22,9 @@
 //                 each chunk's results -> lmr_scatter_results into input order.
 // Chunk j's exchange overlaps chunk j-1's staging on the apply stream; receive
 // buffers are double-buffered between the two streams.
+// Ops whose records commute (add / sub / mul / and / or / xor, nothing returned) pack bucketed
+// regions instead (lmr_bucket.hip): per owner, slices by owner bucket, sent whole, binned by the
+// owner without a coarse pass; over the peer transport the pack writes them into the owners' HBM.
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
