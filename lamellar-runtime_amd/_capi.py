@@ -76,6 +76,9 @@ class lmr_transport_t(Structure):
 
 XHDR_WORDS = 7     # LMR_XHDR_WORDS
 XHDR_SCALAR, XHDR_ORDERED = 1, 2   # LMR_XHDR_SCALAR, LMR_XHDR_ORDERED (flags word of a header row)
+# LMR_XHDR_FIXED, _DEVCOUNT, _OVERFLOW, _BUCKETS: fixed regions, device-count staging, a non-empty
+# overflow list, regions laid out by owner bucket (sent whole)
+XHDR_FIXED, XHDR_DEVCOUNT, XHDR_OVERFLOW, XHDR_BUCKETS = 4, 8, 16, 32
 
 
 # ---- AM wire format (include/lamellar_gpu_ops.h, "AM wire format")

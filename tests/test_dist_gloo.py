@@ -470,6 +470,20 @@ def test_host_transport_callbacks_gloo():
         assert pe[r]["bad_status"][0] != 0 and pe[r]["raised"][0] == 1
 
 
+def test_header_flag_constants_match_the_header(capi):
+    """Every LMR_XHDR_* define of include/lamellar_gpu_ops.h has its mirror in _capi (same value)."""
+    import re
+    from lamellar_runtime_amd import _capi
+    hdr = open(os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "include",
+                            "lamellar_gpu_ops.h")).read()
+    defs = dict(re.findall(r"#define LMR_XHDR_(\w+) (\d+)", hdr))
+    assert {"WORDS", "SCALAR", "ORDERED", "FIXED", "DEVCOUNT", "OVERFLOW", "BUCKETS"} <= set(defs)
+    for name, v in defs.items():
+        assert getattr(_capi, "XHDR_" + name) == int(v), name
+    flags = [int(v) for n, v in defs.items() if n != "WORDS"]
+    assert all(f & (f - 1) == 0 for f in flags) and len(set(flags)) == len(flags)   # distinct single bits
+
+
 def test_exchange_plan_flag_bits(capi):
     """The header's flags word: LMR_XHDR_SCALAR (1) means no values travel; LMR_XHDR_ORDERED (2)
     marks an in-order stream (one reference AM per destination) and changes no split."""
