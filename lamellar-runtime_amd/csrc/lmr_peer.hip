@@ -156,6 +156,15 @@ __global__ void k_peer_free(uint64_t* freed, uint32_t npes, uint32_t stride, uin
     __hip_atomic_store(freed + uint64_t(p) * stride, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
+// the pointer tables written from kernel arguments (no copy engine at set-up)
+struct PeerTabArgs {
+    uint8_t* p[4 * kPeerMaxPes];
+};
+__global__ void k_peer_tables(PeerTabArgs a, uint8_t** tab, uint32_t n) {
+    const uint32_t i = threadIdx.x;
+    if (i < n) tab[i] = a.p[i];
+}
+
 }  // namespace
 
 struct PeerTransport {
@@ -387,7 +396,8 @@ lmr_status_t lmr_transport_peer_create(const lmr_transport_t* base, const char* 
         PeSlot* s = &t->mb.slots[p];
         if (!host_wait([&] { return ld_acq(&s->ready) == 1; }, to) || s->region_recs != t->R) return fail(LMR_E_HIP);
     }
-    // the PEs map their regions at each other one PE at a time, in PE order
+    // the PEs map their regions at each other one PE at a time, in PE order, each through its first
+    // kernel on the tables (8 processes sharing one GPU that imported at once stalled there)
     for (uint32_t p = 0; p < t->me; p++)
         if (!host_wait([&] { return ld_acq(&t->mb.slots[p].mapped) == 1; }, to)) return fail(LMR_E_HIP);
     t->mapped.assign(size_t(t->npes) * kRegionAllocs, nullptr);
@@ -403,7 +413,6 @@ lmr_status_t lmr_transport_peer_create(const lmr_transport_t* base, const char* 
                 return fail(LMR_E_HIP);
             dst = static_cast<uint8_t*>(pp);
         }
-    st_rel(&mine->mapped, 1);
     step("peers mapped");
     // pointer tables: destination q's regions for this PE as the source, per parity
     std::vector<uint8_t*> tab(size_t(4) * t->npes);
@@ -412,10 +421,15 @@ lmr_status_t lmr_transport_peer_create(const lmr_transport_t* base, const char* 
             tab[size_t(b) * 2 * t->npes + q] = t->mapped[size_t(q) * kRegionAllocs + size_t(b) * 2];
             tab[(size_t(b) * 2 + 1) * t->npes + q] = t->mapped[size_t(q) * kRegionAllocs + size_t(b) * 2 + 1];
         }
-    if (hipMalloc(&t->d_tab, tab.size() * sizeof(uint8_t*)) != hipSuccess ||
-        hipMemcpy(t->d_tab, tab.data(), tab.size() * sizeof(uint8_t*), hipMemcpyHostToDevice) != hipSuccess)
-        return fail(LMR_E_HIP);
+    if (hipMalloc(&t->d_tab, tab.size() * sizeof(uint8_t*)) != hipSuccess) return fail(LMR_E_HIP);
+    step("table allocated");
+    PeerTabArgs ta{};
+    for (size_t i = 0; i < tab.size(); i++) ta.p[i] = tab[i];
+    hipLaunchKernelGGL(k_peer_tables, dim3(1), dim3(4 * kPeerMaxPes), 0, nullptr, ta, t->d_tab, uint32_t(tab.size()));
+    if (hipGetLastError() != hipSuccess || hipStreamSynchronize(nullptr) != hipSuccess) return fail(LMR_E_HIP);
     step("tables");
+    // the next PE maps only once this one's first kernel after its imports has completed
+    st_rel(&mine->mapped, 1);
     st_rel(&mine->opened, 1);
     for (uint32_t p = 0; p < t->npes; p++)
         if (!host_wait([&] { return ld_acq(&t->mb.slots[p].opened) == 1; }, to)) return fail(LMR_E_HIP);
